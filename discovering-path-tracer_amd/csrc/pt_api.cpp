@@ -1,0 +1,563 @@
+// pt_api.cpp — the C-ABI shim (include/pathtracer.h).
+//
+// Replaces the Vulkan resource/dispatch seam of src/Vulkan/VulkanRayTracer.cpp:
+// staging buffers + vkCmdCopyBuffer become hipMemcpyAsync, the descriptor set
+// becomes a RenderParams struct passed by value, vkCmdPushConstants +
+// vkCmdDispatch become one kernel launch, and the per-batch fence wait becomes
+// an explicit pt_synchronize / pt_read_accum.  Scene preparation that the
+// device layout needs (threading the BVH, building triangle records) happens
+// here once per upload.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/pathtracer.h"
+#include "pt_device.h"
+#include "scene/bvh.h"
+#include "scene/camera.h"
+#include "scene/light.h"
+#include "scene/obj_loader.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define PT_HIP(call)                                                                   \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) return fail(PT_ERR_HIP, std::string(#call ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+void dev_free(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+// Threads the reference node array: renumbers nodes in the order the
+// reference's DFS visits them (right child first) and records, for each, the
+// node visited after its subtree.  Fails on anything that is not a tree.
+int thread_bvh(const pt_bvh_node* nodes, size_t n, bool int_bits, size_t n_tris, std::vector<float4>* out) {
+  if (n == 0 || n > 0x7fffffffull) return fail(PT_ERR_SCENE, "BVH has no nodes or too many");
+  std::vector<int32_t> left(n), right(n);
+  for (size_t i = 0; i < n; ++i) {
+    float lw = nodes[i].min_bounds[3], rw = nodes[i].max_bounds[3];
+    int32_t l, r;
+    if (int_bits) {
+      memcpy(&l, &lw, 4);
+      memcpy(&r, &rw, 4);
+    } else {
+      // int(node.minBounds.w) (raytrace_comp.comp:173-174): only exact
+      // below 2^24, so refuse anything the float cannot hold exactly.
+      if (!(lw == floorf(lw)) || !(rw == floorf(rw)) || fabsf(lw) >= 16777216.0f || fabsf(rw) >= 16777216.0f)
+        return fail(PT_ERR_SCENE, "float-encoded BVH index is not an exact integer below 2^24 (node " +
+                                      std::to_string(i) + "); rebuild with PT_NODES_INT_BITS");
+      l = (int32_t)lw;
+      r = (int32_t)rw;
+    }
+    left[i] = l;
+    right[i] = r;
+    if (l == -1) {
+      if (r < 0 || (size_t)r >= n_tris)
+        return fail(PT_ERR_SCENE, "leaf " + std::to_string(i) + " has triangle index out of range");
+    } else if (l < 0 || (size_t)l >= n || r < 0 || (size_t)r >= n) {
+      return fail(PT_ERR_SCENE, "node " + std::to_string(i) + " has child index out of range");
+    }
+  }
+  std::vector<int32_t> order;
+  order.reserve(n);
+  std::vector<int32_t> newidx(n, -1);
+  std::vector<int32_t> stack;
+  stack.push_back(0);
+  while (!stack.empty()) {
+    const int32_t v = stack.back();
+    stack.pop_back();
+    if (newidx[v] != -1) return fail(PT_ERR_SCENE, "BVH node reachable twice (not a tree)");
+    newidx[v] = (int32_t)order.size();
+    order.push_back(v);
+    if (left[v] != -1) {
+      stack.push_back(left[v]);    // :198  push left
+      stack.push_back(right[v]);   // :199  push right -> popped first
+    }
+  }
+  const size_t m = order.size();
+  std::vector<int32_t> size(n, 1);
+  for (size_t k = m; k-- > 0;) {
+    const int32_t v = order[k];
+    if (left[v] != -1) size[v] = 1 + size[left[v]] + size[right[v]];
+  }
+  out->assign(2 * m, make_float4(0, 0, 0, 0));
+  for (size_t k = 0; k < m; ++k) {
+    const int32_t v = order[k];
+    const pt_bvh_node& nd = nodes[v];
+    const int32_t skip = (int32_t)k + size[v];
+    const int32_t tri = left[v] == -1 ? right[v] : -1;
+    float fs, ft;
+    memcpy(&fs, &skip, 4);
+    memcpy(&ft, &tri, 4);
+    (*out)[2 * k] = make_float4(nd.min_bounds[0], nd.min_bounds[1], nd.min_bounds[2], fs);
+    (*out)[2 * k + 1] = make_float4(nd.max_bounds[0], nd.max_bounds[1], nd.max_bounds[2], ft);
+  }
+  return PT_OK;
+}
+
+}  // namespace
+
+struct pt_context {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  float4* d_nodes = nullptr;
+  int n_nodes = 0;
+  float4* d_tris = nullptr;
+  int n_tris = 0;
+  ptd::LightRec* d_lights = nullptr;
+  int n_lights = 0;
+  float4* d_accum = nullptr;
+  bool own_accum = false;
+  int width = 0, height = 0;
+  unsigned long long* d_stats = nullptr;
+  float cam[16] = {0};
+  bool has_camera = false;
+  bool has_scene = false;
+  pt_params params{4, 3};
+  int nranks = 1, rank = 0;
+  bool stats_mode = false;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  bool timed = false;
+  // ring of event pairs, one per render launch since pt_reset_launch_times
+  static constexpr int kRing = 512;
+  hipEvent_t ring[kRing][2] = {};
+  int ring_n = 0;
+};
+
+struct pt_scene {
+  pt::ObjScene obj;
+  std::vector<uint32_t> bvh_indices;
+  std::vector<pt::BVHNode> nodes;
+  uint32_t flags = 0;
+};
+
+extern "C" {
+
+int pt_abi_version(void) { return PT_ABI_VERSION; }
+const char* pt_last_error(void) { return g_err.c_str(); }
+
+int pt_create(int device_ordinal, pt_context** out) {
+  if (!out) return fail(PT_ERR_INVALID, "out is null");
+  *out = nullptr;
+  int n = 0;
+  PT_HIP(hipGetDeviceCount(&n));
+  if (device_ordinal < 0 || device_ordinal >= n)
+    return fail(PT_ERR_INVALID, "device ordinal " + std::to_string(device_ordinal) + " out of range (" +
+                                    std::to_string(n) + " devices)");
+  PT_HIP(hipSetDevice(device_ordinal));
+  hipDeviceProp_t prop;
+  PT_HIP(hipGetDeviceProperties(&prop, device_ordinal));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(PT_ERR_UNSUPPORTED, std::string("built for gfx950, device is ") + prop.gcnArchName);
+  pt_context* c = new pt_context();
+  c->device = device_ordinal;
+  hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(c->d_stats, 0, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
+  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
+  for (int i = 0; i < pt_context::kRing && e == hipSuccess; ++i) {
+    e = hipEventCreate(&c->ring[i][0]);
+    if (e == hipSuccess) e = hipEventCreate(&c->ring[i][1]);
+  }
+  if (e != hipSuccess) {
+    pt_destroy(c);
+    return fail(PT_ERR_HIP, std::string("context setup: ") + hipGetErrorString(e));
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return PT_OK;
+}
+
+int pt_destroy(pt_context* c) {
+  if (!c) return PT_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  dev_free(c->d_nodes);
+  dev_free(c->d_tris);
+  dev_free(c->d_lights);
+  if (c->own_accum) dev_free(c->d_accum);
+  dev_free(c->d_stats);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  for (int i = 0; i < pt_context::kRing; ++i)
+    for (int j = 0; j < 2; ++j)
+      if (c->ring[i][j]) (void)hipEventDestroy(c->ring[i][j]);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return PT_OK;
+}
+
+int pt_set_stream(pt_context* c, void* s) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return PT_OK;
+}
+
+int pt_synchronize(pt_context* c) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  PT_HIP(hipSetDevice(c->device));
+  PT_HIP(hipStreamSynchronize(c->stream));
+  return PT_OK;
+}
+
+int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats, const uint32_t* indices,
+                    size_t n_indices, const pt_bvh_node* nodes, size_t n_nodes, const float* uvs,
+                    size_t n_uv_floats, const uint32_t* mat_indices, size_t n_mat, uint32_t flags) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  if (!vertices || !indices || !nodes) return fail(PT_ERR_INVALID, "null scene array");
+  if (n_vertex_floats % 3 || n_indices % 3 || n_indices == 0)
+    return fail(PT_ERR_SCENE, "vertex/index array sizes must be non-zero multiples of 3");
+  if (n_nodes != 2 * (n_indices / 3) - 1)
+    return fail(PT_ERR_SCENE, "expected 2T-1 = " + std::to_string(2 * (n_indices / 3) - 1) + " nodes, got " +
+                                  std::to_string(n_nodes));
+  if ((n_uv_floats && !uvs) || (n_mat && !mat_indices)) return fail(PT_ERR_INVALID, "null uv/material array");
+  if (n_indices / 3 > 0x7fffffffull) return fail(PT_ERR_UNSUPPORTED, "too many triangles");
+  const size_t nv = n_vertex_floats / 3;
+  for (size_t i = 0; i < n_indices; ++i)
+    if (indices[i] >= nv) return fail(PT_ERR_SCENE, "vertex index out of range at " + std::to_string(i));
+  std::vector<float4> threaded;
+  int rc = thread_bvh(nodes, n_nodes, (flags & PT_NODES_INT_BITS) != 0, n_indices / 3, &threaded);
+  if (rc) return rc;
+  PT_HIP(hipSetDevice(c->device));
+  PT_HIP(hipStreamSynchronize(c->stream));
+  dev_free(c->d_nodes);
+  dev_free(c->d_tris);
+  c->has_scene = false;
+  const int T = (int)(n_indices / 3);
+  float* d_v = nullptr;
+  uint32_t* d_i = nullptr;
+  PT_HIP(hipMalloc((void**)&c->d_nodes, threaded.size() * sizeof(float4)));
+  PT_HIP(hipMalloc((void**)&c->d_tris, (size_t)T * 3 * sizeof(float4)));
+  PT_HIP(hipMalloc((void**)&d_v, n_vertex_floats * sizeof(float) + 16));
+  PT_HIP(hipMalloc((void**)&d_i, n_indices * sizeof(uint32_t)));
+  PT_HIP(hipMemcpyAsync(c->d_nodes, threaded.data(), threaded.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  PT_HIP(hipMemcpyAsync(d_v, vertices, n_vertex_floats * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  PT_HIP(hipMemcpyAsync(d_i, indices, n_indices * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+  PT_HIP(ptd::launch_setup_tris(d_v, d_i, T, c->d_tris, c->stream));
+  PT_HIP(hipStreamSynchronize(c->stream));
+  (void)hipFree(d_v);
+  (void)hipFree(d_i);
+  c->n_nodes = (int)(threaded.size() / 2);
+  c->n_tris = T;
+  c->has_scene = true;
+  return PT_OK;
+}
+
+int pt_upload_lights(pt_context* c, const pt_area_light* lights, size_t n) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  if (n && !lights) return fail(PT_ERR_INVALID, "null lights");
+  if (n > 1024) return fail(PT_ERR_UNSUPPORTED, "more than 1024 lights");
+  PT_HIP(hipSetDevice(c->device));
+  PT_HIP(hipStreamSynchronize(c->stream));
+  dev_free(c->d_lights);
+  c->n_lights = 0;
+  if (n) {
+    PT_HIP(hipMalloc((void**)&c->d_lights, n * sizeof(ptd::LightRec)));
+    PT_HIP(hipMemcpyAsync(c->d_lights, lights, n * sizeof(ptd::LightRec), hipMemcpyHostToDevice, c->stream));
+    PT_HIP(hipStreamSynchronize(c->stream));
+  }
+  c->n_lights = (int)n;
+  return PT_OK;
+}
+
+int pt_set_camera(pt_context* c, const float ubo[16]) {
+  if (!c || !ubo) return fail(PT_ERR_INVALID, "null argument");
+  memcpy(c->cam, ubo, sizeof c->cam);
+  c->has_camera = true;
+  return PT_OK;
+}
+
+int pt_set_params(pt_context* c, const pt_params* p) {
+  if (!c || !p) return fail(PT_ERR_INVALID, "null argument");
+  if (p->max_depth < 0 || p->max_depth > 64 || p->sss_bounces < 0 || p->sss_bounces > 64)
+    return fail(PT_ERR_INVALID, "max_depth and sss_bounces must be in [0,64]");
+  c->params = *p;
+  return PT_OK;
+}
+
+int pt_set_partition(pt_context* c, int nranks, int rank) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(PT_ERR_INVALID, "bad partition");
+  c->nranks = nranks;
+  c->rank = rank;
+  return PT_OK;
+}
+
+int pt_clear_accum(pt_context* c) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
+  PT_HIP(hipSetDevice(c->device));
+  PT_HIP(ptd::launch_clear(c->d_accum, c->width, c->height, c->nranks, c->rank, c->stream));
+  return PT_OK;
+}
+
+int pt_resize_and_clear(pt_context* c, int w, int h) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  if (w <= 0 || h <= 0 || (long long)w * h > (1ll << 31)) return fail(PT_ERR_INVALID, "bad resolution");
+  PT_HIP(hipSetDevice(c->device));
+  if (!(c->own_accum && c->width == w && c->height == h)) {
+    PT_HIP(hipStreamSynchronize(c->stream));
+    if (c->own_accum) dev_free(c->d_accum);
+    c->d_accum = nullptr;
+    c->own_accum = false;
+    PT_HIP(hipMalloc((void**)&c->d_accum, (size_t)w * h * sizeof(float4)));
+    c->own_accum = true;
+    c->width = w;
+    c->height = h;
+  }
+  return pt_clear_accum(c);
+}
+
+int pt_bind_accum(pt_context* c, void* ptr, int w, int h) {
+  if (!c || !ptr) return fail(PT_ERR_INVALID, "null argument");
+  if (w <= 0 || h <= 0) return fail(PT_ERR_INVALID, "bad resolution");
+  if (((uintptr_t)ptr) & 15) return fail(PT_ERR_INVALID, "accumulation buffer must be 16-B aligned");
+  PT_HIP(hipSetDevice(c->device));
+  PT_HIP(hipStreamSynchronize(c->stream));
+  if (c->own_accum) dev_free(c->d_accum);
+  c->d_accum = (float4*)ptr;
+  c->own_accum = false;
+  c->width = w;
+  c->height = h;
+  return PT_OK;
+}
+
+void* pt_accum_device_ptr(pt_context* c) { return c ? (void*)c->d_accum : nullptr; }
+
+int pt_read_accum(pt_context* c, float* rgba, size_t n) {
+  if (!c || !rgba) return fail(PT_ERR_INVALID, "null argument");
+  if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
+  const size_t need = (size_t)c->width * c->height * 4;
+  if (n < need) return fail(PT_ERR_INVALID, "output buffer too small: need " + std::to_string(need) + " floats");
+  PT_HIP(hipSetDevice(c->device));
+  PT_HIP(hipMemcpyAsync(rgba, c->d_accum, need * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  PT_HIP(hipStreamSynchronize(c->stream));
+  return PT_OK;
+}
+
+int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  if (!c->has_scene) return fail(PT_ERR_INVALID, "no scene uploaded");
+  if (!c->has_camera) return fail(PT_ERR_INVALID, "no camera set");
+  if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
+  ptd::RenderParams p;
+  p.nodes = c->d_nodes;
+  p.tris = c->d_tris;
+  p.lights = c->d_lights;
+  p.accum = c->d_accum;
+  p.stats = c->d_stats;
+  p.n_nodes = c->n_nodes;
+  p.n_lights = c->n_lights;
+  p.width = c->width;
+  p.height = c->height;
+  p.first_batch = first_batch;
+  p.n_batches = n_batches;
+  p.max_depth = c->params.max_depth;
+  p.sss_bounces = c->params.sss_bounces;
+  for (int i = 0; i < 3; ++i) {
+    p.cam_pos[i] = c->cam[i];
+    p.cam_dir[i] = c->cam[4 + i];
+    p.cam_up[i] = c->cam[8 + i];
+  }
+  p.fov = c->cam[12];
+  p.blocks_x = (c->width + 15) / 16;
+  p.blocks_total = p.blocks_x * ((c->height + 15) / 16);
+  p.nranks = c->nranks;
+  p.rank = c->rank;
+  PT_HIP(hipSetDevice(c->device));
+  const int slot = c->ring_n % pt_context::kRing;
+  PT_HIP(hipEventRecord(c->ev0, c->stream));
+  PT_HIP(hipEventRecord(c->ring[slot][0], c->stream));
+  PT_HIP(ptd::launch_render(p, c->stats_mode, c->stream));
+  PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
+  PT_HIP(hipEventRecord(c->ev1, c->stream));
+  c->ring_n++;
+  c->timed = true;
+  return PT_OK;
+}
+
+int pt_dispatch(pt_context* c, uint32_t sample_batch) { return pt_render(c, sample_batch, 1); }
+
+int pt_set_stats_mode(pt_context* c, int enabled) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  c->stats_mode = enabled != 0;
+  return PT_OK;
+}
+
+int pt_get_stats(pt_context* c, pt_stats* out) {
+  if (!c || !out) return fail(PT_ERR_INVALID, "null argument");
+  unsigned long long h[4];
+  PT_HIP(hipSetDevice(c->device));
+  PT_HIP(hipMemcpyAsync(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  PT_HIP(hipStreamSynchronize(c->stream));
+  out->rays = h[0];
+  out->nodes = h[1];
+  out->leaf_tests = h[2];
+  out->samples = h[3];
+  return PT_OK;
+}
+
+int pt_reset_stats(pt_context* c) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  PT_HIP(hipSetDevice(c->device));
+  PT_HIP(hipMemsetAsync(c->d_stats, 0, 4 * sizeof(unsigned long long), c->stream));
+  return PT_OK;
+}
+
+int pt_last_launch_ms(pt_context* c, float* ms) {
+  if (!c || !ms) return fail(PT_ERR_INVALID, "null argument");
+  if (!c->timed) return fail(PT_ERR_INVALID, "no launch recorded");
+  PT_HIP(hipEventSynchronize(c->ev1));
+  PT_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  return PT_OK;
+}
+
+int pt_launch_times_ms(pt_context* c, float* out, size_t max_n, size_t* n_out) {
+  if (!c || !n_out) return fail(PT_ERR_INVALID, "null argument");
+  const int have = c->ring_n < pt_context::kRing ? c->ring_n : pt_context::kRing;
+  const int first = c->ring_n - have;
+  size_t n = 0;
+  PT_HIP(hipSetDevice(c->device));
+  for (int k = first; k < c->ring_n && n < max_n; ++k) {
+    const int slot = k % pt_context::kRing;
+    PT_HIP(hipEventSynchronize(c->ring[slot][1]));
+    if (out) PT_HIP(hipEventElapsedTime(&out[n], c->ring[slot][0], c->ring[slot][1]));
+    ++n;
+  }
+  *n_out = n;
+  return PT_OK;
+}
+
+int pt_reset_launch_times(pt_context* c) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  c->ring_n = 0;
+  return PT_OK;
+}
+
+// ---------------------------------------------------------------- scene ----
+
+int pt_scene_load_obj(const char* path, pt_scene** out) {
+  if (!path || !out) return fail(PT_ERR_INVALID, "null argument");
+  pt_scene* s = new pt_scene();
+  std::string err;
+  if (pt::load_obj_file(path, &s->obj, &err) != 0) {
+    delete s;
+    return fail(PT_ERR_IO, err);
+  }
+  *out = s;
+  return PT_OK;
+}
+
+int pt_scene_parse_obj(const char* text, size_t len, pt_scene** out) {
+  if (!text || !out) return fail(PT_ERR_INVALID, "null argument");
+  pt_scene* s = new pt_scene();
+  std::string err;
+  if (pt::parse_obj(text, len, &s->obj, &err) != 0) {
+    delete s;
+    return fail(PT_ERR_IO, err);
+  }
+  *out = s;
+  return PT_OK;
+}
+
+int pt_scene_from_arrays(const float* v, size_t nvf, const uint32_t* idx, size_t ni, pt_scene** out) {
+  if (!out || (nvf && !v) || (ni && !idx)) return fail(PT_ERR_INVALID, "null argument");
+  if (nvf % 3 || ni % 3) return fail(PT_ERR_SCENE, "sizes must be multiples of 3");
+  pt_scene* s = new pt_scene();
+  s->obj.vertices.assign(v, v + nvf);
+  s->obj.indices.assign(idx, idx + ni);
+  s->obj.materialIds.assign(ni / 3, 0u);
+  *out = s;
+  return PT_OK;
+}
+
+int pt_scene_build_bvh(pt_scene* s, uint32_t flags, int threads) {
+  if (!s) return fail(PT_ERR_INVALID, "null scene");
+  const size_t ni = s->obj.indices.size();
+  if (ni == 0 || ni % 3) return fail(PT_ERR_SCENE, "scene has no triangles");
+  pt::BVHOptions o;
+  o.encoding = (flags & PT_NODES_INT_BITS) ? pt::BVHEncoding::kIntBits : pt::BVHEncoding::kFloat;
+  o.threads = threads;
+  s->bvh_indices.assign(ni, 0);
+  s->nodes.assign(2 * (ni / 3) - 1, pt::BVHNode{});
+  std::string err;
+  if (pt::build_bvh(s->obj.vertices.data(), s->obj.vertices.size(), s->obj.indices.data(), ni,
+                    s->bvh_indices.data(), s->nodes.data(), o, &err) != 0) {
+    s->bvh_indices.clear();
+    s->nodes.clear();
+    return fail(PT_ERR_SCENE, err);
+  }
+  s->flags = flags;
+  return PT_OK;
+}
+
+int pt_scene_counts(const pt_scene* s, size_t* nvf, size_t* ni, size_t* nn, size_t* nuv, size_t* nmat) {
+  if (!s) return fail(PT_ERR_INVALID, "null scene");
+  if (nvf) *nvf = s->obj.vertices.size();
+  if (ni) *ni = s->obj.indices.size();
+  if (nn) *nn = s->nodes.size();
+  if (nuv) *nuv = s->obj.texcoords.size();
+  if (nmat) *nmat = s->obj.materialIds.size();
+  return PT_OK;
+}
+
+int pt_scene_copy(const pt_scene* s, float* v, uint32_t* idx, pt_bvh_node* nodes, float* uvs, uint32_t* mat) {
+  if (!s) return fail(PT_ERR_INVALID, "null scene");
+  if (v) memcpy(v, s->obj.vertices.data(), s->obj.vertices.size() * 4);
+  if (idx) {
+    const auto& src = s->nodes.empty() ? s->obj.indices : s->bvh_indices;   // BVH order once built
+    memcpy(idx, src.data(), src.size() * 4);
+  }
+  if (nodes) memcpy(nodes, s->nodes.data(), s->nodes.size() * sizeof(pt_bvh_node));
+  if (uvs) memcpy(uvs, s->obj.texcoords.data(), s->obj.texcoords.size() * 4);
+  if (mat) memcpy(mat, s->obj.materialIds.data(), s->obj.materialIds.size() * 4);
+  return PT_OK;
+}
+
+int pt_scene_upload(pt_context* c, const pt_scene* s) {
+  if (!c || !s) return fail(PT_ERR_INVALID, "null argument");
+  if (s->nodes.empty()) return fail(PT_ERR_INVALID, "build the BVH first (pt_scene_build_bvh)");
+  return pt_upload_scene(c, s->obj.vertices.data(), s->obj.vertices.size(), s->bvh_indices.data(),
+                         s->bvh_indices.size(), (const pt_bvh_node*)s->nodes.data(), s->nodes.size(),
+                         s->obj.texcoords.data(), s->obj.texcoords.size(), s->obj.materialIds.data(),
+                         s->obj.materialIds.size(), s->flags);
+}
+
+int pt_scene_free(pt_scene* s) {
+  delete s;
+  return PT_OK;
+}
+
+int pt_pack_light(const float pos[3], const float nrm[3], const float inten[3], const float size[2],
+                  pt_area_light* out) {
+  if (!pos || !nrm || !inten || !size || !out) return fail(PT_ERR_INVALID, "null argument");
+  pt::Light l({{pos[0], pos[1], pos[2]}}, {{nrm[0], nrm[1], nrm[2]}}, {{inten[0], inten[1], inten[2]}},
+              {{size[0], size[1]}});
+  memcpy(out, &l.getLights()[0], sizeof *out);
+  return PT_OK;
+}
+
+int pt_default_camera(float ubo[16]) {
+  if (!ubo) return fail(PT_ERR_INVALID, "null argument");
+  pt::Camera cam;
+  cam.toUBO(ubo);
+  return PT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,51 @@
+// Device-side data layout and kernel launchers (host-visible declarations).
+//
+// HBM layout (all 16-B aligned, built once per scene upload):
+//   nodes : 2 x float4 per BVH node, renumbered in the reference traversal's
+//           visiting order (right child first, raytrace_comp.comp:198-199):
+//             [0] = {min.x, min.y, min.z, skip}     skip = int bits
+//             [1] = {max.x, max.y, max.z, tri}      tri  = int bits, -1 internal
+//           An internal node whose box is hit continues at k+1 (its right
+//           child); a missed node or a leaf continues at `skip`, the node the
+//           reference's stack would pop next.  Same visit sequence, no stack.
+//   tris  : 3 x float4 per triangle slot (slot = the reference's triIdx, the
+//           row of the BVH-reordered index buffer):
+//             {v0.xyz, e1.x} {e1.yz, e2.xy} {e2.z, n.xyz}
+//           e1 = v1-v0, e2 = v2-v0 and n = normalize(cross(e1,e2)) are exactly
+//           the values the reference recomputes per test (:119-120, :189).
+//   accum : float4[H][W], RGBA32F running mean.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ptd {
+
+struct LightRec {          // == pt_area_light / AreaLightData
+  float position[4];
+  float normal[4];
+  float intensity[4];
+  float size[4];
+};
+
+struct RenderParams {
+  const float4* nodes;
+  const float4* tris;
+  const LightRec* lights;
+  float4* accum;
+  unsigned long long* stats;   // rays, nodes, leaf tests, samples (stats mode only)
+  int n_nodes;
+  int n_lights;
+  int width, height;
+  uint32_t first_batch, n_batches;
+  int max_depth, sss_bounces;
+  float cam_pos[3], cam_dir[3], cam_up[3], fov;
+  int blocks_x, blocks_total;   // 16x16-pixel blocks
+  int nranks, rank;             // block b is rendered iff b % nranks == rank
+};
+
+hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices, int n_tris, float4* d_tris,
+                             hipStream_t stream);
+hipError_t launch_clear(float4* accum, int width, int height, int nranks, int rank, hipStream_t stream);
+hipError_t launch_render(const RenderParams& p, bool stats, hipStream_t stream);
+
+}  // namespace ptd

@@ -1,0 +1,427 @@
+// pt_device.hip — the CDNA4 path-tracing kernels.
+//
+// One thread per pixel, one 64-lane wave per 8x8 pixel tile, four waves per
+// 256-thread workgroup covering a 16x16 block (the reference's workgroup
+// footprint, raytrace_comp.comp:43).  Each thread runs n_batches consecutive
+// samples of its pixel and folds them into the running mean in registers, so
+// the accumulation buffer is read and written once per launch instead of once
+// per sample; the op sequence per sample is identical to n separate 1-spp
+// dispatches (raytrace_comp.comp:467-469).
+//
+// Traversal (raytrace_comp.comp:159-204) is the reference's exhaustive DFS,
+// executed stack-free over the threaded layout documented in pt_device.h: the
+// node visit sequence, the AABB tests and the strict '<' tie-break are the
+// reference's, so hits are bit-identical.  Two exact shortcuts:
+//   * shadow rays only need "is there a hit closer than the light"
+//     (:359, :398) — any accepted triangle with t < 1e30 and !(t >= limit)
+//     settles it, so traversal stops there;
+//   * the light pre-pass (:319-320) traces exactly the depth-0 ray (:333), so
+//     that closest hit is computed once and used for both.
+// In stats mode neither shortcut is taken and every reference traceRay call
+// is counted with its exhaustive node/leaf counts.
+//
+// Numerics: every float op is the reference's, in its order, via pt_math.h;
+// the file is compiled with -ffp-contract=off and correctly rounded div/sqrt.
+#include "pt_device.h"
+#include "pt_math.h"
+
+#pragma clang fp contract(off)
+
+namespace ptd {
+using namespace ptm;
+
+namespace {
+
+struct Ctr {
+  uint32_t rays, nodes, leaves;
+};
+
+struct Hit {
+  float t;
+  int tri;   // -1 = miss
+};
+
+// intersectAABB (:102-112) with invDir hoisted (same value every node).
+__device__ __forceinline__ bool slab(v3 o, v3 inv, float4 a, float4 b) {
+  const float t0x = (a.x - o.x) * inv.x, t0y = (a.y - o.y) * inv.y, t0z = (a.z - o.z) * inv.z;
+  const float t1x = (b.x - o.x) * inv.x, t1y = (b.y - o.y) * inv.y, t1z = (b.z - o.z) * inv.z;
+  const float tmin = fmax_(fmax_(fmin_(t0x, t1x), fmin_(t0y, t1y)), fmin_(t0z, t1z));
+  const float tmax = fmin_(fmin_(fmax_(t0x, t1x), fmax_(t0y, t1y)), fmax_(t0z, t1z));
+  return tmin <= tmax && tmax >= 0.0f;
+}
+
+// intersectTriangle (:114-157), edges precomputed; UV tail is dead code.
+__device__ __forceinline__ bool tri_test(v3 o, v3 d, float4 A, float4 B, float4 C, float* tout) {
+  const float EPS = 0.000001f;
+  const v3 v0 = mk(A.x, A.y, A.z);
+  const v3 e1 = mk(A.w, B.x, B.y);
+  const v3 e2 = mk(B.z, B.w, C.x);
+  const v3 p = cross(d, e2);
+  const float det = dot(e1, p);
+  if (fabs_(det) < EPS) return false;
+  const float inv = 1.0f / det;
+  const v3 s = sub(o, v0);
+  const float u = inv * dot(s, p);
+  if (u < 0.0f || u > 1.0f) return false;
+  const v3 q = cross(s, e1);
+  const float v = inv * dot(d, q);
+  if (v < 0.0f || u + v > 1.0f) return false;
+  const float t = inv * dot(e2, q);
+  if (t <= EPS) return false;
+  *tout = t;
+  return true;
+}
+
+template <bool STATS>
+__device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c) {
+  const v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  float best = 1e30f;
+  int bt = -1;
+  if (STATS) c.rays++;
+  int k = 0;
+  const int n = P.n_nodes;
+  while (k < n) {
+    const float4 a = P.nodes[2 * k];
+    const float4 b = P.nodes[2 * k + 1];
+    if (STATS) c.nodes++;
+    const bool h = slab(o, inv, a, b);
+    const int tri = __float_as_int(b.w);
+    if (h && tri >= 0) {
+      if (STATS) c.leaves++;
+      const float4* T = P.tris + 3 * tri;
+      float t;
+      if (tri_test(o, d, T[0], T[1], T[2], &t) && t < best) {
+        best = t;
+        bt = tri;
+      }
+    }
+    k = (h && tri < 0) ? k + 1 : __float_as_int(a.w);
+  }
+  Hit r;
+  r.t = best;
+  r.tri = bt;
+  return r;
+}
+
+// Shadow query for "!hit || hit.t >= limit" (:359, :398): true iff some
+// triangle the reference would accept (t < 1e30) has !(t >= limit).
+template <bool STATS>
+__device__ bool occluded(const RenderParams& P, v3 o, v3 d, float limit, Ctr& c) {
+  const v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  bool occ = false;
+  if (STATS) c.rays++;
+  int k = 0;
+  const int n = P.n_nodes;
+  while (k < n) {
+    const float4 a = P.nodes[2 * k];
+    const float4 b = P.nodes[2 * k + 1];
+    if (STATS) c.nodes++;
+    const bool h = slab(o, inv, a, b);
+    const int tri = __float_as_int(b.w);
+    if (h && tri >= 0) {
+      if (STATS) c.leaves++;
+      const float4* T = P.tris + 3 * tri;
+      float t;
+      if (tri_test(o, d, T[0], T[1], T[2], &t) && t < 1e30f && !(t >= limit)) {
+        occ = true;
+        if (!STATS) return true;
+      }
+    }
+    k = (h && tri < 0) ? k + 1 : __float_as_int(a.w);
+  }
+  return occ;
+}
+
+__device__ __forceinline__ void light_frame(const LightRec& L, v3* right, v3* up) {
+  const v3 n = normalize(mk(L.normal[0], L.normal[1], L.normal[2]));
+  const v3 basis = fabs_(n.y) < 0.999f ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+  *right = normalize(cross(n, basis));
+  *up = cross(*right, n);
+}
+
+// sampleAreaLight (:255-268)
+__device__ __forceinline__ v3 sample_area_light(const LightRec& L, uint32_t* rng) {
+  const float u = rng_next(rng) * 2.0f - 1.0f;
+  const float v = rng_next(rng) * 2.0f - 1.0f;
+  v3 right, up;
+  light_frame(L, &right, &up);
+  const v3 pos = mk(L.position[0], L.position[1], L.position[2]);
+  return add(add(pos, muls(muls(muls(right, u), L.size[0]), 0.5f)), muls(muls(muls(up, v), L.size[1]), 0.5f));
+}
+
+// intersectAreaLight (:271-298)
+__device__ __forceinline__ bool intersect_area_light(v3 o, v3 d, const LightRec& L, float* t) {
+  const v3 n_raw = mk(L.normal[0], L.normal[1], L.normal[2]);
+  const v3 pos = mk(L.position[0], L.position[1], L.position[2]);
+  const float denom = dot(n_raw, d);
+  if (fabs_(denom) < 0.0001f) return false;
+  const float tt = dot(n_raw, sub(pos, o)) / denom;
+  *t = tt;
+  if (tt <= 0.0f) return false;
+  const v3 hp = add(o, muls(d, tt));
+  v3 right, up;
+  light_frame(L, &right, &up);
+  const v3 th = sub(hp, pos);
+  const float u = dot(th, right);
+  const float v = dot(th, up);
+  return fabs_(u) <= L.size[0] * 0.5f && fabs_(v) <= L.size[1] * 0.5f;
+}
+
+// sampleSphere (:246-253)
+__device__ __forceinline__ v3 sample_sphere(uint32_t* rng) {
+  const float z = 2.0f * rng_next(rng) - 1.0f;
+  const float th = (2.0f * 0x1.921fb6p+1f) * rng_next(rng);
+  const float r = sqrt_(1.0f - z * z);
+  return mk(r * cos_(th), r * sin_(th), z);
+}
+
+// sampleHemisphere (:229-243)
+__device__ __forceinline__ v3 sample_hemisphere(v3 n, uint32_t* rng) {
+  const float r1 = rng_next(rng);
+  const float r2 = rng_next(rng);
+  const float th = acos_(sqrt_(1.0f - r1));
+  const float ph = (2.0f * 0x1.921fb6p+1f) * r2;
+  const float st = sin_(th);
+  const v3 l = mk(st * cos_(ph), st * sin_(ph), cos_(th));
+  const v3 upv = fabs_(n.z) < 0.999f ? mk(0.0f, 0.0f, 1.0f) : mk(1.0f, 0.0f, 0.0f);
+  const v3 t = normalize(cross(upv, n));
+  const v3 b = cross(n, t);
+  return add(add(muls(t, l.x), muls(b, l.y)), muls(n, l.z));
+}
+
+__device__ __forceinline__ v3 tri_normal(const RenderParams& P, int tri) {
+  const float4 C = P.tris[3 * tri + 2];
+  return mk(C.y, C.z, C.w);
+}
+
+__device__ __forceinline__ void add_ctr(Ctr& a, const Ctr& b) {
+  a.rays += b.rays;
+  a.nodes += b.nodes;
+  a.leaves += b.leaves;
+}
+
+// pathTrace (:300-418)
+template <bool STATS>
+__device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr& c) {
+  const float OFFSET = 0.001f;
+  v3 thr = mk(1.0f, 1.0f, 1.0f);
+  v3 rad = mk(0.0f, 0.0f, 0.0f);
+  uint32_t rng = seed;                                  // :307 re-seed
+
+  Hit h0;
+  h0.t = 1e30f;
+  h0.tri = -1;
+  bool have_h0 = false;
+  Ctr c0 = {0u, 0u, 0u};
+  for (int i = 0; i < P.n_lights; ++i) {                // :311-328
+    const LightRec L = P.lights[i];
+    float tl;
+    if (intersect_area_light(ro, rd, L, &tl)) {
+      if (!have_h0) {
+        h0 = trace_closest<STATS>(P, ro, rd, c0);
+        have_h0 = true;
+      }
+      if (STATS) add_ctr(c, c0);
+      if (h0.tri < 0 || h0.t > tl) return mk(L.intensity[0], L.intensity[1], L.intensity[2]);
+    }
+  }
+
+  for (int depth = 0; depth < P.max_depth; ++depth) {   // :331
+    Hit h;
+    if (depth == 0) {
+      if (!have_h0) {
+        h0 = trace_closest<STATS>(P, ro, rd, c0);
+        have_h0 = true;
+      }
+      if (STATS) add_ctr(c, c0);
+      h = h0;
+    } else {
+      h = trace_closest<STATS>(P, ro, rd, c);
+    }
+    if (h.tri < 0) {
+      rad = add(rad, mul(thr, mk(0.0f, 0.0f, 0.0f)));  // background (:336)
+      break;
+    }
+    const v3 hp = add(ro, muls(rd, h.t));               // :188
+    const v3 hn = tri_normal(P, h.tri);                 // :189
+
+    const v3 albedo = mk(0.8f, 0.8f, 0.8f);
+    v3 direct = mk(0.0f, 0.0f, 0.0f);
+    for (int i = 0; i < P.n_lights; ++i) {              // :345-366
+      const LightRec L = P.lights[i];
+      const v3 lp = sample_area_light(L, &rng);
+      const v3 ld = normalize(sub(lp, hp));
+      const float diff = fmax_(dot(hn, ld), 0.0f);
+      const float dist = length(sub(lp, hp));
+      if (!occluded<STATS>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c)) {
+        const float d2 = dist * dist;
+        const v3 contrib = muls(muls(mk(L.intensity[0], L.intensity[1], L.intensity[2]), diff), 1.0f / fmax_(d2, 0.01f));
+        direct = add(direct, mul(albedo, contrib));
+      }
+    }
+    rad = add(rad, mul(thr, direct));
+
+    const v3 sss_albedo = mk(1.0f, 0.2f, 0.1f);         // :371-408
+    const float sss_radius = 1.0f;
+    v3 sss_thr = mk(1.0f, 1.0f, 1.0f);
+    v3 so = sub(hp, muls(hn, OFFSET));
+    v3 sd = sample_sphere(&rng);
+    for (int k = 0; k < P.sss_bounces; ++k) {
+      const Hit sh = trace_closest<STATS>(P, so, sd, c);
+      if (sh.tri < 0) break;
+      const float travel = sh.t;
+      const v3 cp = add(so, muls(sd, travel));
+      const v3 sn = tri_normal(P, sh.tri);
+      v3 sl = mk(0.0f, 0.0f, 0.0f);
+      for (int i = 0; i < P.n_lights; ++i) {
+        const LightRec L = P.lights[i];
+        const v3 lp = sample_area_light(L, &rng);
+        const v3 ed = normalize(sub(lp, cp));
+        const float ediff = fmax_(dot(sn, ed), 0.0f);
+        const float edist = length(sub(lp, cp));
+        if (!occluded<STATS>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c)) {
+          const float d2 = edist * edist;
+          sl = add(sl, muls(mul(muls(sss_albedo, ediff), mk(L.intensity[0], L.intensity[1], L.intensity[2])),
+                            1.0f / fmax_(d2, 0.01f)));
+        }
+      }
+      rad = add(rad, muls(mul(mul(thr, sss_thr), sl), 1.0f + sss_radius * 0.5f));
+      sss_thr = mul(sss_thr, muls(sss_albedo, exp_(-travel / (sss_radius * 1.5f))));
+      so = sub(cp, muls(sn, OFFSET));
+      sd = sample_sphere(&rng);
+    }
+
+    const v3 bd = sample_hemisphere(hn, &rng);          // :411-414
+    thr = mul(thr, muls(albedo, dot(hn, bd)));
+    ro = add(hp, muls(hn, OFFSET));
+    rd = bd;
+  }
+  return rad;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
+  const int blk = (int)blockIdx.x * P.nranks + P.rank;
+  const int tid = (int)threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int bx = blk % P.blocks_x, by = blk / P.blocks_x;
+  const int px = bx * 16 + (wave & 1) * 8 + (lane & 7);
+  const int py = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+  const bool active = blk < P.blocks_total && px < P.width && py < P.height;   // :425-428
+  Ctr c = {0u, 0u, 0u};
+  if (active) {
+    const int W = P.width, H = P.height;
+    const v3 cpos = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+    const v3 cdir = mk(P.cam_dir[0], P.cam_dir[1], P.cam_dir[2]);
+    const v3 cup = mk(P.cam_up[0], P.cam_up[1], P.cam_up[2]);
+    // Per-pixel constants of main() (:430-432, :446-447, :457), hoisted out
+    // of the sample loop — same values every sample.
+    const float ndcX0 = (2.0f * (float)px / (float)W) - 1.0f;
+    const float ndcY0 = (2.0f * (float)py / (float)H) - 1.0f;
+    const float aspect = (float)W / (float)H;
+    const v3 right = normalize(cross(cdir, neg(cup)));
+    const v3 up = normalize(cross(right, cdir));
+    const float tanFov = tan_(radians_(P.fov * 0.5f));
+    const size_t pix = (size_t)py * (size_t)W + (size_t)px;
+    float4 acc = P.accum[pix];
+    for (uint32_t s = 0; s < P.n_batches; ++s) {
+      const uint32_t batch = P.first_batch + s;
+      const uint32_t seed = (batch * (uint32_t)H + (uint32_t)py) * (uint32_t)W + (uint32_t)px;   // :435
+      uint32_t rng = seed;
+      // randomGaussian x2 (:218-226, :445, :451)
+      float u1 = fmax_(1e-38f, rng_next(&rng));
+      float u2 = rng_next(&rng);
+      float r = sqrt_(-2.0f * log_(u1));
+      float th = (2.0f * 0x1.921fb6p+1f) * u2;
+      const float ax = (r * cos_(th)) * 0.02f;
+      const float ay = (r * sin_(th)) * 0.02f;
+      const v3 origin = add(add(cpos, muls(right, ax)), muls(up, ay));   // :448
+      u1 = fmax_(1e-38f, rng_next(&rng));
+      u2 = rng_next(&rng);
+      r = sqrt_(-2.0f * log_(u1));
+      th = (2.0f * 0x1.921fb6p+1f) * u2;
+      const float jx = r * cos_(th), jy = r * sin_(th);
+      const float ndcX = ndcX0 + (jx * 0.5f) / (float)W;                 // :453-454
+      const float ndcY = ndcY0 + (jy * 0.5f) / (float)H;
+      const v3 base = normalize(sub(add(cdir, muls(neg(right), (ndcX * tanFov) * aspect)), muls(up, ndcY * tanFov)));
+      const v3 focal = add(cpos, muls(base, 3.0f));                       // :459
+      const v3 dir = normalize(sub(focal, origin));                       // :460
+      const v3 col = path_trace<STATS>(P, origin, dir, seed, c);
+      const float fb = (float)batch, fb1 = (float)(batch + 1u);           // :468
+      acc.x = (acc.x * fb + col.x) / fb1;
+      acc.y = (acc.y * fb + col.y) / fb1;
+      acc.z = (acc.z * fb + col.z) / fb1;
+      acc.w = (acc.w * fb + 1.0f) / fb1;
+    }
+    P.accum[pix] = acc;
+  }
+  if (STATS) {
+    const unsigned long long rays = wave_sum(c.rays), nodes = wave_sum(c.nodes), leaves = wave_sum(c.leaves);
+    const unsigned long long smp = wave_sum(active ? (unsigned long long)P.n_batches : 0ull);
+    if (lane == 0) {
+      atomicAdd(&P.stats[0], rays);
+      atomicAdd(&P.stats[1], nodes);
+      atomicAdd(&P.stats[2], leaves);
+      atomicAdd(&P.stats[3], smp);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void setup_tris_kernel(const float* __restrict__ V, const uint32_t* __restrict__ I,
+                                                         int n_tris, float4* __restrict__ out) {
+  const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (t >= n_tris) return;
+  const uint32_t i0 = I[3 * t + 0] * 3u, i1 = I[3 * t + 1] * 3u, i2 = I[3 * t + 2] * 3u;
+  const v3 v0 = mk(V[i0], V[i0 + 1], V[i0 + 2]);
+  const v3 v1 = mk(V[i1], V[i1 + 1], V[i1 + 2]);
+  const v3 v2 = mk(V[i2], V[i2 + 1], V[i2 + 2]);
+  const v3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+  const v3 n = normalize(cross(e1, e2));
+  out[3 * t + 0] = make_float4(v0.x, v0.y, v0.z, e1.x);
+  out[3 * t + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+  out[3 * t + 2] = make_float4(e2.z, n.x, n.y, n.z);
+}
+
+__global__ __launch_bounds__(256) void clear_kernel(float4* accum, int W, int H, int nranks, int rank) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (size_t)W * (size_t)H) return;
+  const int x = (int)(i % (size_t)W), y = (int)(i / (size_t)W);
+  const int blocks_x = (W + 15) / 16;
+  const int b = (y / 16) * blocks_x + x / 16;
+  const float z = (b % nranks == rank) ? 0.0f : -0.0f;
+  accum[i] = make_float4(z, z, z, z);
+}
+
+}  // namespace
+
+hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices, int n_tris, float4* d_tris,
+                             hipStream_t stream) {
+  if (n_tris <= 0) return hipSuccess;
+  setup_tris_kernel<<<(n_tris + 255) / 256, 256, 0, stream>>>(d_vertices, d_indices, n_tris, d_tris);
+  return hipGetLastError();
+}
+
+hipError_t launch_clear(float4* accum, int width, int height, int nranks, int rank, hipStream_t stream) {
+  const size_t n = (size_t)width * (size_t)height;
+  if (n == 0) return hipSuccess;
+  clear_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(accum, width, height, nranks, rank);
+  return hipGetLastError();
+}
+
+hipError_t launch_render(const RenderParams& p, bool stats, hipStream_t stream) {
+  const int grid = (p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;   // blocks b = rank + i*nranks
+  if (grid <= 0 || p.n_batches == 0) return hipSuccess;
+  if (stats)
+    render_kernel<true><<<grid, 256, 0, stream>>>(p);
+  else
+    render_kernel<false><<<grid, 256, 0, stream>>>(p);
+  return hipGetLastError();
+}
+
+}  // namespace ptd

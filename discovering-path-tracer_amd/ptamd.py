@@ -1,0 +1,278 @@
+"""ptamd — Python binding of the MI355X path tracer's C ABI (include/pathtracer.h).
+
+A thin ctypes layer over libptamd.so, mirroring the reference's host-side
+objects: Scene (OBJ ingest + BVH, src/BoundingVolumeHierarchy.h), pack_light
+(src/Light.cpp), default_camera (src/Camera.cpp) and Renderer — the
+replacement for VulkanRayTracer's upload/dispatch/readback
+(src/Vulkan/VulkanRayTracer.cpp).  There is no fallback: if the library is
+missing or the GPU is absent, calls raise.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libptamd.so")
+
+PT_OK = 0
+PT_NODES_INT_BITS = 0x1
+
+# Every symbol include/pathtracer.h declares (tests check the .so exports them).
+EXPORTS = [
+    "pt_abi_version", "pt_last_error", "pt_create", "pt_destroy", "pt_set_stream", "pt_synchronize",
+    "pt_upload_scene", "pt_upload_lights", "pt_set_camera", "pt_set_params", "pt_resize_and_clear",
+    "pt_bind_accum", "pt_clear_accum", "pt_accum_device_ptr", "pt_read_accum", "pt_dispatch", "pt_render",
+    "pt_set_partition", "pt_set_stats_mode", "pt_get_stats", "pt_reset_stats", "pt_last_launch_ms",
+    "pt_launch_times_ms", "pt_reset_launch_times",
+    "pt_scene_load_obj", "pt_scene_parse_obj", "pt_scene_from_arrays", "pt_scene_build_bvh",
+    "pt_scene_counts", "pt_scene_copy", "pt_scene_upload", "pt_scene_free", "pt_pack_light",
+    "pt_default_camera",
+]
+
+
+class PTError(RuntimeError):
+    pass
+
+
+class Params(ctypes.Structure):
+    _fields_ = [("max_depth", ctypes.c_int), ("sss_bounces", ctypes.c_int)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("rays", ctypes.c_uint64), ("nodes", ctypes.c_uint64), ("leaf_tests", ctypes.c_uint64),
+                ("samples", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libptamd.so (build it with `make -C discovering-path-tracer_amd`)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PTError(f"{LIB_PATH} not built; run __graft_entry__.build() or make -C {HERE}")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz, u32, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
+        psz = ctypes.POINTER(sz)
+        sig = {
+            "pt_abi_version": ([], i32), "pt_last_error": ([], ctypes.c_char_p),
+            "pt_create": ([i32, ctypes.POINTER(vp)], i32), "pt_destroy": ([vp], i32),
+            "pt_set_stream": ([vp, vp], i32), "pt_synchronize": ([vp], i32),
+            "pt_upload_scene": ([vp, vp, sz, vp, sz, vp, sz, vp, sz, vp, sz, u32], i32),
+            "pt_upload_lights": ([vp, vp, sz], i32), "pt_set_camera": ([vp, vp], i32),
+            "pt_set_params": ([vp, ctypes.POINTER(Params)], i32),
+            "pt_resize_and_clear": ([vp, i32, i32], i32), "pt_bind_accum": ([vp, vp, i32, i32], i32),
+            "pt_clear_accum": ([vp], i32), "pt_accum_device_ptr": ([vp], vp),
+            "pt_read_accum": ([vp, vp, sz], i32), "pt_dispatch": ([vp, u32], i32),
+            "pt_render": ([vp, u32, u32], i32), "pt_set_partition": ([vp, i32, i32], i32),
+            "pt_set_stats_mode": ([vp, i32], i32), "pt_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
+            "pt_reset_stats": ([vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
+            "pt_launch_times_ms": ([vp, vp, sz, psz], i32), "pt_reset_launch_times": ([vp], i32),
+            "pt_scene_load_obj": ([ctypes.c_char_p, ctypes.POINTER(vp)], i32),
+            "pt_scene_parse_obj": ([ctypes.c_char_p, sz, ctypes.POINTER(vp)], i32),
+            "pt_scene_from_arrays": ([vp, sz, vp, sz, ctypes.POINTER(vp)], i32),
+            "pt_scene_build_bvh": ([vp, u32, i32], i32),
+            "pt_scene_counts": ([vp, psz, psz, psz, psz, psz], i32),
+            "pt_scene_copy": ([vp, vp, vp, vp, vp, vp], i32), "pt_scene_upload": ([vp, vp], i32),
+            "pt_scene_free": ([vp], i32), "pt_pack_light": ([vp, vp, vp, vp, vp], i32),
+            "pt_default_camera": ([vp], i32),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def _check(rc, what):
+    if rc != PT_OK:
+        raise PTError(f"{what} failed ({rc}): {lib().pt_last_error().decode()}")
+
+
+def _ptr(a):
+    return a.ctypes.data if a is not None and a.size else None
+
+
+class Scene:
+    """OBJ (or raw arrays) + BVH, built by the native host layer."""
+
+    def __init__(self, handle):
+        self._h = ctypes.c_void_p(handle) if not isinstance(handle, ctypes.c_void_p) else handle
+
+    @classmethod
+    def load_obj(cls, path):
+        h = ctypes.c_void_p()
+        _check(lib().pt_scene_load_obj(path.encode(), ctypes.byref(h)), "pt_scene_load_obj")
+        return cls(h)
+
+    @classmethod
+    def parse_obj(cls, text: bytes):
+        h = ctypes.c_void_p()
+        _check(lib().pt_scene_parse_obj(text, len(text), ctypes.byref(h)), "pt_scene_parse_obj")
+        return cls(h)
+
+    @classmethod
+    def from_arrays(cls, vertices, indices):
+        v = np.ascontiguousarray(vertices, np.float32).reshape(-1)
+        i = np.ascontiguousarray(indices, np.uint32).reshape(-1)
+        h = ctypes.c_void_p()
+        _check(lib().pt_scene_from_arrays(_ptr(v), v.size, _ptr(i), i.size, ctypes.byref(h)), "pt_scene_from_arrays")
+        return cls(h)
+
+    def build_bvh(self, int_bits=False, threads=0):
+        self.int_bits = int_bits
+        _check(lib().pt_scene_build_bvh(self._h, PT_NODES_INT_BITS if int_bits else 0, threads), "pt_scene_build_bvh")
+        return self
+
+    def counts(self):
+        c = [ctypes.c_size_t() for _ in range(5)]
+        _check(lib().pt_scene_counts(self._h, *[ctypes.byref(x) for x in c]), "pt_scene_counts")
+        return tuple(x.value for x in c)
+
+    def arrays(self):
+        """(vertices, indices [BVH order once built], nodes (N,8) float32, uvs, mat_indices)."""
+        nvf, ni, nn, nuv, nmat = self.counts()
+        v = np.zeros(nvf, np.float32)
+        i = np.zeros(ni, np.uint32)
+        n = np.zeros((nn, 8), np.float32)
+        uv = np.zeros(nuv, np.float32)
+        m = np.zeros(nmat, np.uint32)
+        _check(lib().pt_scene_copy(self._h, _ptr(v), _ptr(i), _ptr(n), _ptr(uv), _ptr(m)), "pt_scene_copy")
+        return v, i, n, uv, m
+
+    def close(self):
+        if self._h:
+            lib().pt_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def pack_light(position, normal, intensity, size):
+    """Light::packData (src/Light.cpp:16-33) -> 16 float32."""
+    out = np.zeros(16, np.float32)
+    args = [np.ascontiguousarray(a, np.float32) for a in (position, normal, intensity, size)]
+    _check(lib().pt_pack_light(*[a.ctypes.data for a in args], out.ctypes.data), "pt_pack_light")
+    return out
+
+
+def reference_light():
+    """The scene light of VulkanRayTracer.cpp:149-162."""
+    return pack_light([0, 2, 0], [0, -1, 0], [10, 10, 10], [2.5, 2.5])
+
+
+def default_camera():
+    ubo = np.zeros(16, np.float32)
+    _check(lib().pt_default_camera(ubo.ctypes.data), "pt_default_camera")
+    return ubo
+
+
+class Renderer:
+    """One GPU's path tracer: upload, dispatch/render, read back."""
+
+    def __init__(self, device=0):
+        self._c = ctypes.c_void_p()
+        _check(lib().pt_create(device, ctypes.byref(self._c)), "pt_create")
+        self.width = self.height = 0
+
+    def upload_scene(self, vertices, indices, nodes, uvs=None, mat=None, int_bits=False):
+        v = np.ascontiguousarray(vertices, np.float32).reshape(-1)
+        i = np.ascontiguousarray(indices, np.uint32).reshape(-1)
+        n = np.ascontiguousarray(nodes, np.float32).reshape(-1)
+        uv = None if uvs is None else np.ascontiguousarray(uvs, np.float32).reshape(-1)
+        m = None if mat is None else np.ascontiguousarray(mat, np.uint32).reshape(-1)
+        _check(lib().pt_upload_scene(self._c, _ptr(v), v.size, _ptr(i), i.size, _ptr(n), n.size // 8,
+                                     _ptr(uv), 0 if uv is None else uv.size, _ptr(m), 0 if m is None else m.size,
+                                     PT_NODES_INT_BITS if int_bits else 0), "pt_upload_scene")
+
+    def upload(self, scene: Scene):
+        _check(lib().pt_scene_upload(self._c, scene._h), "pt_scene_upload")
+
+    def upload_lights(self, lights16):
+        l = np.ascontiguousarray(lights16, np.float32).reshape(-1)
+        _check(lib().pt_upload_lights(self._c, _ptr(l), l.size // 16), "pt_upload_lights")
+
+    def set_camera(self, ubo16):
+        u = np.ascontiguousarray(ubo16, np.float32).reshape(16)
+        _check(lib().pt_set_camera(self._c, u.ctypes.data), "pt_set_camera")
+
+    def set_params(self, max_depth=4, sss_bounces=3):
+        p = Params(max_depth, sss_bounces)
+        _check(lib().pt_set_params(self._c, ctypes.byref(p)), "pt_set_params")
+
+    def set_partition(self, nranks, rank):
+        _check(lib().pt_set_partition(self._c, nranks, rank), "pt_set_partition")
+
+    def set_stream(self, stream_handle):
+        _check(lib().pt_set_stream(self._c, stream_handle), "pt_set_stream")
+
+    def resize_and_clear(self, w, h):
+        _check(lib().pt_resize_and_clear(self._c, w, h), "pt_resize_and_clear")
+        self.width, self.height = w, h
+
+    def bind_accum(self, device_ptr, w, h):
+        _check(lib().pt_bind_accum(self._c, device_ptr, w, h), "pt_bind_accum")
+        self.width, self.height = w, h
+
+    def clear(self):
+        _check(lib().pt_clear_accum(self._c), "pt_clear_accum")
+
+    def accum_ptr(self):
+        return lib().pt_accum_device_ptr(self._c)
+
+    def dispatch(self, sample_batch):
+        _check(lib().pt_dispatch(self._c, sample_batch), "pt_dispatch")
+
+    def render(self, first_batch, n_batches):
+        _check(lib().pt_render(self._c, first_batch, n_batches), "pt_render")
+
+    def synchronize(self):
+        _check(lib().pt_synchronize(self._c), "pt_synchronize")
+
+    def read_accum(self):
+        out = np.empty(self.width * self.height * 4, np.float32)
+        _check(lib().pt_read_accum(self._c, out.ctypes.data, out.size), "pt_read_accum")
+        return out
+
+    def set_stats_mode(self, on):
+        _check(lib().pt_set_stats_mode(self._c, 1 if on else 0), "pt_set_stats_mode")
+
+    def reset_stats(self):
+        _check(lib().pt_reset_stats(self._c), "pt_reset_stats")
+
+    def stats(self):
+        s = Stats()
+        _check(lib().pt_get_stats(self._c, ctypes.byref(s)), "pt_get_stats")
+        return {"rays": s.rays, "nodes": s.nodes, "leaf_tests": s.leaf_tests, "samples": s.samples}
+
+    def last_launch_ms(self):
+        ms = ctypes.c_float()
+        _check(lib().pt_last_launch_ms(self._c, ctypes.byref(ms)), "pt_last_launch_ms")
+        return ms.value
+
+    def launch_times_ms(self):
+        n = ctypes.c_size_t()
+        out = np.zeros(512, np.float32)
+        _check(lib().pt_launch_times_ms(self._c, out.ctypes.data, out.size, ctypes.byref(n)), "pt_launch_times_ms")
+        return out[: n.value].copy()
+
+    def reset_launch_times(self):
+        _check(lib().pt_reset_launch_times(self._c), "pt_reset_launch_times")
+
+    def close(self):
+        if self._c:
+            lib().pt_destroy(self._c)
+            self._c = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

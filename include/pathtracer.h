@@ -1,0 +1,180 @@
+/*
+ * pathtracer.h — C ABI of the MI355X-native path-tracing pixel kernel.
+ *
+ * This is the drop-in boundary.  The reference has no plugin/operator API:
+ * its seam is the Vulkan compute interface that VulkanRayTracer builds and
+ * drives (src/Vulkan/VulkanRayTracer.cpp) for the shader
+ * src/shaders/raytrace_comp.comp.  Every entry point below replaces one piece
+ * of that seam; the comment on each cites what it replaces.  A maintainer
+ * swaps the Vulkan descriptor/dispatch code for these calls.
+ *
+ * Conventions (inherited from the reference):
+ *   - every call returns int status: PT_OK (0) or a negative PT_ERR_*;
+ *     pt_last_error() describes the last failure on the calling thread.
+ *     Nothing throws across the ABI.
+ *   - the caller keeps ownership of every host array; uploads copy.
+ *   - the accumulation buffer is device-resident (RGBA32F, row-major,
+ *     pixel (x,y) at index y*W+x) until read back.
+ *   - one context per GPU, driven from one thread.  Calls are ordered on the
+ *     context's HIP stream; pt_dispatch/pt_render return once the work is
+ *     enqueued, pt_read_accum/pt_synchronize wait for it (the reference blocks
+ *     on a fence after every dispatch, VulkanCommandBuffer.cpp:140).
+ */
+#ifndef PATHTRACER_H_
+#define PATHTRACER_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_ABI_VERSION 1
+
+enum {
+  PT_OK = 0,
+  PT_ERR_INVALID = -1,     /* bad argument / state */
+  PT_ERR_HIP = -2,         /* HIP runtime failure */
+  PT_ERR_SCENE = -3,       /* malformed scene / BVH */
+  PT_ERR_IO = -4,          /* file not found / parse error */
+  PT_ERR_UNSUPPORTED = -5  /* valid input this build does not handle */
+};
+
+/* BVHNode — src/BoundingVolumeHierarchy.h:8-13, std430 stride 32 B.
+ * min_bounds.w = left child or -1 (leaf); max_bounds.w = right child or the
+ * leaf's triangle index.  Indices are floats (reference) unless
+ * PT_NODES_INT_BITS is passed, in which case they are int32 bit patterns. */
+typedef struct pt_bvh_node {
+  float min_bounds[4];
+  float max_bounds[4];
+} pt_bvh_node;
+
+/* AreaLightData — src/Light.h:6-12, 64 B. */
+typedef struct pt_area_light {
+  float position[4];
+  float normal[4];
+  float intensity[4];
+  float size[4];
+} pt_area_light;
+
+/* Tunables the reference hard-codes (raytrace_comp.comp:304,373). */
+typedef struct pt_params {
+  int max_depth;    /* MAX_DEPTH, reference 4 */
+  int sss_bounces;  /* SSS_MAX_BOUNCES, reference 3 */
+} pt_params;
+
+/* Statistics of the reference traversal (exhaustive DFS, raytrace_comp.comp:159-204),
+ * accumulated while stats mode is on: traceRay calls, BVH nodes visited,
+ * leaf triangle tests, pixel-samples. */
+typedef struct pt_stats {
+  uint64_t rays;
+  uint64_t nodes;
+  uint64_t leaf_tests;
+  uint64_t samples;
+} pt_stats;
+
+typedef struct pt_context pt_context;
+
+/* upload flags */
+#define PT_NODES_INT_BITS 0x1u
+
+/* ---- lifetime ---------------------------------------------------------- */
+int pt_abi_version(void);
+const char* pt_last_error(void);
+/* Replaces VulkanWindow's device/queue selection (VulkanWindow.cpp:106-174)
+ * and VulkanRayTracer::initComputePipeline's pipeline creation (:624-672). */
+int pt_create(int device_ordinal, pt_context** out);
+int pt_destroy(pt_context* ctx);
+/* Launch on a caller-owned hipStream_t (e.g. torch's current stream); NULL
+ * returns to the context's own stream. */
+int pt_set_stream(pt_context* ctx, void* hip_stream);
+int pt_synchronize(pt_context* ctx);
+
+/* ---- scene upload (VulkanRayTracer.cpp:100-311, bindings 1,2,3,6,7) ---- */
+/* vertices: float[3V] (binding 1); indices: uint[3T] in BVH-leaf order
+ * (binding 2); nodes: BVHNode[2T-1] (binding 3); uvs (binding 6) and
+ * mat_indices (binding 7) are accepted for interface parity and validated but
+ * do not affect the output (raytrace_comp.comp:150-154,192 are dead). */
+int pt_upload_scene(pt_context* ctx,
+                    const float* vertices, size_t n_vertex_floats,
+                    const uint32_t* indices, size_t n_indices,
+                    const pt_bvh_node* nodes, size_t n_nodes,
+                    const float* uvs, size_t n_uv_floats,
+                    const uint32_t* mat_indices, size_t n_mat,
+                    uint32_t flags);
+/* binding 5 (VulkanRayTracer.cpp:165-176) */
+int pt_upload_lights(pt_context* ctx, const pt_area_light* lights, size_t n_lights);
+/* binding 4: std140 CameraBuffer — pos@0, dir@16, up@32, fov.x@48
+ * (raytrace_comp.comp:67-73; written at VulkanRayTracer.cpp:761-764). */
+int pt_set_camera(pt_context* ctx, const float camera_ubo[16]);
+int pt_set_params(pt_context* ctx, const pt_params* params);
+
+/* ---- accumulation image (binding 0, VulkanRayTracer.cpp:317-320) ------- */
+/* Allocate (or reuse) a W x H RGBA32F buffer and zero it.  The reference
+ * never clears its image (VulkanImage.cpp:71); batch 0 multiplies prev by 0. */
+int pt_resize_and_clear(pt_context* ctx, int width, int height);
+/* Render into caller-owned device memory of W*H*16 bytes instead (not
+ * cleared; call pt_clear_accum). */
+int pt_bind_accum(pt_context* ctx, void* device_ptr, int width, int height);
+int pt_clear_accum(pt_context* ctx);
+void* pt_accum_device_ptr(pt_context* ctx);
+int pt_read_accum(pt_context* ctx, float* rgba, size_t n_floats);
+
+/* ---- the hot path ------------------------------------------------------ */
+/* One 1-spp accumulation pass with push constant sample_batch
+ * (VulkanRayTracer.cpp:803-813 vkCmdPushConstants + vkCmdDispatch). */
+int pt_dispatch(pt_context* ctx, uint32_t sample_batch);
+/* n_batches sequential passes first_batch..first_batch+n-1 fused into one
+ * launch; bit-identical to that many pt_dispatch calls. */
+int pt_render(pt_context* ctx, uint32_t first_batch, uint32_t n_batches);
+
+/* ---- multi-GPU screen-space partition ------------------ */
+/* Pixels are grouped into 16x16 blocks, numbered row-major; this context
+ * renders block b iff b % nranks == rank.  pt_clear_accum then writes +0 to
+ * owned pixels and -0 (the IEEE additive identity) to the others, so a sum
+ * reduction of all ranks' buffers is bit-identical to a single-GPU frame. */
+int pt_set_partition(pt_context* ctx, int nranks, int rank);
+
+/* ---- instrumentation --------------------------------------------------- */
+/* Stats mode runs the reference-exhaustive traversal with counters (output is
+ * unchanged); used for the roofline's algorithmic byte count. */
+int pt_set_stats_mode(pt_context* ctx, int enabled);
+int pt_get_stats(pt_context* ctx, pt_stats* out);
+int pt_reset_stats(pt_context* ctx);
+/* Device time of the last pt_render/pt_dispatch launch, from HIP events
+ * recorded on the launch stream. */
+int pt_last_launch_ms(pt_context* ctx, float* ms);
+/* Device times of every render launch since pt_reset_launch_times (the last
+ * 512 at most), oldest first; waits for them to finish. */
+int pt_launch_times_ms(pt_context* ctx, float* out, size_t max_n, size_t* n_out);
+int pt_reset_launch_times(pt_context* ctx);
+
+/* ---- host scene layer (L1 producers: BVH, Light, OBJ ingest) ----------- */
+typedef struct pt_scene pt_scene;
+/* tinyobj::ObjReader::ParseFromFile + index gathering (VulkanRayTracer.cpp:64-92) */
+int pt_scene_load_obj(const char* path, pt_scene** out);
+int pt_scene_parse_obj(const char* text, size_t len, pt_scene** out);
+/* scene from raw arrays (e.g. synthetic meshes) */
+int pt_scene_from_arrays(const float* vertices, size_t n_vertex_floats,
+                         const uint32_t* indices, size_t n_indices, pt_scene** out);
+/* BVH bvh(objVertices, objIndices) (BoundingVolumeHierarchy.cpp:5-23);
+ * flags: PT_NODES_INT_BITS; threads 0 = all cores. */
+int pt_scene_build_bvh(pt_scene* scene, uint32_t flags, int threads);
+int pt_scene_counts(const pt_scene* scene, size_t* n_vertex_floats, size_t* n_indices,
+                    size_t* n_nodes, size_t* n_uv_floats, size_t* n_mat);
+int pt_scene_copy(const pt_scene* scene, float* vertices, uint32_t* indices, pt_bvh_node* nodes,
+                  float* uvs, uint32_t* mat_indices);
+int pt_scene_upload(pt_context* ctx, const pt_scene* scene);
+int pt_scene_free(pt_scene* scene);
+/* Light lights(positions, normals, intensities, sizes) packing (Light.cpp:16-33) */
+int pt_pack_light(const float position[3], const float normal[3], const float intensity[3],
+                  const float size[2], pt_area_light* out);
+/* Camera getters for the reference's default orbit camera, as the UBO
+ * (Camera.cpp:4-10, 84-106): pos (0,0,5) dir (0,0,-1) up (0,1,0) fov 60. */
+int pt_default_camera(float camera_ubo[16]);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PATHTRACER_H_ */
