@@ -35,6 +35,26 @@ def algorithmic_bytes(st):
     return 32 * st["nodes"] + 48 * st["leaf_tests"] + 32 * st["samples"]
 
 
+def profiled_traffic():
+    """HBM bytes per launch of the current kernel source from the newest
+    committed rocprofv3 PMC summary (tools/gpu_profile.sh ->
+    tools/summarize_profile.py): FETCH_SIZE (x2, gfx950) + WRITE_SIZE.
+    None if no summary was taken of this exact pt_device.hip."""
+    import glob
+    import hashlib
+    src = os.path.join(ROOT, "discovering-path-tracer_amd", "csrc", "pt_device.hip")
+    h = hashlib.sha1(open(src, "rb").read()).hexdigest()
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
+        try:
+            d = json.load(open(p))
+        except ValueError:
+            continue
+        if d.get("pt_device_hip_sha1") == h and "hbm_bytes_per_launch" in d:
+            best = (os.path.relpath(p, ROOT), d["hbm_bytes_per_launch"]["total"])
+    return best
+
+
 def cpu_baseline(v, i, n, cam, light):
     """The oracle (scalar C++ restatement of raytrace_comp.comp) on this host,
     all cores, on a bounded sample: every 8th row of the same frame."""
@@ -147,6 +167,7 @@ def main():
         # per-launch algorithmic bytes of one rank's share (the kernel is per-GPU)
         bytes_per_launch = algorithmic_bytes(tot) / world
         achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+        prof = profiled_traffic() if world == 1 else None
         out = {
             "metric": "Mrays/s at 1920x1080x8spp, box.obj BVH",
             "value": round(value, 3),
@@ -166,7 +187,9 @@ def main():
                        "rays_per_frame": int(rays_per_frame),
                        "msamples_per_s": round(W * H * SPP * args.steps / dt / 1e6, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": None if prof is None else int(prof[1]),
+                         "traffic_source": None if prof is None else prof[0],
                          "kernel": "render_kernel<false>", "kernel_ms": round(kernel_ms, 4),
                          "algorithmic_bytes_per_launch": int(bytes_per_launch)},
         }

@@ -450,6 +450,22 @@ int pt_reset_launch_times(pt_context* c) {
   return PT_OK;
 }
 
+int pt_selftest_math(int device, int fn, const float* x, float* y, size_t n) {
+  if (!x || !y) return fail(PT_ERR_INVALID, "null argument");
+  if (n == 0) return PT_OK;
+  PT_HIP(hipSetDevice(device));
+  float *dx = nullptr, *dy = nullptr;
+  PT_HIP(hipMalloc((void**)&dx, n * sizeof(float)));
+  hipError_t e = hipMalloc((void**)&dy, n * sizeof(float));
+  if (e == hipSuccess) e = hipMemcpy(dx, x, n * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = ptd::launch_math(fn, dx, dy, n, nullptr);
+  if (e == hipSuccess) e = hipMemcpy(y, dy, n * sizeof(float), hipMemcpyDeviceToHost);
+  (void)hipFree(dx);
+  if (dy) (void)hipFree(dy);
+  if (e != hipSuccess) return fail(PT_ERR_HIP, std::string("pt_selftest_math: ") + hipGetErrorString(e));
+  return PT_OK;
+}
+
 // ---------------------------------------------------------------- scene ----
 
 int pt_scene_load_obj(const char* path, pt_scene** out) {

@@ -47,5 +47,6 @@ hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices,
                              hipStream_t stream);
 hipError_t launch_clear(float4* accum, int width, int height, int nranks, int rank, hipStream_t stream);
 hipError_t launch_render(const RenderParams& p, bool stats, hipStream_t stream);
+hipError_t launch_math(int fn, const float* x, float* y, size_t n, hipStream_t stream);
 
 }  // namespace ptd

@@ -398,7 +398,34 @@ __global__ __launch_bounds__(256) void clear_kernel(float4* accum, int W, int H,
   accum[i] = make_float4(z, z, z, z);
 }
 
+__global__ __launch_bounds__(256) void math_kernel(int fn, const float* __restrict__ x, float* __restrict__ y,
+                                                   size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float v = x[i];
+  float r;
+  switch (fn) {
+    case 0: r = log_(v); break;
+    case 1: r = exp_(v); break;
+    case 2: r = sin_(v); break;
+    case 3: r = cos_(v); break;
+    case 4: r = tan_(v); break;
+    case 5: r = acos_(v); break;
+    case 6: r = sqrt_(v); break;
+    case 7: { uint32_t s = __float_as_uint(v); r = rng_next(&s); break; }
+    case 8: r = 1.0f / v; break;
+    default: r = v; break;
+  }
+  y[i] = r;
+}
+
 }  // namespace
+
+hipError_t launch_math(int fn, const float* x, float* y, size_t n, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  math_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(fn, x, y, n);
+  return hipGetLastError();
+}
 
 hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices, int n_tris, float4* d_tris,
                              hipStream_t stream) {

@@ -24,7 +24,7 @@ EXPORTS = [
     "pt_upload_scene", "pt_upload_lights", "pt_set_camera", "pt_set_params", "pt_resize_and_clear",
     "pt_bind_accum", "pt_clear_accum", "pt_accum_device_ptr", "pt_read_accum", "pt_dispatch", "pt_render",
     "pt_set_partition", "pt_set_stats_mode", "pt_get_stats", "pt_reset_stats", "pt_last_launch_ms",
-    "pt_launch_times_ms", "pt_reset_launch_times",
+    "pt_launch_times_ms", "pt_reset_launch_times", "pt_selftest_math",
     "pt_scene_load_obj", "pt_scene_parse_obj", "pt_scene_from_arrays", "pt_scene_build_bvh",
     "pt_scene_counts", "pt_scene_copy", "pt_scene_upload", "pt_scene_free", "pt_pack_light",
     "pt_default_camera",
@@ -70,6 +70,7 @@ def lib():
             "pt_set_stats_mode": ([vp, i32], i32), "pt_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
             "pt_reset_stats": ([vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
             "pt_launch_times_ms": ([vp, vp, sz, psz], i32), "pt_reset_launch_times": ([vp], i32),
+            "pt_selftest_math": ([i32, i32, vp, vp, sz], i32),
             "pt_scene_load_obj": ([ctypes.c_char_p, ctypes.POINTER(vp)], i32),
             "pt_scene_parse_obj": ([ctypes.c_char_p, sz, ctypes.POINTER(vp)], i32),
             "pt_scene_from_arrays": ([vp, sz, vp, sz, ctypes.POINTER(vp)], i32),
@@ -166,6 +167,22 @@ def pack_light(position, normal, intensity, size):
 def reference_light():
     """The scene light of VulkanRayTracer.cpp:149-162."""
     return pack_light([0, 2, 0], [0, -1, 0], [10, 10, 10], [2.5, 2.5])
+
+
+def device_math(fn, x, device=0):
+    """Evaluate the kernel's math function `fn` on the GPU (pt_selftest_math)."""
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.empty_like(x)
+    _check(lib().pt_selftest_math(device, fn, x.ctypes.data, y.ctypes.data, x.size), "pt_selftest_math")
+    return y
+
+
+def partition_owned(width, height, nranks, rank):
+    """Pixels a rank renders under pt_set_partition: 16x16 blocks, row-major
+    block id b, owned iff b % nranks == rank.  Returns a (H, W) bool mask."""
+    bx = (width + 15) // 16
+    ys, xs = np.mgrid[0:height, 0:width]
+    return ((ys // 16) * bx + xs // 16) % nranks == rank
 
 
 def default_camera():

@@ -149,6 +149,10 @@ int pt_last_launch_ms(pt_context* ctx, float* ms);
  * 512 at most), oldest first; waits for them to finish. */
 int pt_launch_times_ms(pt_context* ctx, float* out, size_t max_n, size_t* n_out);
 int pt_reset_launch_times(pt_context* ctx);
+/* Evaluates the kernel's fp32 math on the device for bitwise checks against
+ * the oracle: fn 0 log, 1 exp, 2 sin, 3 cos, 4 tan, 5 acos, 6 sqrt,
+ * 7 first RNG draw from the seed given as the float's bits, 8 reciprocal. */
+int pt_selftest_math(int device_ordinal, int fn, const float* x, float* y, size_t n);
 
 /* ---- host scene layer (L1 producers: BVH, Light, OBJ ingest) ----------- */
 typedef struct pt_scene pt_scene;

@@ -654,6 +654,8 @@ void oracle_math(int fn, const float* x, float* y, size_t n) {
       case 4: y[i] = gm_tan(v); break;
       case 5: y[i] = gm_acos(v); break;
       case 6: y[i] = gm_sqrt(v); break;
+      case 7: { uint32_t sd = gm_f2u(v); y[i] = rng_f(&sd); break; }
+      case 8: y[i] = 1.0f / v; break;
       default: y[i] = v; break;
     }
   }
@@ -665,3 +667,21 @@ void oracle_rng(uint32_t seed, float* out, size_t n) {
 }
 
 }  // extern "C"
+
+extern "C" {
+// Single traceRay (raytrace_comp.comp:159-204) for known-answer tests:
+// out[0] = hit (0/1), out[1] = t, out[2..4] = position, out[5..7] = normal;
+// counters[0..2] += rays, nodes, leaves.
+void oracle_trace(const float* verts, const uint32_t* idx, const float* nodes, size_t n_nodes,
+                  const float* o3, const float* d3, float* out, uint64_t* counters) {
+  Scene S;
+  S.V = verts; S.I = idx; S.N = nodes; S.nn = n_nodes;
+  Stats st;
+  Hit h = trace(S, V(o3[0], o3[1], o3[2]), V(d3[0], d3[1], d3[2]), &st);
+  out[0] = h.hit ? 1.0f : 0.0f;
+  out[1] = h.t;
+  out[2] = h.p.x; out[3] = h.p.y; out[4] = h.p.z;
+  out[5] = h.n.x; out[6] = h.n.y; out[7] = h.n.z;
+  if (counters) { counters[0] += st.rays; counters[1] += st.nodes; counters[2] += st.leaves; }
+}
+}

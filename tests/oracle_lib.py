@@ -36,6 +36,7 @@ def lib():
                                     F32P, U64P, ctypes.c_int]
         L.oracle_math.argtypes = [ctypes.c_int, F32P, F32P, sz]
         L.oracle_rng.argtypes = [ctypes.c_uint32, F32P, sz]
+        L.oracle_trace.argtypes = [F32P, U32P, F32P, sz, F32P, F32P, F32P, U64P]
         _LIB = L
     return _LIB
 
@@ -95,3 +96,13 @@ def rng(seed, n):
     out = np.empty(n, np.float32)
     lib().oracle_rng(seed, out, n)
     return out
+
+
+def trace(verts, idx, nodes, origin, direction):
+    """One reference traceRay: (hit, t, position, normal, [rays, nodes, leaves])."""
+    out = np.zeros(8, np.float32)
+    ctr = np.zeros(3, np.uint64)
+    nodes = np.ascontiguousarray(nodes, np.float32).reshape(-1)
+    lib().oracle_trace(np.ascontiguousarray(verts, np.float32), np.ascontiguousarray(idx, np.uint32), nodes,
+                       nodes.size // 8, np.asarray(origin, np.float32), np.asarray(direction, np.float32), out, ctr)
+    return bool(out[0]), float(out[1]), out[2:5].copy(), out[5:8].copy(), ctr
