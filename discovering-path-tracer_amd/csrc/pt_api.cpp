@@ -94,11 +94,25 @@ int thread_bvh(const pt_bvh_node* nodes, size_t n, bool int_bits, size_t n_tris,
     const int32_t v = order[k];
     if (left[v] != -1) size[v] = 1 + size[left[v]] + size[right[v]];
   }
+  // A child whose bounds are bitwise its parent's is hit whenever it is
+  // visited (it is only visited after its parent was hit by the same ray, and
+  // the slab test is a pure function of ray and bounds): flag it in bit 31 of
+  // `skip` so the kernel can skip recomputing the test.
+  std::vector<int32_t> parent(n, -1);
+  for (size_t k = 0; k < m; ++k) {
+    const int32_t v = order[k];
+    if (left[v] != -1) parent[left[v]] = parent[right[v]] = v;
+  }
+  auto same_bounds = [&](int32_t a, int32_t b) {
+    return memcmp(nodes[a].min_bounds, nodes[b].min_bounds, 12) == 0 &&
+           memcmp(nodes[a].max_bounds, nodes[b].max_bounds, 12) == 0;
+  };
   out->assign(2 * m, make_float4(0, 0, 0, 0));
   for (size_t k = 0; k < m; ++k) {
     const int32_t v = order[k];
     const pt_bvh_node& nd = nodes[v];
-    const int32_t skip = (int32_t)k + size[v];
+    const bool implied = parent[v] >= 0 && same_bounds(v, parent[v]);
+    const int32_t skip = (int32_t)(((uint32_t)k + (uint32_t)size[v]) | (implied ? 0x80000000u : 0u));
     const int32_t tri = left[v] == -1 ? right[v] : -1;
     float fs, ft;
     memcpy(&fs, &skip, 4);
@@ -120,6 +134,7 @@ struct pt_context {
   float4* d_tris = nullptr;
   int n_tris = 0;
   ptd::LightRec* d_lights = nullptr;
+  ptd::LightDev* d_lights_dev = nullptr;
   int n_lights = 0;
   float4* d_accum = nullptr;
   bool own_accum = false;
@@ -131,6 +146,7 @@ struct pt_context {
   pt_params params{4, 3};
   int nranks = 1, rank = 0;
   bool stats_mode = false;
+  int opt_scene_lds = 1;   // PT_OPT_SCENE_IN_LDS: 0 never, 1 auto, 2 always
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   // ring of event pairs, one per render launch since pt_reset_launch_times
@@ -191,6 +207,7 @@ int pt_destroy(pt_context* c) {
   dev_free(c->d_nodes);
   dev_free(c->d_tris);
   dev_free(c->d_lights);
+  dev_free(c->d_lights_dev);
   if (c->own_accum) dev_free(c->d_accum);
   dev_free(c->d_stats);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -266,10 +283,13 @@ int pt_upload_lights(pt_context* c, const pt_area_light* lights, size_t n) {
   PT_HIP(hipSetDevice(c->device));
   PT_HIP(hipStreamSynchronize(c->stream));
   dev_free(c->d_lights);
+  dev_free(c->d_lights_dev);
   c->n_lights = 0;
   if (n) {
     PT_HIP(hipMalloc((void**)&c->d_lights, n * sizeof(ptd::LightRec)));
+    PT_HIP(hipMalloc((void**)&c->d_lights_dev, n * sizeof(ptd::LightDev)));
     PT_HIP(hipMemcpyAsync(c->d_lights, lights, n * sizeof(ptd::LightRec), hipMemcpyHostToDevice, c->stream));
+    PT_HIP(ptd::launch_setup_lights(c->d_lights, (int)n, c->d_lights_dev, c->stream));
     PT_HIP(hipStreamSynchronize(c->stream));
   }
   c->n_lights = (int)n;
@@ -359,10 +379,11 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   ptd::RenderParams p;
   p.nodes = c->d_nodes;
   p.tris = c->d_tris;
-  p.lights = c->d_lights;
+  p.lights = c->d_lights_dev;
   p.accum = c->d_accum;
   p.stats = c->d_stats;
   p.n_nodes = c->n_nodes;
+  p.n_tris = c->n_tris;
   p.n_lights = c->n_lights;
   p.width = c->width;
   p.height = c->height;
@@ -384,7 +405,10 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   const int slot = c->ring_n % pt_context::kRing;
   PT_HIP(hipEventRecord(c->ev0, c->stream));
   PT_HIP(hipEventRecord(c->ring[slot][0], c->stream));
-  PT_HIP(ptd::launch_render(p, c->stats_mode, c->stream));
+  const bool fits = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
+  if (c->opt_scene_lds == 2 && !fits) return fail(PT_ERR_UNSUPPORTED, "scene too large for the LDS variant");
+  const bool lds = c->opt_scene_lds == 2 || (c->opt_scene_lds == 1 && fits);
+  PT_HIP(ptd::launch_render(p, c->stats_mode, lds, c->stream));
   PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
   PT_HIP(hipEventRecord(c->ev1, c->stream));
   c->ring_n++;
@@ -393,6 +417,18 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
 }
 
 int pt_dispatch(pt_context* c, uint32_t sample_batch) { return pt_render(c, sample_batch, 1); }
+
+int pt_set_option(pt_context* c, int key, int value) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  switch (key) {
+    case PT_OPT_SCENE_IN_LDS:
+      if (value < 0 || value > 2) return fail(PT_ERR_INVALID, "PT_OPT_SCENE_IN_LDS takes 0, 1 or 2");
+      c->opt_scene_lds = value;
+      return PT_OK;
+    default:
+      return fail(PT_ERR_INVALID, "unknown option " + std::to_string(key));
+  }
+}
 
 int pt_set_stats_mode(pt_context* c, int enabled) {
   if (!c) return fail(PT_ERR_INVALID, "null context");

@@ -27,13 +27,19 @@ struct LightRec {          // == pt_area_light / AreaLightData
   float size[4];
 };
 
+// Light with its sampling frame precomputed on the device (setup_lights_kernel).
+struct LightDev {
+  float pos[3], nraw[3], inten[3], right[3], up[3], size[2], half[2], pad;
+};
+
 struct RenderParams {
   const float4* nodes;
   const float4* tris;
-  const LightRec* lights;
+  const LightDev* lights;
   float4* accum;
   unsigned long long* stats;   // rays, nodes, leaf tests, samples (stats mode only)
   int n_nodes;
+  int n_tris;
   int n_lights;
   int width, height;
   uint32_t first_batch, n_batches;
@@ -45,8 +51,14 @@ struct RenderParams {
 
 hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices, int n_tris, float4* d_tris,
                              hipStream_t stream);
+hipError_t launch_setup_lights(const LightRec* d_in, int n, LightDev* d_out, hipStream_t stream);
 hipError_t launch_clear(float4* accum, int width, int height, int nranks, int rank, hipStream_t stream);
-hipError_t launch_render(const RenderParams& p, bool stats, hipStream_t stream);
+// Scene bytes the LDS-staged variant needs, and the largest it accepts.
+constexpr size_t kMaxSceneLds = 48 * 1024;
+inline size_t scene_lds_bytes(const RenderParams& p) {
+  return ((size_t)2 * p.n_nodes + (size_t)3 * p.n_tris) * 16;
+}
+hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, hipStream_t stream);
 hipError_t launch_math(int fn, const float* x, float* y, size_t n, hipStream_t stream);
 
 }  // namespace ptd

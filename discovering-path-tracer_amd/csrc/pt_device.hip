@@ -84,7 +84,9 @@ __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c) {
     const float4 a = P.nodes[2 * k];
     const float4 b = P.nodes[2 * k + 1];
     if (STATS) c.nodes++;
-    const bool h = slab(o, inv, a, b);
+    const int raw = __float_as_int(a.w);
+    // bit 31: bounds identical to the parent's, which this ray hit -> hit
+    const bool h = raw < 0 ? true : slab(o, inv, a, b);
     const int tri = __float_as_int(b.w);
     if (h && tri >= 0) {
       if (STATS) c.leaves++;
@@ -95,7 +97,7 @@ __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c) {
         bt = tri;
       }
     }
-    k = (h && tri < 0) ? k + 1 : __float_as_int(a.w);
+    k = (h && tri < 0) ? k + 1 : (raw & 0x7fffffff);
   }
   Hit r;
   r.t = best;
@@ -116,7 +118,9 @@ __device__ bool occluded(const RenderParams& P, v3 o, v3 d, float limit, Ctr& c)
     const float4 a = P.nodes[2 * k];
     const float4 b = P.nodes[2 * k + 1];
     if (STATS) c.nodes++;
-    const bool h = slab(o, inv, a, b);
+    const int raw = __float_as_int(a.w);
+    // bit 31: bounds identical to the parent's, which this ray hit -> hit
+    const bool h = raw < 0 ? true : slab(o, inv, a, b);
     const int tri = __float_as_int(b.w);
     if (h && tri >= 0) {
       if (STATS) c.leaves++;
@@ -127,44 +131,36 @@ __device__ bool occluded(const RenderParams& P, v3 o, v3 d, float limit, Ctr& c)
         if (!STATS) return true;
       }
     }
-    k = (h && tri < 0) ? k + 1 : __float_as_int(a.w);
+    k = (h && tri < 0) ? k + 1 : (raw & 0x7fffffff);
   }
   return occ;
 }
 
-__device__ __forceinline__ void light_frame(const LightRec& L, v3* right, v3* up) {
-  const v3 n = normalize(mk(L.normal[0], L.normal[1], L.normal[2]));
-  const v3 basis = fabs_(n.y) < 0.999f ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
-  *right = normalize(cross(n, basis));
-  *up = cross(*right, n);
-}
-
-// sampleAreaLight (:255-268)
-__device__ __forceinline__ v3 sample_area_light(const LightRec& L, uint32_t* rng) {
+// sampleAreaLight (:255-268); the light's frame (:261-264) is precomputed per
+// light by setup_lights_kernel with the same ops.
+__device__ __forceinline__ v3 sample_area_light(const LightDev& L, uint32_t* rng) {
   const float u = rng_next(rng) * 2.0f - 1.0f;
   const float v = rng_next(rng) * 2.0f - 1.0f;
-  v3 right, up;
-  light_frame(L, &right, &up);
-  const v3 pos = mk(L.position[0], L.position[1], L.position[2]);
+  const v3 right = mk(L.right[0], L.right[1], L.right[2]);
+  const v3 up = mk(L.up[0], L.up[1], L.up[2]);
+  const v3 pos = mk(L.pos[0], L.pos[1], L.pos[2]);
   return add(add(pos, muls(muls(muls(right, u), L.size[0]), 0.5f)), muls(muls(muls(up, v), L.size[1]), 0.5f));
 }
 
 // intersectAreaLight (:271-298)
-__device__ __forceinline__ bool intersect_area_light(v3 o, v3 d, const LightRec& L, float* t) {
-  const v3 n_raw = mk(L.normal[0], L.normal[1], L.normal[2]);
-  const v3 pos = mk(L.position[0], L.position[1], L.position[2]);
+__device__ __forceinline__ bool intersect_area_light(v3 o, v3 d, const LightDev& L, float* t) {
+  const v3 n_raw = mk(L.nraw[0], L.nraw[1], L.nraw[2]);
+  const v3 pos = mk(L.pos[0], L.pos[1], L.pos[2]);
   const float denom = dot(n_raw, d);
   if (fabs_(denom) < 0.0001f) return false;
   const float tt = dot(n_raw, sub(pos, o)) / denom;
   *t = tt;
   if (tt <= 0.0f) return false;
   const v3 hp = add(o, muls(d, tt));
-  v3 right, up;
-  light_frame(L, &right, &up);
   const v3 th = sub(hp, pos);
-  const float u = dot(th, right);
-  const float v = dot(th, up);
-  return fabs_(u) <= L.size[0] * 0.5f && fabs_(v) <= L.size[1] * 0.5f;
+  const float u = dot(th, mk(L.right[0], L.right[1], L.right[2]));
+  const float v = dot(th, mk(L.up[0], L.up[1], L.up[2]));
+  return fabs_(u) <= L.half[0] && fabs_(v) <= L.half[1];
 }
 
 // sampleSphere (:246-253)
@@ -172,7 +168,9 @@ __device__ __forceinline__ v3 sample_sphere(uint32_t* rng) {
   const float z = 2.0f * rng_next(rng) - 1.0f;
   const float th = (2.0f * 0x1.921fb6p+1f) * rng_next(rng);
   const float r = sqrt_(1.0f - z * z);
-  return mk(r * cos_(th), r * sin_(th), z);
+  float sn, cs;
+  sincos_(th, &sn, &cs);
+  return mk(r * cs, r * sn, z);
 }
 
 // sampleHemisphere (:229-243)
@@ -181,8 +179,10 @@ __device__ __forceinline__ v3 sample_hemisphere(v3 n, uint32_t* rng) {
   const float r2 = rng_next(rng);
   const float th = acos_(sqrt_(1.0f - r1));
   const float ph = (2.0f * 0x1.921fb6p+1f) * r2;
-  const float st = sin_(th);
-  const v3 l = mk(st * cos_(ph), st * sin_(ph), cos_(th));
+  float st, ct, sp, cp;
+  sincos_(th, &st, &ct);
+  sincos_(ph, &sp, &cp);
+  const v3 l = mk(st * cp, st * sp, ct);
   const v3 upv = fabs_(n.z) < 0.999f ? mk(0.0f, 0.0f, 1.0f) : mk(1.0f, 0.0f, 0.0f);
   const v3 t = normalize(cross(upv, n));
   const v3 b = cross(n, t);
@@ -214,7 +214,7 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
   bool have_h0 = false;
   Ctr c0 = {0u, 0u, 0u};
   for (int i = 0; i < P.n_lights; ++i) {                // :311-328
-    const LightRec L = P.lights[i];
+    const LightDev L = P.lights[i];
     float tl;
     if (intersect_area_light(ro, rd, L, &tl)) {
       if (!have_h0) {
@@ -222,7 +222,7 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
         have_h0 = true;
       }
       if (STATS) add_ctr(c, c0);
-      if (h0.tri < 0 || h0.t > tl) return mk(L.intensity[0], L.intensity[1], L.intensity[2]);
+      if (h0.tri < 0 || h0.t > tl) return mk(L.inten[0], L.inten[1], L.inten[2]);
     }
   }
 
@@ -248,14 +248,14 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
     const v3 albedo = mk(0.8f, 0.8f, 0.8f);
     v3 direct = mk(0.0f, 0.0f, 0.0f);
     for (int i = 0; i < P.n_lights; ++i) {              // :345-366
-      const LightRec L = P.lights[i];
+      const LightDev L = P.lights[i];
       const v3 lp = sample_area_light(L, &rng);
       const v3 ld = normalize(sub(lp, hp));
       const float diff = fmax_(dot(hn, ld), 0.0f);
       const float dist = length(sub(lp, hp));
       if (!occluded<STATS>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c)) {
         const float d2 = dist * dist;
-        const v3 contrib = muls(muls(mk(L.intensity[0], L.intensity[1], L.intensity[2]), diff), 1.0f / fmax_(d2, 0.01f));
+        const v3 contrib = muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), 1.0f / fmax_(d2, 0.01f));
         direct = add(direct, mul(albedo, contrib));
       }
     }
@@ -274,14 +274,14 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
       const v3 sn = tri_normal(P, sh.tri);
       v3 sl = mk(0.0f, 0.0f, 0.0f);
       for (int i = 0; i < P.n_lights; ++i) {
-        const LightRec L = P.lights[i];
+        const LightDev L = P.lights[i];
         const v3 lp = sample_area_light(L, &rng);
         const v3 ed = normalize(sub(lp, cp));
         const float ediff = fmax_(dot(sn, ed), 0.0f);
         const float edist = length(sub(lp, cp));
         if (!occluded<STATS>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c)) {
           const float d2 = edist * edist;
-          sl = add(sl, muls(mul(muls(sss_albedo, ediff), mk(L.intensity[0], L.intensity[1], L.intensity[2])),
+          sl = add(sl, muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])),
                             1.0f / fmax_(d2, 0.01f)));
         }
       }
@@ -299,16 +299,35 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
   return rad;
 }
 
+// Values every lane computes identically (from kernel arguments only): read
+// lane 0's bits into an SGPR so the compiler keeps one scalar copy.
+__device__ __forceinline__ float uniform(float x) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+__device__ __forceinline__ v3 uniform(v3 a) { return mk(uniform(a.x), uniform(a.y), uniform(a.z)); }
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
 
-template <bool STATS>
+// LDS=true stages the whole scene (threaded nodes + triangle records) in LDS
+// once per workgroup; chosen by the host for scenes of at most a few tens of
+// KB (box.obj is 1.3 KB), where every lane re-reads the same few nodes.
+template <bool STATS, bool LDS>
 __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
-  const int blk = (int)blockIdx.x * P.nranks + P.rank;
   const int tid = (int)threadIdx.x;
+  if (LDS) {
+    extern __shared__ float4 lds_scene[];
+    const int nn = 2 * P.n_nodes, nt = 3 * P.n_tris;
+    for (int i = tid; i < nn; i += 256) lds_scene[i] = P.nodes[i];
+    for (int i = tid; i < nt; i += 256) lds_scene[nn + i] = P.tris[i];
+    __syncthreads();
+    P.nodes = lds_scene;
+    P.tris = lds_scene + nn;
+  }
+  const int blk = (int)blockIdx.x * P.nranks + P.rank;
   const int wave = tid >> 6, lane = tid & 63;
   const int bx = blk % P.blocks_x, by = blk / P.blocks_x;
   const int px = bx * 16 + (wave & 1) * 8 + (lane & 7);
@@ -325,9 +344,10 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
     const float ndcX0 = (2.0f * (float)px / (float)W) - 1.0f;
     const float ndcY0 = (2.0f * (float)py / (float)H) - 1.0f;
     const float aspect = (float)W / (float)H;
-    const v3 right = normalize(cross(cdir, neg(cup)));
-    const v3 up = normalize(cross(right, cdir));
-    const float tanFov = tan_(radians_(P.fov * 0.5f));
+    // Camera frame: identical in every lane, so keep one copy in SGPRs.
+    const v3 right = uniform(normalize(cross(cdir, neg(cup))));
+    const v3 up = uniform(normalize(cross(right, cdir)));
+    const float tanFov = uniform(tan_(radians_(P.fov * 0.5f)));
     const size_t pix = (size_t)py * (size_t)W + (size_t)px;
     float4 acc = P.accum[pix];
     for (uint32_t s = 0; s < P.n_batches; ++s) {
@@ -339,14 +359,17 @@ __global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
       float u2 = rng_next(&rng);
       float r = sqrt_(-2.0f * log_(u1));
       float th = (2.0f * 0x1.921fb6p+1f) * u2;
-      const float ax = (r * cos_(th)) * 0.02f;
-      const float ay = (r * sin_(th)) * 0.02f;
+      float sn, cs;
+      sincos_(th, &sn, &cs);
+      const float ax = (r * cs) * 0.02f;
+      const float ay = (r * sn) * 0.02f;
       const v3 origin = add(add(cpos, muls(right, ax)), muls(up, ay));   // :448
       u1 = fmax_(1e-38f, rng_next(&rng));
       u2 = rng_next(&rng);
       r = sqrt_(-2.0f * log_(u1));
       th = (2.0f * 0x1.921fb6p+1f) * u2;
-      const float jx = r * cos_(th), jy = r * sin_(th);
+      sincos_(th, &sn, &cs);
+      const float jx = r * cs, jy = r * sn;
       const float ndcX = ndcX0 + (jx * 0.5f) / (float)W;                 // :453-454
       const float ndcY = ndcY0 + (jy * 0.5f) / (float)H;
       const v3 base = normalize(sub(add(cdir, muls(neg(right), (ndcX * tanFov) * aspect)), muls(up, ndcY * tanFov)));
@@ -386,6 +409,34 @@ __global__ __launch_bounds__(256) void setup_tris_kernel(const float* __restrict
   out[3 * t + 0] = make_float4(v0.x, v0.y, v0.z, e1.x);
   out[3 * t + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
   out[3 * t + 2] = make_float4(e2.z, n.x, n.y, n.z);
+}
+
+// Per-light constants of sampleAreaLight / intersectAreaLight (:261-264,
+// :284-287, :295-296), computed with the shader's ops.
+__global__ __launch_bounds__(64) void setup_lights_kernel(const LightRec* __restrict__ in, int n,
+                                                          LightDev* __restrict__ out) {
+  const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (i >= n) return;
+  const LightRec L = in[i];
+  const v3 nr = mk(L.normal[0], L.normal[1], L.normal[2]);
+  const v3 nn = normalize(nr);
+  const v3 basis = fabs_(nn.y) < 0.999f ? mk(0.0f, 1.0f, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+  const v3 right = normalize(cross(nn, basis));
+  const v3 up = cross(right, nn);
+  LightDev d;
+  for (int c = 0; c < 3; ++c) {
+    d.pos[c] = L.position[c];
+    d.nraw[c] = L.normal[c];
+    d.inten[c] = L.intensity[c];
+  }
+  d.right[0] = right.x; d.right[1] = right.y; d.right[2] = right.z;
+  d.up[0] = up.x; d.up[1] = up.y; d.up[2] = up.z;
+  d.size[0] = L.size[0];
+  d.size[1] = L.size[1];
+  d.half[0] = L.size[0] * 0.5f;
+  d.half[1] = L.size[1] * 0.5f;
+  d.pad = 0.0f;
+  out[i] = d;
 }
 
 __global__ __launch_bounds__(256) void clear_kernel(float4* accum, int W, int H, int nranks, int rank) {
@@ -434,6 +485,12 @@ hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices,
   return hipGetLastError();
 }
 
+hipError_t launch_setup_lights(const LightRec* d_in, int n, LightDev* d_out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  setup_lights_kernel<<<(n + 63) / 64, 64, 0, stream>>>(d_in, n, d_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_clear(float4* accum, int width, int height, int nranks, int rank, hipStream_t stream) {
   const size_t n = (size_t)width * (size_t)height;
   if (n == 0) return hipSuccess;
@@ -441,13 +498,22 @@ hipError_t launch_clear(float4* accum, int width, int height, int nranks, int ra
   return hipGetLastError();
 }
 
-hipError_t launch_render(const RenderParams& p, bool stats, hipStream_t stream) {
+hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, hipStream_t stream) {
   const int grid = (p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;   // blocks b = rank + i*nranks
   if (grid <= 0 || p.n_batches == 0) return hipSuccess;
-  if (stats)
-    render_kernel<true><<<grid, 256, 0, stream>>>(p);
-  else
-    render_kernel<false><<<grid, 256, 0, stream>>>(p);
+  const size_t lds = scene_lds_bytes(p);
+  if (lds_scene && lds > kMaxSceneLds) return hipErrorInvalidValue;
+  if (lds_scene) {
+    if (stats)
+      render_kernel<true, true><<<grid, 256, lds, stream>>>(p);
+    else
+      render_kernel<false, true><<<grid, 256, lds, stream>>>(p);
+  } else {
+    if (stats)
+      render_kernel<true, false><<<grid, 256, 0, stream>>>(p);
+    else
+      render_kernel<false, false><<<grid, 256, 0, stream>>>(p);
+  }
   return hipGetLastError();
 }
 

@@ -135,6 +135,19 @@ PT_FN float cos_(float x) {
     default: return ksin_(r);
   }
 }
+// sin and cos of one argument sharing the reduction: bitwise the same as
+// sin_(x) and cos_(x).
+PT_FN void sincos_(float x, float* s, float* c) {
+  int q;
+  const float r = reduce_(x, &q);
+  const float ks = ksin_(r), kc = kcos_(r);
+  switch (q & 3) {
+    case 0: *s = ks; *c = kc; break;
+    case 1: *s = kc; *c = -ks; break;
+    case 2: *s = -ks; *c = -kc; break;
+    default: *s = -kc; *c = ks; break;
+  }
+}
 PT_FN float tan_(float x) { return sin_(x) / cos_(x); }
 
 // ---------------------------------------------------------------- acosf ----

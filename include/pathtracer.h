@@ -136,6 +136,13 @@ int pt_render(pt_context* ctx, uint32_t first_batch, uint32_t n_batches);
  * reduction of all ranks' buffers is bit-identical to a single-GPU frame. */
 int pt_set_partition(pt_context* ctx, int nranks, int rank);
 
+/* ---- kernel options ---------------------------------------------------- */
+/* PT_OPT_SCENE_IN_LDS: stage the scene in LDS per workgroup — 0 never,
+ * 1 when it fits in 48 KB (default), 2 always (error if it does not fit).
+ * Output is identical either way. */
+#define PT_OPT_SCENE_IN_LDS 1
+int pt_set_option(pt_context* ctx, int key, int value);
+
 /* ---- instrumentation --------------------------------------------------- */
 /* Stats mode runs the reference-exhaustive traversal with counters (output is
  * unchanged); used for the roofline's algorithmic byte count. */

@@ -16,8 +16,10 @@ pytestmark = pytest.mark.gpu
 TOL = 1e-4   # north_star per-channel tolerance; every assertion below is stricter (bitwise)
 
 
-def _setup(v, i, n, cam=scenes.DEFAULT_CAMERA, lights=scenes.REFERENCE_LIGHT, depth=4, sss=3, int_bits=False):
+def _setup(v, i, n, cam=scenes.DEFAULT_CAMERA, lights=scenes.REFERENCE_LIGHT, depth=4, sss=3, int_bits=False,
+           lds=1):
     r = ptamd.Renderer(0)
+    r.set_option(ptamd.PT_OPT_SCENE_IN_LDS, lds)
     r.upload_scene(v, i, n, int_bits=int_bits)
     r.upload_lights(lights)
     r.set_camera(cam)
@@ -46,10 +48,11 @@ def _assert_same(gpu, ref, what=""):
                              f"first at pixel {bad[0] // 4} gpu={gpu[bad[0]]} ref={ref[bad[0]]}")
 
 
+@pytest.mark.parametrize("lds", [0, 2])
 @pytest.mark.parametrize("W,H,depth,nb", [(256, 256, 1, 1), (256, 256, 4, 1), (64, 48, 4, 8), (17, 13, 4, 3)])
-def test_box_matches_oracle(W, H, depth, nb):
+def test_box_matches_oracle(W, H, depth, nb, lds):
     v, i, n = _box()
-    r = _setup(v, i, n, depth=depth)
+    r = _setup(v, i, n, depth=depth, lds=lds)
     r.resize_and_clear(W, H)
     r.render(0, nb)
     gpu = r.read_accum()
@@ -75,10 +78,11 @@ def test_dispatch_sequence_equals_fused_render():
     _assert_same(r.read_accum(), seq, "render(0,2)+render(2,3)")
 
 
-def test_stats_mode_counts_and_output():
+@pytest.mark.parametrize("lds", [0, 2])
+def test_stats_mode_counts_and_output(lds):
     v, i, n = _box()
     W, H, nb = 128, 96, 3
-    r = _setup(v, i, n)
+    r = _setup(v, i, n, lds=lds)
     r.resize_and_clear(W, H)
     r.render(0, nb)
     plain = r.read_accum()
@@ -95,10 +99,11 @@ def test_stats_mode_counts_and_output():
     assert st["samples"] == W * H * nb
 
 
-def test_box_1080p_8spp_full_frame():
+@pytest.mark.parametrize("lds", [0, 1])
+def test_box_1080p_8spp_full_frame(lds):
     """The bench configuration (BASELINE.json configs[1]) compared in full."""
     v, i, n = _box()
-    r = _setup(v, i, n)
+    r = _setup(v, i, n, lds=lds)
     r.resize_and_clear(1920, 1080)
     r.render(0, 8)
     gpu = r.read_accum()
@@ -168,12 +173,13 @@ def test_edge_params():
         _assert_same(r.read_accum(), ref, f"depth={depth} sss={sss} lights={lights.size // 16}")
 
 
-def test_displaced_sphere_substitute():
+@pytest.mark.parametrize("lds", [0, 1])
+def test_displaced_sphere_substitute(lds):
     sv, si = scenes.displaced_sphere(3)
     s = ptamd.Scene.from_arrays(sv, si).build_bvh()
     v, i, n, _, _ = s.arrays()
     cam = scenes.camera((0.0, 0.5, 3.0))
-    r = _setup(v, i, n, cam=cam)
+    r = _setup(v, i, n, cam=cam, lds=lds)
     r.resize_and_clear(80, 60)
     r.render(0, 2)
     ref, _ = _oracle(v, i, n, 80, 60, nb=2, cam=cam)
