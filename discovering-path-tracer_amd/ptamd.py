@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libptamd.so")
+LIB_PATH = os.environ.get("PTAMD_LIB") or os.path.join(HERE, "libptamd.so")   # override: A/B of builds
 
 PT_OK = 0
 PT_NODES_INT_BITS = 0x1

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--w", type=int, default=1920)
     ap.add_argument("--h", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=8)
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     scene, cam = load_scene(a.scene)
@@ -44,21 +45,27 @@ def main():
     for spec in a.variants:
         name, _, kv = spec.partition(":")
         r = ptamd.Renderer(0)
+        depth, sss = 4, 3
         for item in filter(None, kv.split(",")):
             k, v = item.split("=")
-            key = ptamd.PT_OPT_SCENE_IN_LDS if k == "lds" else int(k[3:])
-            r.set_option(key, int(v))
+            if k == "depth":
+                depth = int(v)
+            elif k == "sss":
+                sss = int(v)
+            else:
+                key = ptamd.PT_OPT_SCENE_IN_LDS if k == "lds" else int(k[3:])
+                r.set_option(key, int(v))
         r.upload(scene)
         r.upload_lights(scenes.REFERENCE_LIGHT)
         r.set_camera(cam)
-        r.set_params(4, 3)
+        r.set_params(depth, sss)
         r.resize_and_clear(a.w, a.h)
         rs.append((name, r))
     ref = None
     for name, r in rs:
         r.render(0, a.spp)   # warm + parity between variants
         img = r.read_accum()
-        if ref is None:
+        if ref is None or a.no_parity:
             ref = img
         elif not np.array_equal(img.view(np.uint32), ref.view(np.uint32)):
             print(f"WARNING: variant {name} output differs from {rs[0][0]}")
