@@ -123,14 +123,46 @@ int thread_bvh(const pt_bvh_node* nodes, size_t n, bool int_bits, size_t n_tris,
   return PT_OK;
 }
 
+// Drops internal nodes flagged as implied-hit from a threaded array: such a
+// node does nothing but continue at k+1, so every link into it can point at
+// the next kept node instead.  The kept nodes' visit sequence (and every slab
+// and triangle test) is unchanged; only the pass-through visits disappear.
+// Used by the fast kernel; stats mode keeps the full array so it still counts
+// the reference's node visits.
+void collapse_implied(const std::vector<float4>& full, std::vector<float4>* out) {
+  const size_t m = full.size() / 2;
+  auto raw_skip = [&](size_t k) { int32_t s; memcpy(&s, &full[2 * k].w, 4); return s; };
+  auto tri_of = [&](size_t k) { int32_t t; memcpy(&t, &full[2 * k + 1].w, 4); return t; };
+  auto dropped = [&](size_t k) { return raw_skip(k) < 0 && tri_of(k) < 0; };
+  std::vector<int32_t> nxt(m + 1);
+  int32_t kept = 0;
+  for (size_t k = 0; k < m; ++k)
+    if (!dropped(k)) ++kept;
+  nxt[m] = kept;
+  for (size_t k = m; k-- > 0;) nxt[k] = dropped(k) ? nxt[k + 1] : --kept;
+  out->clear();
+  out->reserve(2 * (size_t)nxt[m]);
+  for (size_t k = 0; k < m; ++k) {
+    if (dropped(k)) continue;
+    const int32_t raw = raw_skip(k);
+    const int32_t skip = (int32_t)((uint32_t)nxt[raw & 0x7fffffff] | ((uint32_t)raw & 0x80000000u));
+    float4 a = full[2 * k];
+    memcpy(&a.w, &skip, 4);
+    out->push_back(a);
+    out->push_back(full[2 * k + 1]);
+  }
+}
+
 }  // namespace
 
 struct pt_context {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
-  float4* d_nodes = nullptr;
+  float4* d_nodes = nullptr;        // threaded, implied internal nodes collapsed (fast kernel)
   int n_nodes = 0;
+  float4* d_nodes_full = nullptr;   // threaded, every reference node (stats mode)
+  int n_nodes_full = 0;
   float4* d_tris = nullptr;
   int n_tris = 0;
   ptd::LightRec* d_lights = nullptr;
@@ -205,6 +237,7 @@ int pt_destroy(pt_context* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   dev_free(c->d_nodes);
+  dev_free(c->d_nodes_full);
   dev_free(c->d_tris);
   dev_free(c->d_lights);
   dev_free(c->d_lights_dev);
@@ -248,29 +281,35 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   const size_t nv = n_vertex_floats / 3;
   for (size_t i = 0; i < n_indices; ++i)
     if (indices[i] >= nv) return fail(PT_ERR_SCENE, "vertex index out of range at " + std::to_string(i));
-  std::vector<float4> threaded;
+  std::vector<float4> threaded, collapsed;
   int rc = thread_bvh(nodes, n_nodes, (flags & PT_NODES_INT_BITS) != 0, n_indices / 3, &threaded);
   if (rc) return rc;
+  collapse_implied(threaded, &collapsed);
   PT_HIP(hipSetDevice(c->device));
   PT_HIP(hipStreamSynchronize(c->stream));
   dev_free(c->d_nodes);
+  dev_free(c->d_nodes_full);
   dev_free(c->d_tris);
   c->has_scene = false;
   const int T = (int)(n_indices / 3);
-  float* d_v = nullptr;
-  uint32_t* d_i = nullptr;
-  PT_HIP(hipMalloc((void**)&c->d_nodes, threaded.size() * sizeof(float4)));
+  struct Staging {   // vertex/index copies live only until the triangle records are built
+    float* v = nullptr;
+    uint32_t* i = nullptr;
+    ~Staging() { if (v) (void)hipFree(v); if (i) (void)hipFree(i); }
+  } st;
+  PT_HIP(hipMalloc((void**)&c->d_nodes, collapsed.size() * sizeof(float4)));
+  PT_HIP(hipMalloc((void**)&c->d_nodes_full, threaded.size() * sizeof(float4)));
   PT_HIP(hipMalloc((void**)&c->d_tris, (size_t)T * 3 * sizeof(float4)));
-  PT_HIP(hipMalloc((void**)&d_v, n_vertex_floats * sizeof(float) + 16));
-  PT_HIP(hipMalloc((void**)&d_i, n_indices * sizeof(uint32_t)));
-  PT_HIP(hipMemcpyAsync(c->d_nodes, threaded.data(), threaded.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
-  PT_HIP(hipMemcpyAsync(d_v, vertices, n_vertex_floats * sizeof(float), hipMemcpyHostToDevice, c->stream));
-  PT_HIP(hipMemcpyAsync(d_i, indices, n_indices * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
-  PT_HIP(ptd::launch_setup_tris(d_v, d_i, T, c->d_tris, c->stream));
+  PT_HIP(hipMalloc((void**)&st.v, n_vertex_floats * sizeof(float) + 16));
+  PT_HIP(hipMalloc((void**)&st.i, n_indices * sizeof(uint32_t)));
+  PT_HIP(hipMemcpyAsync(c->d_nodes, collapsed.data(), collapsed.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  PT_HIP(hipMemcpyAsync(c->d_nodes_full, threaded.data(), threaded.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+  PT_HIP(hipMemcpyAsync(st.v, vertices, n_vertex_floats * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  PT_HIP(hipMemcpyAsync(st.i, indices, n_indices * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
+  PT_HIP(ptd::launch_setup_tris(st.v, st.i, T, c->d_tris, c->stream));
   PT_HIP(hipStreamSynchronize(c->stream));
-  (void)hipFree(d_v);
-  (void)hipFree(d_i);
-  c->n_nodes = (int)(threaded.size() / 2);
+  c->n_nodes = (int)(collapsed.size() / 2);
+  c->n_nodes_full = (int)(threaded.size() / 2);
   c->n_tris = T;
   c->has_scene = true;
   return PT_OK;
@@ -377,12 +416,12 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   if (!c->has_camera) return fail(PT_ERR_INVALID, "no camera set");
   if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
   ptd::RenderParams p;
-  p.nodes = c->d_nodes;
+  p.nodes = c->stats_mode ? c->d_nodes_full : c->d_nodes;
   p.tris = c->d_tris;
   p.lights = c->d_lights_dev;
   p.accum = c->d_accum;
   p.stats = c->d_stats;
-  p.n_nodes = c->n_nodes;
+  p.n_nodes = c->stats_mode ? c->n_nodes_full : c->n_nodes;
   p.n_tris = c->n_tris;
   p.n_lights = c->n_lights;
   p.width = c->width;

@@ -339,7 +339,10 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 // once per workgroup; chosen by the host for scenes of at most a few tens of
 // KB (box.obj is 1.3 KB), where every lane re-reads the same few nodes.
 template <bool STATS, bool LDS>
-__global__ __launch_bounds__(256) void render_kernel(RenderParams P) {
+#ifndef PT_RENDER_MIN_BLOCKS
+#define PT_RENDER_MIN_BLOCKS 5
+#endif
+__global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(RenderParams P) {
   const int tid = (int)threadIdx.x;
   if (LDS) {
     extern __shared__ float4 lds_scene[];
