@@ -47,6 +47,7 @@ struct RenderParams {
   float cam_pos[3], cam_dir[3], cam_up[3], fov;
   int blocks_x, blocks_total;   // 16x16-pixel blocks
   int nranks, rank;             // block b is rendered iff b % nranks == rank
+  int spl;                      // sample lanes per pixel: 1, 2, 4 or 8
 };
 
 hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices, int n_tris, float4* d_tris,

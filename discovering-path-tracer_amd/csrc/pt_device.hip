@@ -353,17 +353,43 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
     P.nodes = lds_scene;
     P.tris = lds_scene + nn;
   }
-  const int blk = (int)blockIdx.x * P.nranks + P.rank;
+  // Work mapping.  A 16x16 pixel tile (the partition unit) is split into
+  // SPL workgroups; lane l of wave w handles pixel q = w*(64/SPL) + l/SPL of
+  // its workgroup and sample slot j = l % SPL, so the SPL lanes of a pixel
+  // trace that pixel's samples side by side: coherent rays, and SPL times
+  // finer work granularity than one pixel per thread, which is what keeps a
+  // tile-split frame fast on 8 GPUs (pixels on geometry cost ~10x the others).
+  // A persistent variant pulling wave-sized items from per-XCD queues was
+  // measured slower at every SPL, on 1 GPU and on a 1/8 tile share.
+  const int spl = P.spl;
+  const int tile = ((int)blockIdx.x / spl) * P.nranks + P.rank;
+  const int part = (int)blockIdx.x % spl;
   const int wave = tid >> 6, lane = tid & 63;
   __shared__ int cand_buf[4][kCand][64];
+  __shared__ float4 col_buf[4][64];
   int* cand = &cand_buf[wave][0][lane];
-  const int bx = blk % P.blocks_x, by = blk / P.blocks_x;
-  const int px = bx * 16 + (wave & 1) * 8 + (lane & 7);
-  const int py = by * 16 + (wave >> 1) * 8 + (lane >> 3);
-  const bool active = blk < P.blocks_total && px < P.width && py < P.height;   // :425-428
+  const int q = wave * (64 / spl) + lane / spl;       // pixel within the workgroup
+  const int j = lane % spl;                           // sample slot
+  const int bx = tile % P.blocks_x, by = tile / P.blocks_x;
+  const int px = bx * 16 + q % 16;
+  const int py = by * 16 + part * (16 / spl) + q / 16;
+  const bool active = tile < P.blocks_total && px < P.width && py < P.height;   // :425-428
   Ctr c = {0u, 0u, 0u};
+  const int W = P.width, H = P.height;
+  const size_t pix = (size_t)py * (size_t)W + (size_t)px;
+  uint32_t nsamp = 0;
+  if (active && (uint32_t)j < P.n_batches)
+    nsamp = (P.n_batches - (uint32_t)j + (uint32_t)spl - 1) / (uint32_t)spl;
+  // Running mean (:467-469): lane j of a pixel folds channels c = j (mod spl)
+  // of that pixel, sample by sample in batch order.
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   if (active) {
-    const int W = P.width, H = P.height;
+    const float* a = (const float*)&P.accum[pix];
+#pragma unroll
+    for (int ch = 0; ch < 4; ++ch)
+      if (ch % spl == j) acc[ch] = a[ch];
+  }
+  {
     const v3 cpos = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     const v3 cdir = mk(P.cam_dir[0], P.cam_dir[1], P.cam_dir[2]);
     const v3 cup = mk(P.cam_up[0], P.cam_up[1], P.cam_up[2]);
@@ -376,9 +402,10 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
     const v3 right = uniform(normalize(cross(cdir, neg(cup))));
     const v3 up = uniform(normalize(cross(right, cdir)));
     const float tanFov = uniform(tan_(radians_(P.fov * 0.5f)));
-    const size_t pix = (size_t)py * (size_t)W + (size_t)px;
-    float4 acc = P.accum[pix];
-    for (uint32_t s = 0; s < P.n_batches; ++s) {
+    for (uint32_t base = 0; base < P.n_batches; base += (uint32_t)spl) {
+     const uint32_t s = base + (uint32_t)j;
+     float4 col4 = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+     if (active && s < P.n_batches) {
       const uint32_t batch = P.first_batch + s;
       const uint32_t seed = (batch * (uint32_t)H + (uint32_t)py) * (uint32_t)W + (uint32_t)px;   // :435
       uint32_t rng = seed;
@@ -400,21 +427,43 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
       const float jx = r * cs, jy = r * sn;
       const float ndcX = ndcX0 + (jx * 0.5f) / (float)W;                 // :453-454
       const float ndcY = ndcY0 + (jy * 0.5f) / (float)H;
-      const v3 base = normalize(sub(add(cdir, muls(neg(right), (ndcX * tanFov) * aspect)), muls(up, ndcY * tanFov)));
-      const v3 focal = add(cpos, muls(base, 3.0f));                       // :459
+      const v3 bdir = normalize(sub(add(cdir, muls(neg(right), (ndcX * tanFov) * aspect)), muls(up, ndcY * tanFov)));
+      const v3 focal = add(cpos, muls(bdir, 3.0f));                       // :459
       const v3 dir = normalize(sub(focal, origin));                       // :460
       const v3 col = path_trace<STATS>(P, origin, dir, seed, c, cand);
-      const float fb = (float)batch, fb1 = (float)(batch + 1u);           // :468
-      acc.x = (acc.x * fb + col.x) / fb1;
-      acc.y = (acc.y * fb + col.y) / fb1;
-      acc.z = (acc.z * fb + col.z) / fb1;
-      acc.w = (acc.w * fb + 1.0f) / fb1;
+      col4 = make_float4(col.x, col.y, col.z, 1.0f);                      // vec4(color, 1.0)
+     }
+     // hand the chunk's colours to the folding lanes of the same pixel
+     col_buf[wave][lane] = col4;
+     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+     __builtin_amdgcn_wave_barrier();
+     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+     if (active) {
+      const uint32_t m = min((uint32_t)spl, P.n_batches - base);
+      const int first_lane = lane - j;
+      for (uint32_t t = 0; t < m; ++t) {
+        const uint32_t batch = P.first_batch + base + t;
+        const float fb = (float)batch, fb1 = (float)(batch + 1u);          // :468
+        const float* cc = (const float*)&col_buf[wave][first_lane + (int)t];
+#pragma unroll
+        for (int ch = 0; ch < 4; ++ch)
+          if (ch % spl == j) acc[ch] = (acc[ch] * fb + cc[ch]) / fb1;
+      }
+     }
+     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+     __builtin_amdgcn_wave_barrier();
+     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    P.accum[pix] = acc;
+  }
+  if (active) {
+    float* a = (float*)&P.accum[pix];
+#pragma unroll
+    for (int ch = 0; ch < 4; ++ch)
+      if (ch % spl == j) a[ch] = acc[ch];
   }
   if (STATS) {
     const unsigned long long rays = wave_sum(c.rays), nodes = wave_sum(c.nodes), leaves = wave_sum(c.leaves);
-    const unsigned long long smp = wave_sum(active ? (unsigned long long)P.n_batches : 0ull);
+    const unsigned long long smp = wave_sum((unsigned long long)nsamp);
     if (lane == 0) {
       atomicAdd(&P.stats[0], rays);
       atomicAdd(&P.stats[1], nodes);
@@ -527,21 +576,16 @@ hipError_t launch_clear(float4* accum, int width, int height, int nranks, int ra
 }
 
 hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, hipStream_t stream) {
-  const int grid = (p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;   // blocks b = rank + i*nranks
+  if (p.spl != 1 && p.spl != 2 && p.spl != 4 && p.spl != 8) return hipErrorInvalidValue;
+  // owned tiles b = rank + i*nranks, each split into spl workgroups
+  const long long grid = (long long)(p.blocks_total + p.nranks - 1 - p.rank) / p.nranks * p.spl;
   if (grid <= 0 || p.n_batches == 0) return hipSuccess;
-  const size_t lds = scene_lds_bytes(p);
-  if (lds_scene && lds > kMaxSceneLds) return hipErrorInvalidValue;
-  if (lds_scene) {
-    if (stats)
-      render_kernel<true, true><<<grid, 256, lds, stream>>>(p);
-    else
-      render_kernel<false, true><<<grid, 256, lds, stream>>>(p);
-  } else {
-    if (stats)
-      render_kernel<true, false><<<grid, 256, 0, stream>>>(p);
-    else
-      render_kernel<false, false><<<grid, 256, 0, stream>>>(p);
-  }
+  if (grid > 0x7fffffffll) return hipErrorInvalidValue;
+  const size_t lds = lds_scene ? scene_lds_bytes(p) : 0;
+  if (lds > kMaxSceneLds) return hipErrorInvalidValue;
+  void (*kern)(RenderParams) = lds_scene ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
+                                         : (stats ? render_kernel<true, false> : render_kernel<false, false>);
+  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), lds, stream, p);
   return hipGetLastError();
 }
 

@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("PTAMD_LIB") or os.path.join(HERE, "libptamd.so")   # 
 PT_OK = 0
 PT_NODES_INT_BITS = 0x1
 PT_OPT_SCENE_IN_LDS = 1
+PT_OPT_SAMPLE_LANES = 2
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).
 EXPORTS = [

@@ -141,6 +141,10 @@ int pt_set_partition(pt_context* ctx, int nranks, int rank);
  * 1 when it fits in 48 KB (default), 2 always (error if it does not fit).
  * Output is identical either way. */
 #define PT_OPT_SCENE_IN_LDS 1
+/* PT_OPT_SAMPLE_LANES: lanes that trace one pixel's samples side by side in
+ * pt_render — 0 auto (min(n_batches, 8) rounded down to 1/2/4/8), or 1, 2, 4, 8.
+ * Output is identical for every value. */
+#define PT_OPT_SAMPLE_LANES 2
 int pt_set_option(pt_context* ctx, int key, int value);
 
 /* ---- instrumentation --------------------------------------------------- */

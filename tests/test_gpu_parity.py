@@ -61,6 +61,20 @@ def test_box_matches_oracle(W, H, depth, nb, lds):
     assert np.all(np.abs(gpu - ref) <= TOL)
 
 
+@pytest.mark.parametrize("spl", [1, 2, 4, 8])
+@pytest.mark.parametrize("nb", [1, 3, 8, 13])
+def test_sample_lanes(spl, nb):
+    """Every sample-lane mapping gives the oracle's frame, including sample
+    counts that are not multiples of the lane count and ragged tiles."""
+    v, i, n = _box()
+    r = _setup(v, i, n)
+    r.set_option(ptamd.PT_OPT_SAMPLE_LANES, spl)
+    r.resize_and_clear(40, 27)
+    r.render(2, nb)
+    ref, _ = _oracle(v, i, n, 40, 27, first=2, nb=nb)
+    _assert_same(r.read_accum(), ref, f"spl={spl} nb={nb}")
+
+
 def test_dispatch_sequence_equals_fused_render():
     v, i, n = _box()
     r = _setup(v, i, n)

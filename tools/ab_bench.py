@@ -52,6 +52,8 @@ def main():
                 depth = int(v)
             elif k == "sss":
                 sss = int(v)
+            elif k == "nr":      # emulate one rank of an N-GPU tile split: nr=N (rank 0)
+                r.set_partition(int(v), 0)
             else:
                 key = ptamd.PT_OPT_SCENE_IN_LDS if k == "lds" else int(k[3:])
                 r.set_option(key, int(v))
