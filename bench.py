@@ -1,16 +1,23 @@
 #!/usr/bin/env python3
 """Benchmark: Mrays/s of the path-tracing pixel kernel on box.obj at
-1920x1080, 8 spp, 4 bounces (BASELINE.json configs[1]), 1..N GPUs.
+1920x1080, 8 spp, 4 bounces (BASELINE.json configs[1]), on 1..N GPUs.
 
-A step = one frame: clear the accumulation buffer, run the 8 sample batches
-(one fused launch, bit-identical to 8 progressive 1-spp dispatches) and, for
-N > 1, combine the ranks' screen tiles on rank 0 with one RCCL reduction.
-Mrays/s counts the reference's traceRay invocations (all kinds: light
-pre-pass, primary/bounce, shadow, SSS, SSS-shadow), measured by a stats-mode
-pass of the same frame before the timed region.
+A step is one frame.  It renders the 8 sample batches from a fresh
+accumulator in one fused launch, bit-identical to 8 progressive 1-spp
+dispatches after a clear.  For N > 1 the frame is split into 16x16 screen
+tiles (tile b on rank b % N).  Every rank packs its tiles and the root
+assembles them with one RCCL gather.  The gather of frame k overlaps the
+render of frame k+1 (double-buffered); the timed region ends only after the
+last frame is assembled.
+
+Mrays/s counts the reference's traceRay invocations of all kinds: light
+pre-pass, primary/bounce, shadow, SSS and SSS-shadow.  A stats-mode pass of
+the same frame, run before the timed region, measures them.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU).  Rank 0 prints one JSON line.
+torch.distributed.run, one process per GPU.  Rank 0 prints one JSON line.
+Other workloads: --scene sphere (the labelled Sylveon substitute) or
+--scene synthetic:<T> (SURVEY §8d config 5 cloud, camera at z=2.2).
 """
 import argparse
 import json
@@ -25,7 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "discovering-path-tracer_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-W, H, SPP, DEPTH, SSS = 1920, 1080, 8, 4, 3
+DEPTH, SSS = 4, 3
 
 
 def algorithmic_bytes(st):
@@ -33,6 +40,25 @@ def algorithmic_bytes(st):
     (12 B indices + 36 B vertices) under the reference's exhaustive traversal,
     + 32 B accumulation read-modify-write per pixel-sample."""
     return 32 * st["nodes"] + 48 * st["leaf_tests"] + 32 * st["samples"]
+
+
+def load_scene(name):
+    import ptamd
+    import scenes
+    if name == "box":
+        s = ptamd.Scene.load_obj(scenes.BOX_OBJ).build_bvh()
+        return s, scenes.DEFAULT_CAMERA, False, "box.obj"
+    if name == "sphere":
+        v, i = scenes.displaced_sphere(6)
+        s = ptamd.Scene.from_arrays(v, i).build_bvh()
+        return s, scenes.camera((0.0, 0.5, 3.0)), False, f"displaced icosphere ({i.size // 3} tris, Sylveon substitute)"
+    if name.startswith("synthetic:"):
+        t = int(name.split(":")[1])
+        v, i = scenes.random_triangles(t, seed=42)
+        big = 2 * t - 1 >= (1 << 24)
+        s = ptamd.Scene.from_arrays(v, i).build_bvh(int_bits=big)
+        return s, scenes.camera((0.0, 0.0, 2.2)), big, f"synthetic {t} random triangles, camera z=2.2"
+    raise SystemExit(f"unknown scene {name}")
 
 
 def profiled_traffic():
@@ -55,20 +81,20 @@ def profiled_traffic():
     return best
 
 
-def cpu_baseline(v, i, n, cam, light):
+def cpu_baseline(v, i, n, cam, light, W, H, spp):
     """The oracle (scalar C++ restatement of raytrace_comp.comp) on this host,
-    all cores, on a bounded sample: every 8th row of the same frame."""
+    all cores, on a bounded sample of the same workload."""
     import oracle_lib
     threads = min(16, os.cpu_count() or 1)
-    stride = 1
+    stride = 1 if W * H <= 1920 * 1080 else 4
     oracle_lib.render(v, i, n.reshape(-1), cam, light, 64, 64, n_batches=1, nthreads=threads)   # warm
     t0 = time.perf_counter()
-    _, st = oracle_lib.render(v, i, n.reshape(-1), cam, light, W, H, n_batches=SPP, max_depth=DEPTH,
+    _, st = oracle_lib.render(v, i, n.reshape(-1), cam, light, W, H, n_batches=spp, max_depth=DEPTH,
                               sss_bounces=SSS, row_stride=stride, row_phase=0, nthreads=threads)
     dt = time.perf_counter() - t0
     return {"value": round(float(st[0]) / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"the full {W}x{H}x{SPP}spp box frame (rows y%{stride}==0, {H // stride} rows, "
-                      f"{int(st[0])} rays, {dt:.2f} s, {threads} std::threads)"}
+            "sample": f"rows y%{stride}==0 of the same {W}x{H}x{spp}spp frame ({H // stride} rows, "
+                      f"{int(st[0])} rays, {dt:.2f} s, {threads} std::threads, oracle/pt_oracle.cpp)"}
 
 
 def main():
@@ -76,43 +102,56 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--scene", default="box")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=8)
+    ap.add_argument("--collective", choices=["gather", "reduce"], default="gather")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", action="store_true", help="N>1: compare the assembled frame with a 1-GPU render")
     args = ap.parse_args()
+    W, H, SPP = args.width, args.height, args.spp
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # Rehearsal knobs for a 1-GPU box: every rank on one device, gloo staged on the host.
+    device = int(os.environ.get("PT_BENCH_DEVICE", local))
+    backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
 
-    import torch   # load torch's HIP runtime first so libptamd shares it
+    import torch   # load torch's HIP runtime first so libptamd binds to the same one
     import ptamd
     import scenes
 
     dist = None
+    dev = torch.device("cuda", device)
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
 
-    scene = ptamd.Scene.load_obj(scenes.BOX_OBJ).build_bvh()
+    def allreduce_max(t):
+        if backend == "nccl":
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return t
+        c = t.cpu()
+        dist.all_reduce(c, op=dist.ReduceOp.MAX)
+        return c
+
+    scene, cam, int_bits, scene_desc = load_scene(args.scene)
     v, i, n, _, _ = scene.arrays()
-    cam, light = scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT
-    r = ptamd.Renderer(local)
-    r.upload_scene(v, i, n)
+    light = scenes.REFERENCE_LIGHT
+    r = ptamd.Renderer(device)
+    r.upload_scene(v, i, n, int_bits=int_bits)
     r.upload_lights(light)
     r.set_camera(cam)
     r.set_params(DEPTH, SSS)
     r.set_partition(world, rank)
-    frame = None
-    if world > 1:
-        # torch owns the accumulation buffer so RCCL can reduce it in place;
-        # the kernel runs on torch's current stream, ordering it with the collective.
-        frame = torch.empty((H, W, 4), dtype=torch.float32, device=f"cuda:{local}")
-        r.bind_accum(frame.data_ptr(), W, H)
-        r.set_stream(torch.cuda.current_stream().cuda_stream)
-    else:
-        r.resize_and_clear(W, H)
+    r.set_stream(torch.cuda.current_stream(dev).cuda_stream)   # order with torch's collectives
+    r.resize_and_clear(W, H)
 
     # Stats pass (untimed): the reference's exact traversal counts for one frame.
     r.set_stats_mode(True)
@@ -121,55 +160,127 @@ def main():
     r.render(0, SPP)
     st = r.stats()
     r.set_stats_mode(False)
-    counts = np.array([st["rays"], st["nodes"], st["leaf_tests"], st["samples"]], np.float64)
+    mine = np.array([st["rays"], st["nodes"], st["leaf_tests"], st["samples"]], np.float64)
+    counts = mine
     if dist is not None:
-        t = torch.tensor(counts, dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t)
+        t = torch.tensor(mine, dtype=torch.float64, device=dev)
+        if backend == "nccl":
+            dist.all_reduce(t)
+        else:
+            t = t.cpu()
+            dist.all_reduce(t)
         counts = t.cpu().numpy()
     rays_per_frame = float(counts[0])
-    tot = {"nodes": counts[1], "leaf_tests": counts[2], "samples": counts[3]}
 
-    def step():
-        r.clear()
-        r.render(0, SPP)
-        if dist is not None:
-            dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+    # --- the step ---------------------------------------------------------
+    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+    pending = []
+    finish = None
+    if dist is None:
+        def step():
+            r.render(0, SPP)
+    elif args.collective == "reduce":
+        r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 0)
+        frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+        r.bind_accum(frame.data_ptr(), W, H)
+
+        def step():
+            r.clear()                   # +0 owned, -0 elsewhere: the SUM is bit-exact
+            r.render(0, SPP)
+            if backend == "nccl":
+                dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+            else:
+                c = frame.cpu()
+                dist.reduce(c, dst=0, op=dist.ReduceOp.SUM)
+                if rank == 0:
+                    frame.copy_(c)
+    else:
+        max_own = int(allreduce_max(torch.tensor([r.tiles_owned()], dtype=torch.int64, device=dev)).item())
+        send = [torch.zeros((max_own, 256, 4), dtype=torch.float32, device=dev) for _ in range(2)]
+        recv = [[torch.empty((max_own, 256, 4), dtype=torch.float32, device=dev) for _ in range(world)]
+                for _ in range(2)] if rank == 0 else None
+        out = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+        state = {"k": 0}
+
+        def finish(work, buf):
+            if work is not None:
+                work.wait()
+            if rank == 0:
+                for src in range(world):
+                    r.tiles_unpack(recv[buf][src].data_ptr(), src, out.data_ptr())
+
+        def step():
+            buf = state["k"] % 2
+            state["k"] += 1
+            r.render(0, SPP)
+            r.tiles_pack(send[buf].data_ptr())
+            if backend == "nccl":
+                work = dist.gather(send[buf], recv[buf] if rank == 0 else None, dst=0, async_op=True)
+            else:
+                host = [torch.empty_like(x, device="cpu") for x in recv[buf]] if rank == 0 else None
+                dist.gather(send[buf].cpu(), host, dst=0)
+                if rank == 0:
+                    for x, h in zip(recv[buf], host):
+                        x.copy_(h)
+                work = None
+            pending.append((work, buf))
+            if len(pending) > 1:          # frame k-1 is assembled while frame k renders
+                finish(*pending.pop(0))
+
+    def drain():
+        while pending:
+            finish(*pending.pop(0))
 
     for _ in range(args.warmup):
         step()
+    drain()
     r.synchronize()
+    torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
-    torch.cuda.synchronize()
     r.reset_launch_times()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     r.synchronize()
-    torch.cuda.synchronize()
+    torch.cuda.synchronize(dev)
     if dist is not None:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
     kt = r.launch_times_ms()
     kernel_ms = float(np.mean(kt)) if kt.size else float("nan")
     if dist is not None:
-        t = torch.tensor([kernel_ms], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        kernel_ms = float(t.item())
+        t = allreduce_max(torch.tensor([dt, kernel_ms], dtype=torch.float64, device=dev))
+        dt, kernel_ms = float(t[0]), float(t[1])
+
+    verified = None
+    if args.verify and dist is not None and rank == 0:
+        # the assembled frame must be bitwise the single-GPU frame
+        ref = ptamd.Renderer(device)
+        ref.upload_scene(v, i, n, int_bits=int_bits)
+        ref.upload_lights(light)
+        ref.set_camera(cam)
+        ref.set_params(DEPTH, SSS)
+        ref.resize_and_clear(W, H)
+        ref.render(0, SPP)
+        want = ref.read_accum()
+        got = (out if args.collective == "gather" else frame).cpu().numpy().reshape(-1)
+        verified = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+        if not verified:
+            raise SystemExit("bench --verify: assembled frame differs from the single-GPU frame")
 
     if rank == 0:
         ms_per_step = dt / args.steps * 1e3
         value = rays_per_frame * args.steps / dt / 1e6
-        # per-launch algorithmic bytes of one rank's share (the kernel is per-GPU)
-        bytes_per_launch = algorithmic_bytes(tot) / world
-        achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
-        prof = profiled_traffic() if world == 1 else None
-        out = {
-            "metric": "Mrays/s at 1920x1080x8spp, box.obj BVH",
+        # per-GPU launch: rank 0's share of the algorithmic bytes over the slowest rank's kernel time
+        own_bytes = algorithmic_bytes({"nodes": mine[1], "leaf_tests": mine[2], "samples": mine[3]})
+        achieved = own_bytes / (kernel_ms * 1e-3) / 1e9
+        default_cfg = args.scene == "box" and (W, H, SPP) == (1920, 1080, 8)
+        prof = profiled_traffic() if (world == 1 and default_cfg) else None
+        wl = f"{scene_desc} {W}x{H} {SPP}spp {DEPTH} bounces {SSS} sss"
+        out_line = {
+            "metric": "Mrays/s at 1920x1080x8spp, box.obj BVH" if default_cfg else f"Mrays/s, {wl}",
             "value": round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -180,22 +291,24 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (scenes/box.obj, reference camera and light, progressive sample batches 0-7)",
-            "config": {"workload": "box.obj 1920x1080 8spp 4 bounces 3 sss", "width": W, "height": H,
-                       "spp": SPP, "max_depth": DEPTH, "sss_bounces": SSS,
-                       "parallelism": f"tiles{world}" if world > 1 else "single",
+            "data": "synthetic (reference scene, camera and light; progressive sample batches 0-%d)" % (SPP - 1),
+            "config": {"workload": wl, "width": W, "height": H, "spp": SPP, "max_depth": DEPTH,
+                       "sss_bounces": SSS,
+                       "parallelism": f"tiles{world}-{args.collective}" if world > 1 else "single",
                        "rays_per_frame": int(rays_per_frame),
                        "msamples_per_s": round(W * H * SPP * args.steps / dt / 1e6, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": None if prof is None else int(prof[1]),
                          "traffic_source": None if prof is None else prof[0],
-                         "kernel": "render_kernel<false>", "kernel_ms": round(kernel_ms, 4),
-                         "algorithmic_bytes_per_launch": int(bytes_per_launch)},
+                         "kernel": "render_kernel<false,*>", "kernel_ms": round(kernel_ms, 4),
+                         "algorithmic_bytes_per_launch": int(own_bytes)},
         }
+        if verified is not None:
+            out_line["verified_bitwise_vs_single_gpu"] = verified
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(v, i, n, cam, light)
-        print(json.dumps(out), flush=True)
+            out_line["cpu_baseline"] = cpu_baseline(v, i, n, cam, light, W, H, SPP)
+        print(json.dumps(out_line), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

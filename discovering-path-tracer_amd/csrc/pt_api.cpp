@@ -180,6 +180,7 @@ struct pt_context {
   bool stats_mode = false;
   int opt_scene_lds = 1;   // PT_OPT_SCENE_IN_LDS: 0 never, 1 auto, 2 always
   int opt_sample_lanes = 0;   // PT_OPT_SAMPLE_LANES: 0 auto, else 1/2/4/8
+  int opt_fresh = 0;          // PT_OPT_FRESH_BATCH0
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   // ring of event pairs, one per render launch since pt_reset_launch_times
@@ -441,6 +442,7 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   p.blocks_total = p.blocks_x * ((c->height + 15) / 16);
   p.nranks = c->nranks;
   p.rank = c->rank;
+  p.fresh = c->opt_fresh;
   if (c->opt_sample_lanes) {
     p.spl = c->opt_sample_lanes;
   } else {
@@ -472,6 +474,10 @@ int pt_dispatch(pt_context* c, uint32_t sample_batch) { return pt_render(c, samp
 int pt_set_option(pt_context* c, int key, int value) {
   if (!c) return fail(PT_ERR_INVALID, "null context");
   switch (key) {
+    case PT_OPT_FRESH_BATCH0:
+      if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_FRESH_BATCH0 takes 0 or 1");
+      c->opt_fresh = value;
+      return PT_OK;
     case PT_OPT_SAMPLE_LANES:
       if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8)
         return fail(PT_ERR_INVALID, "PT_OPT_SAMPLE_LANES takes 0 (auto), 1, 2, 4 or 8");
@@ -484,6 +490,31 @@ int pt_set_option(pt_context* c, int key, int value) {
     default:
       return fail(PT_ERR_INVALID, "unknown option " + std::to_string(key));
   }
+}
+
+int pt_tiles_owned(pt_context* c, int* n_tiles) {
+  if (!c || !n_tiles) return fail(PT_ERR_INVALID, "null argument");
+  if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
+  *n_tiles = ptd::owned_tiles(c->width, c->height, c->nranks, c->rank);
+  return PT_OK;
+}
+
+int pt_tiles_pack(pt_context* c, void* dst) {
+  if (!c || !dst) return fail(PT_ERR_INVALID, "null argument");
+  if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
+  PT_HIP(hipSetDevice(c->device));
+  PT_HIP(ptd::launch_tiles(true, c->d_accum, (float4*)dst, c->width, c->height, c->nranks, c->rank, c->stream));
+  return PT_OK;
+}
+
+int pt_tiles_unpack(pt_context* c, const void* src, int src_rank, void* frame) {
+  if (!c || !src || !frame) return fail(PT_ERR_INVALID, "null argument");
+  if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer (it sets the frame size)");
+  if (src_rank < 0 || src_rank >= c->nranks) return fail(PT_ERR_INVALID, "src_rank out of range");
+  if ((((uintptr_t)src) & 15) || (((uintptr_t)frame) & 15)) return fail(PT_ERR_INVALID, "buffers must be 16-B aligned");
+  PT_HIP(hipSetDevice(c->device));
+  PT_HIP(ptd::launch_tiles(false, (float4*)frame, (float4*)src, c->width, c->height, c->nranks, src_rank, c->stream));
+  return PT_OK;
 }
 
 int pt_set_stats_mode(pt_context* c, int enabled) {

@@ -48,11 +48,15 @@ struct RenderParams {
   int blocks_x, blocks_total;   // 16x16-pixel blocks
   int nranks, rank;             // block b is rendered iff b % nranks == rank
   int spl;                      // sample lanes per pixel: 1, 2, 4 or 8
+  int fresh;                    // first_batch == 0 starts from +0 without reading accum
 };
 
 hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices, int n_tris, float4* d_tris,
                              hipStream_t stream);
 hipError_t launch_setup_lights(const LightRec* d_in, int n, LightDev* d_out, hipStream_t stream);
+int owned_tiles(int width, int height, int nranks, int rank);
+hipError_t launch_tiles(bool pack, float4* frame, float4* packed, int width, int height, int nranks, int rank,
+                        hipStream_t stream);
 hipError_t launch_clear(float4* accum, int width, int height, int nranks, int rank, hipStream_t stream);
 // Scene bytes the LDS-staged variant needs, and the largest it accepts.
 constexpr size_t kMaxSceneLds = 48 * 1024;

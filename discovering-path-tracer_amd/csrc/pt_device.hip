@@ -383,7 +383,10 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
   // Running mean (:467-469): lane j of a pixel folds channels c = j (mod spl)
   // of that pixel, sample by sample in batch order.
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  if (active) {
+  // fresh: a launch that starts at batch 0 begins a new accumulation from a
+  // cleared (+0) image — what pt_clear_accum would have stored — without
+  // reading it (PT_OPT_FRESH_BATCH0).
+  if (active && !(P.fresh && P.first_batch == 0)) {
     const float* a = (const float*)&P.accum[pix];
 #pragma unroll
     for (int ch = 0; ch < 4; ++ch)
@@ -526,6 +529,25 @@ __global__ __launch_bounds__(256) void clear_kernel(float4* accum, int W, int H,
   accum[i] = make_float4(z, z, z, z);
 }
 
+// Owned 16x16 tiles <-> a dense buffer (tile o = owned block rank + o*nranks,
+// 256 float4 row-major inside the tile, zeros outside the image): what a rank
+// ships to the root so the frame can be assembled by a gather.
+template <bool PACK>
+__global__ __launch_bounds__(256) void tiles_kernel(float4* frame, float4* packed, int W, int H, int blocks_x,
+                                                    int nranks, int rank) {
+  const int o = (int)blockIdx.x;
+  const int b = o * nranks + rank;
+  const int t = (int)threadIdx.x;
+  const int x = (b % blocks_x) * 16 + (t & 15), y = (b / blocks_x) * 16 + (t >> 4);
+  const bool in = x < W && y < H;
+  const size_t pi = (size_t)y * (size_t)W + (size_t)x;
+  const size_t ti = (size_t)o * 256 + (size_t)t;
+  if (PACK)
+    packed[ti] = in ? frame[pi] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  else if (in)
+    frame[pi] = packed[ti];
+}
+
 __global__ __launch_bounds__(256) void math_kernel(int fn, const float* __restrict__ x, float* __restrict__ y,
                                                    size_t n) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -565,6 +587,23 @@ hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices,
 hipError_t launch_setup_lights(const LightRec* d_in, int n, LightDev* d_out, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   setup_lights_kernel<<<(n + 63) / 64, 64, 0, stream>>>(d_in, n, d_out);
+  return hipGetLastError();
+}
+
+int owned_tiles(int width, int height, int nranks, int rank) {
+  const int total = ((width + 15) / 16) * ((height + 15) / 16);
+  return total > rank ? (total - rank + nranks - 1) / nranks : 0;
+}
+
+hipError_t launch_tiles(bool pack, float4* frame, float4* packed, int width, int height, int nranks, int rank,
+                        hipStream_t stream) {
+  const int n = owned_tiles(width, height, nranks, rank);
+  if (n <= 0) return hipSuccess;
+  const int bx = (width + 15) / 16;
+  if (pack)
+    tiles_kernel<true><<<n, 256, 0, stream>>>(frame, packed, width, height, bx, nranks, rank);
+  else
+    tiles_kernel<false><<<n, 256, 0, stream>>>(frame, packed, width, height, bx, nranks, rank);
   return hipGetLastError();
 }
 

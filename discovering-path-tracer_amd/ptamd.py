@@ -19,13 +19,14 @@ PT_OK = 0
 PT_NODES_INT_BITS = 0x1
 PT_OPT_SCENE_IN_LDS = 1
 PT_OPT_SAMPLE_LANES = 2
+PT_OPT_FRESH_BATCH0 = 3
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).
 EXPORTS = [
     "pt_abi_version", "pt_last_error", "pt_create", "pt_destroy", "pt_set_stream", "pt_synchronize",
     "pt_upload_scene", "pt_upload_lights", "pt_set_camera", "pt_set_params", "pt_resize_and_clear",
     "pt_bind_accum", "pt_clear_accum", "pt_accum_device_ptr", "pt_read_accum", "pt_dispatch", "pt_render",
-    "pt_set_partition", "pt_set_option", "pt_set_stats_mode", "pt_get_stats", "pt_reset_stats", "pt_last_launch_ms",
+    "pt_set_partition", "pt_tiles_owned", "pt_tiles_pack", "pt_tiles_unpack", "pt_set_option", "pt_set_stats_mode", "pt_get_stats", "pt_reset_stats", "pt_last_launch_ms",
     "pt_launch_times_ms", "pt_reset_launch_times", "pt_selftest_math",
     "pt_scene_load_obj", "pt_scene_parse_obj", "pt_scene_from_arrays", "pt_scene_build_bvh",
     "pt_scene_counts", "pt_scene_copy", "pt_scene_upload", "pt_scene_free", "pt_pack_light",
@@ -69,7 +70,9 @@ def lib():
             "pt_clear_accum": ([vp], i32), "pt_accum_device_ptr": ([vp], vp),
             "pt_read_accum": ([vp, vp, sz], i32), "pt_dispatch": ([vp, u32], i32),
             "pt_render": ([vp, u32, u32], i32), "pt_set_partition": ([vp, i32, i32], i32),
-            "pt_set_stats_mode": ([vp, i32], i32), "pt_set_option": ([vp, i32, i32], i32), "pt_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
+            "pt_set_stats_mode": ([vp, i32], i32), "pt_set_option": ([vp, i32, i32], i32),
+            "pt_tiles_owned": ([vp, ctypes.POINTER(i32)], i32), "pt_tiles_pack": ([vp, vp], i32),
+            "pt_tiles_unpack": ([vp, vp, i32, vp], i32), "pt_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
             "pt_reset_stats": ([vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
             "pt_launch_times_ms": ([vp, vp, sz, psz], i32), "pt_reset_launch_times": ([vp], i32),
             "pt_selftest_math": ([i32, i32, vp, vp, sz], i32),
@@ -228,6 +231,17 @@ class Renderer:
 
     def set_partition(self, nranks, rank):
         _check(lib().pt_set_partition(self._c, nranks, rank), "pt_set_partition")
+
+    def tiles_owned(self):
+        n = ctypes.c_int()
+        _check(lib().pt_tiles_owned(self._c, ctypes.byref(n)), "pt_tiles_owned")
+        return n.value
+
+    def tiles_pack(self, dst_device_ptr):
+        _check(lib().pt_tiles_pack(self._c, dst_device_ptr), "pt_tiles_pack")
+
+    def tiles_unpack(self, src_device_ptr, src_rank, frame_device_ptr):
+        _check(lib().pt_tiles_unpack(self._c, src_device_ptr, src_rank, frame_device_ptr), "pt_tiles_unpack")
 
     def set_option(self, key, value):
         _check(lib().pt_set_option(self._c, key, value), "pt_set_option")

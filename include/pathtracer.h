@@ -135,6 +135,14 @@ int pt_render(pt_context* ctx, uint32_t first_batch, uint32_t n_batches);
  * owned pixels and -0 (the IEEE additive identity) to the others, so a sum
  * reduction of all ranks' buffers is bit-identical to a single-GPU frame. */
 int pt_set_partition(pt_context* ctx, int nranks, int rank);
+/* Gather-based assembly (cheaper than a full-frame sum for N > 2): a rank
+ * packs the tiles it owns into a dense device buffer of
+ * n_tiles * 16*16 float4 (pt_tiles_owned), ships it to the root, and the
+ * root unpacks each rank's buffer into a W x H frame.  The frame size and
+ * partition are the context's; all work is enqueued on its stream. */
+int pt_tiles_owned(pt_context* ctx, int* n_tiles);
+int pt_tiles_pack(pt_context* ctx, void* dst_device);
+int pt_tiles_unpack(pt_context* ctx, const void* src_device, int src_rank, void* frame_device);
 
 /* ---- kernel options ---------------------------------------------------- */
 /* PT_OPT_SCENE_IN_LDS: stage the scene in LDS per workgroup — 0 never,
@@ -145,6 +153,11 @@ int pt_set_partition(pt_context* ctx, int nranks, int rank);
  * pt_render — 0 auto (min(n_batches, 8) rounded down to 1/2/4/8), or 1, 2, 4, 8.
  * Output is identical for every value. */
 #define PT_OPT_SAMPLE_LANES 2
+/* PT_OPT_FRESH_BATCH0: 1 = a launch whose first batch is 0 starts from a
+ * cleared (+0) accumulator without reading it — bitwise what
+ * pt_clear_accum + pt_render give, minus a clear and a read of the image.
+ * 0 (default) = read the accumulator, as the reference does (prev * 0). */
+#define PT_OPT_FRESH_BATCH0 3
 int pt_set_option(pt_context* ctx, int key, int value);
 
 /* ---- instrumentation --------------------------------------------------- */

@@ -3,6 +3,11 @@ import sys
 
 import pytest
 
+# Load torch (and its HIP runtime) before libptamd.so: the library then binds
+# to that same libamdhip64 (matched by SONAME) instead of pulling a second HIP
+# runtime into the process when a test later hands it torch device memory.
+import torch  # noqa: F401,E402
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "discovering-path-tracer_amd")
 for p in (PKG, os.path.join(ROOT, "tests"), ROOT):

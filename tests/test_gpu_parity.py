@@ -144,6 +144,46 @@ def test_partition_sum_is_bit_exact():
         _assert_same(acc, want, f"sum over {nranks} ranks")
 
 
+def test_fresh_batch0_ignores_stale_accumulator():
+    v, i, n = _box()
+    r = _setup(v, i, n)
+    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+    r.resize_and_clear(64, 40)
+    r.render(0, 3)          # leaves a finished frame in the buffer
+    r.render(0, 4)          # restarts at batch 0 without clearing
+    ref, _ = _oracle(v, i, n, 64, 40, nb=4)
+    _assert_same(r.read_accum(), ref, "fresh restart")
+    r.render(4, 2)          # continuing batches still read the accumulator
+    ref, _ = _oracle(v, i, n, 64, 40, nb=6)
+    _assert_same(r.read_accum(), ref, "fresh + continue")
+
+
+@pytest.mark.parametrize("nranks", [2, 3, 8])
+def test_tile_gather_assembles_frame(nranks):
+    """pt_tiles_pack on every rank + pt_tiles_unpack on the root = the
+    single-GPU frame (the gather path bench.py uses for N > 2)."""
+    import torch
+    v, i, n = _box()
+    W, H = 150, 70
+    frame = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+    root = None
+    for rank in range(nranks):
+        r = _setup(v, i, n)
+        r.set_partition(nranks, rank)
+        r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+        r.resize_and_clear(W, H)
+        r.render(0, 8)
+        buf = torch.empty((r.tiles_owned(), 256, 4), dtype=torch.float32, device="cuda")
+        r.tiles_pack(buf.data_ptr())
+        r.synchronize()
+        if root is None:
+            root = r
+        root.tiles_unpack(buf.data_ptr(), rank, frame.data_ptr())
+        root.synchronize()
+    ref, _ = _oracle(v, i, n, W, H, nb=8)
+    _assert_same(frame.cpu().numpy().reshape(-1), ref, f"gather over {nranks}")
+
+
 @pytest.mark.parametrize("ntri,int_bits", [(1, False), (2, False), (1000, False), (20000, True)])
 def test_random_triangles(ntri, int_bits):
     tv, ti = scenes.random_triangles(ntri, seed=ntri)
