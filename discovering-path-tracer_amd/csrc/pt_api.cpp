@@ -181,6 +181,8 @@ struct pt_context {
   int opt_scene_lds = 1;   // PT_OPT_SCENE_IN_LDS: 0 never, 1 auto, 2 always
   int opt_sample_lanes = 0;   // PT_OPT_SAMPLE_LANES: 0 auto, else 1/2/4/8
   int opt_fresh = 0;          // PT_OPT_FRESH_BATCH0
+  int opt_kernel = 0;         // PT_OPT_KERNEL: 0 auto, 1 path-recursive, 2 lane state machine
+  int opt_sm_batch = 1;       // PT_OPT_SM_BATCH
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   // ring of event pairs, one per render launch since pt_reset_launch_times
@@ -443,6 +445,7 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   p.nranks = c->nranks;
   p.rank = c->rank;
   p.fresh = c->opt_fresh;
+  p.sm_batch = c->opt_sm_batch;
   if (c->opt_sample_lanes) {
     p.spl = c->opt_sample_lanes;
   } else {
@@ -461,7 +464,11 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   const bool fits = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
   if (c->opt_scene_lds == 2 && !fits) return fail(PT_ERR_UNSUPPORTED, "scene too large for the LDS variant");
   const bool lds = c->opt_scene_lds == 2 || (c->opt_scene_lds == 1 && fits);
-  PT_HIP(ptd::launch_render(p, c->stats_mode, lds, c->stream));
+  // auto: the path-recursive kernel while the scene fits in LDS (short walks,
+  // shading-bound), the lane state machine once traversal dominates
+  const bool sm = c->opt_kernel == 2 || (c->opt_kernel == 0 && !lds);
+  if (sm) p.spl = 1;
+  PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream));
   PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
   PT_HIP(hipEventRecord(c->ev1, c->stream));
   c->ring_n++;
@@ -474,6 +481,14 @@ int pt_dispatch(pt_context* c, uint32_t sample_batch) { return pt_render(c, samp
 int pt_set_option(pt_context* c, int key, int value) {
   if (!c) return fail(PT_ERR_INVALID, "null context");
   switch (key) {
+    case PT_OPT_KERNEL:
+      if (value < 0 || value > 2) return fail(PT_ERR_INVALID, "PT_OPT_KERNEL takes 0, 1 or 2");
+      c->opt_kernel = value;
+      return PT_OK;
+    case PT_OPT_SM_BATCH:
+      if (value < 1 || value > 64) return fail(PT_ERR_INVALID, "PT_OPT_SM_BATCH takes 1..64");
+      c->opt_sm_batch = value;
+      return PT_OK;
     case PT_OPT_FRESH_BATCH0:
       if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_FRESH_BATCH0 takes 0 or 1");
       c->opt_fresh = value;

@@ -49,6 +49,7 @@ struct RenderParams {
   int nranks, rank;             // block b is rendered iff b % nranks == rank
   int spl;                      // sample lanes per pixel: 1, 2, 4 or 8
   int fresh;                    // first_batch == 0 starts from +0 without reading accum
+  int sm_batch;                 // state-machine kernel: lanes that must be waiting before shading runs
 };
 
 hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices, int n_tris, float4* d_tris,
@@ -63,7 +64,7 @@ constexpr size_t kMaxSceneLds = 48 * 1024;
 inline size_t scene_lds_bytes(const RenderParams& p) {
   return ((size_t)2 * p.n_nodes + (size_t)3 * p.n_tris) * 16;
 }
-hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, hipStream_t stream);
+hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool state_machine, hipStream_t stream);
 hipError_t launch_math(int fn, const float* x, float* y, size_t n, hipStream_t stream);
 
 }  // namespace ptd

@@ -569,6 +569,399 @@ __global__ __launch_bounds__(256) void math_kernel(int fn, const float* __restri
   y[i] = r;
 }
 
+// ===========================================================================
+// Lane state-machine kernel, for scenes where traversal dominates.
+//
+// In the path-recursive kernel above every lane of a wave walks its own ray
+// and the wave runs until its longest walk ends: with thousands of node
+// visits per ray and a wide spread between rays (measured lane utilisation
+// 14 % on a 1M-triangle cloud) most lanes idle.  Here each lane is a small
+// state machine over pathTrace (:300-418) — phases PRIMARY, DIRECT, SSS,
+// SSS_SHADOW, BOUNCE — holding at most one ray in flight.  The wave steps
+// every in-flight ray a few nodes at a time; a lane whose ray has finished
+// runs the shading that consumes the result and emits its next ray (or starts
+// its pixel's next sample) so lanes stay busy until the pixel's last sample.
+// The arithmetic, RNG draws and traversal order per ray are exactly those of
+// path_trace(); only the interleaving across lanes differs.
+// ===========================================================================
+enum : int { PH_BEGIN = 0, PH_PRIMARY, PH_DIRECT, PH_SSS, PH_SSS_SHADOW, PH_BOUNCE };
+
+struct Trav {
+  v3 o, d, inv;
+  int k;        // next node
+  float lim;    // closest: best t so far; shadow: occlusion limit
+  int res;      // closest: best triangle (-1 none); shadow: 1 once occluded
+  int shadow;   // 0 closest-hit, 1 shadow query
+  int nc;       // queued leaf candidates (closest)
+  uint32_t cn, cl;   // node visits / leaf tests of this ray (stats)
+};
+
+struct PathSt {
+  uint32_t s, rng;
+  int phase, depth, li, k;
+  v3 thr, rad, hp, hn, acc3, pend, sss_thr, so, sd, cp, sn;
+  float travel;
+};
+
+__device__ __forceinline__ void trav_start(Trav& T, v3 o, v3 d, bool shadow, float limit) {
+  T.o = o;
+  T.d = d;
+  T.inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  T.k = 0;
+  T.shadow = shadow ? 1 : 0;
+  T.lim = shadow ? limit : 1e30f;
+  T.res = shadow ? 0 : -1;
+  T.nc = 0;
+  T.cn = 0u;
+  T.cl = 0u;
+}
+
+// One node of the walk; returns true when the ray is finished.
+template <bool STATS>
+__device__ __forceinline__ bool trav_step(const RenderParams& P, Trav& T, int* cand) {
+  if (T.k >= P.n_nodes) {
+    if (!T.shadow) {
+      float best = T.lim;
+      int bt = T.res;
+      test_candidates(P, T.o, T.d, cand, T.nc, &best, &bt);
+      T.lim = best;
+      T.res = bt;
+      T.nc = 0;
+    }
+    return true;
+  }
+  const float4 a = P.nodes[2 * T.k];
+  const float4 b = P.nodes[2 * T.k + 1];
+  if (STATS) T.cn++;
+  const int raw = __float_as_int(a.w);
+  const bool h = raw < 0 ? true : slab(T.o, T.inv, a, b);
+  const int tri = __float_as_int(b.w);
+  if (h && tri >= 0) {
+    if (STATS) T.cl++;
+    if (T.shadow) {
+      const float4* Tr = P.tris + 3 * tri;
+      float t;
+      if (tri_test(T.o, T.d, Tr[0], Tr[1], Tr[2], &t) && t < 1e30f && !(t >= T.lim)) {
+        T.res = 1;
+        if (!STATS) return true;
+      }
+    } else {
+      cand[T.nc * 64] = tri;
+      if (++T.nc == kCand) {
+        float best = T.lim;
+        int bt = T.res;
+        test_candidates(P, T.o, T.d, cand, T.nc, &best, &bt);
+        T.lim = best;
+        T.res = bt;
+        T.nc = 0;
+      }
+    }
+  }
+  T.k = (h && tri < 0) ? T.k + 1 : (raw & 0x7fffffff);
+  return false;
+}
+
+struct CamFrame {
+  v3 cpos, cdir, right, up;
+  float tanFov, aspect, ndcX0, ndcY0;
+  int W, H, px, py;
+};
+
+// main() ray generation (:430-460) for one sample batch.
+__device__ __forceinline__ void camera_ray(const CamFrame& F, uint32_t seed, v3* origin, v3* dir) {
+  uint32_t rng = seed;
+  float u1 = fmax_(1e-38f, rng_next(&rng));
+  float u2 = rng_next(&rng);
+  float r = sqrt_(-2.0f * log_(u1));
+  float th = (2.0f * 0x1.921fb6p+1f) * u2;
+  float sn, cs;
+  sincos_(th, &sn, &cs);
+  const float ax = (r * cs) * 0.02f;
+  const float ay = (r * sn) * 0.02f;
+  *origin = add(add(F.cpos, muls(F.right, ax)), muls(F.up, ay));
+  u1 = fmax_(1e-38f, rng_next(&rng));
+  u2 = rng_next(&rng);
+  r = sqrt_(-2.0f * log_(u1));
+  th = (2.0f * 0x1.921fb6p+1f) * u2;
+  sincos_(th, &sn, &cs);
+  const float jx = r * cs, jy = r * sn;
+  const float ndcX = F.ndcX0 + (jx * 0.5f) / (float)F.W;
+  const float ndcY = F.ndcY0 + (jy * 0.5f) / (float)F.H;
+  const v3 bdir =
+      normalize(sub(add(F.cdir, muls(neg(F.right), (ndcX * F.tanFov) * F.aspect)), muls(F.up, ndcY * F.tanFov)));
+  const v3 focal = add(F.cpos, muls(bdir, 3.0f));
+  *dir = normalize(sub(focal, *origin));
+}
+
+// Runs lane-local shading from the current phase until the lane needs a ray
+// traced (returns true, T set up) or has finished all its samples (false).
+template <bool STATS>
+__device__ bool sm_run(const RenderParams& P, const CamFrame& F, PathSt& S, Trav& T, Ctr& c, float* acc) {
+  const float OFFSET = 0.001f;
+  const v3 albedo = mk(0.8f, 0.8f, 0.8f);
+  const v3 sss_albedo = mk(1.0f, 0.2f, 0.1f);
+  const float sss_radius = 1.0f;
+  v3 color = mk(0.0f, 0.0f, 0.0f);
+  for (;;) {
+    bool finished = false;   // sample complete, `color` holds its radiance
+    switch (S.phase) {
+      case PH_BEGIN: {
+        const uint32_t batch = P.first_batch + S.s;
+        const uint32_t seed = (batch * (uint32_t)F.H + (uint32_t)F.py) * (uint32_t)F.W + (uint32_t)F.px;   // :435
+        v3 o, d;
+        camera_ray(F, seed, &o, &d);
+        S.rng = seed;                                                         // :307
+        S.thr = mk(1.0f, 1.0f, 1.0f);
+        S.rad = mk(0.0f, 0.0f, 0.0f);
+        S.depth = 0;
+        bool need = P.max_depth > 0;
+        for (int i = 0; i < P.n_lights && !need; ++i) {
+          float tl;
+          need = intersect_area_light(o, d, P.lights[i], &tl);
+        }
+        if (need) {
+          trav_start(T, o, d, false, 0.0f);
+          S.phase = PH_PRIMARY;
+          return true;
+        }
+        finished = true;   // no light in view and max_depth 0: radiance 0
+        break;
+      }
+      case PH_PRIMARY: {
+        // light pre-pass (:311-328) on the same ray, then depth 0 (:333)
+        bool lit = false;
+        for (int i = 0; i < P.n_lights; ++i) {
+          const LightDev L = P.lights[i];
+          float tl;
+          if (intersect_area_light(T.o, T.d, L, &tl)) {
+            if (STATS) { c.rays++; c.nodes += T.cn; c.leaves += T.cl; }
+            if (T.res < 0 || T.lim > tl) {
+              color = mk(L.inten[0], L.inten[1], L.inten[2]);
+              lit = true;
+              break;
+            }
+          }
+        }
+        if (lit) { finished = true; break; }
+        if (P.max_depth == 0) { color = S.rad; finished = true; break; }
+        if (STATS) { c.rays++; c.nodes += T.cn; c.leaves += T.cl; }
+        S.phase = PH_BOUNCE;   // handled as the result of a closest-hit trace at depth S.depth
+        continue;
+      }
+      case PH_BOUNCE: {
+        if (S.depth > 0 && STATS) { c.rays++; c.nodes += T.cn; c.leaves += T.cl; }
+        if (T.res < 0) {
+          S.rad = add(S.rad, mul(S.thr, mk(0.0f, 0.0f, 0.0f)));   // background (:336)
+          color = S.rad;
+          finished = true;
+          break;
+        }
+        S.hp = add(T.o, muls(T.d, T.lim));
+        S.hn = tri_normal(P, T.res);
+        S.acc3 = mk(0.0f, 0.0f, 0.0f);   // directLight
+        S.li = 0;
+        S.phase = PH_DIRECT;
+        S.k = -1;                         // marks "no shadow ray returned yet"
+        continue;
+      }
+      case PH_DIRECT: {
+        if (S.k >= 0) {   // a shadow ray for light S.li has returned
+          if (STATS) { c.rays++; c.nodes += T.cn; c.leaves += T.cl; }
+          if (!T.res) S.acc3 = add(S.acc3, mul(albedo, S.pend));
+          S.li++;
+        }
+        if (S.li < P.n_lights) {                                            // :345-366
+          const LightDev L = P.lights[S.li];
+          const v3 lp = sample_area_light(L, &S.rng);
+          const v3 ld = normalize(sub(lp, S.hp));
+          const float diff = fmax_(dot(S.hn, ld), 0.0f);
+          const float dist = length(sub(lp, S.hp));
+          const float d2 = dist * dist;
+          S.pend = muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), 1.0f / fmax_(d2, 0.01f));
+          trav_start(T, add(S.hp, muls(S.hn, OFFSET)), ld, true, dist - OFFSET);
+          S.k = 0;
+          return true;
+        }
+        S.rad = add(S.rad, mul(S.thr, S.acc3));
+        // SSS walk (:371-408): the first direction is drawn even if no step runs
+        S.sss_thr = mk(1.0f, 1.0f, 1.0f);
+        S.so = sub(S.hp, muls(S.hn, OFFSET));
+        S.sd = sample_sphere(&S.rng);
+        S.k = 0;
+        if (S.k < P.sss_bounces) {
+          trav_start(T, S.so, S.sd, false, 0.0f);
+          S.phase = PH_SSS;
+          return true;
+        }
+        S.phase = -1;   // to the bounce
+        break;
+      }
+      case PH_SSS: {
+        if (STATS) { c.rays++; c.nodes += T.cn; c.leaves += T.cl; }
+        if (T.res < 0) { S.phase = -1; break; }                           // :381 miss ends the walk
+        S.travel = T.lim;
+        S.cp = add(S.so, muls(S.sd, S.travel));
+        S.sn = tri_normal(P, T.res);
+        S.acc3 = mk(0.0f, 0.0f, 0.0f);   // sssLight
+        S.li = 0;
+        S.phase = PH_SSS_SHADOW;
+        if (P.n_lights > 0) {
+          const LightDev L = P.lights[0];
+          const v3 lp = sample_area_light(L, &S.rng);
+          const v3 ed = normalize(sub(lp, S.cp));
+          const float ediff = fmax_(dot(S.sn, ed), 0.0f);
+          const float edist = length(sub(lp, S.cp));
+          const float d2 = edist * edist;
+          S.pend = muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])), 1.0f / fmax_(d2, 0.01f));
+          trav_start(T, add(S.cp, muls(S.sn, OFFSET)), ed, true, edist - OFFSET);
+          return true;
+        }
+        continue;
+      }
+      case PH_SSS_SHADOW: {
+        if (S.li < P.n_lights) {   // the shadow ray for light S.li returned
+          if (STATS) { c.rays++; c.nodes += T.cn; c.leaves += T.cl; }
+          if (!T.res) S.acc3 = add(S.acc3, S.pend);
+          S.li++;
+        }
+        if (S.li < P.n_lights) {
+          const LightDev L = P.lights[S.li];
+          const v3 lp = sample_area_light(L, &S.rng);
+          const v3 ed = normalize(sub(lp, S.cp));
+          const float ediff = fmax_(dot(S.sn, ed), 0.0f);
+          const float edist = length(sub(lp, S.cp));
+          const float d2 = edist * edist;
+          S.pend = muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])), 1.0f / fmax_(d2, 0.01f));
+          trav_start(T, add(S.cp, muls(S.sn, OFFSET)), ed, true, edist - OFFSET);
+          return true;
+        }
+        S.rad = add(S.rad, muls(mul(mul(S.thr, S.sss_thr), S.acc3), 1.0f + sss_radius * 0.5f));
+        S.sss_thr = mul(S.sss_thr, muls(sss_albedo, exp_(-S.travel / (sss_radius * 1.5f))));
+        S.so = sub(S.cp, muls(S.sn, OFFSET));
+        S.sd = sample_sphere(&S.rng);
+        S.k++;
+        if (S.k < P.sss_bounces) {
+          trav_start(T, S.so, S.sd, false, 0.0f);
+          S.phase = PH_SSS;
+          return true;
+        }
+        S.phase = -1;
+        break;
+      }
+      default:
+        break;
+    }
+    if (!finished && S.phase == -1) {
+      // indirect bounce (:411-414)
+      const v3 bd = sample_hemisphere(S.hn, &S.rng);
+      S.thr = mul(S.thr, muls(albedo, dot(S.hn, bd)));
+      const v3 ro = add(S.hp, muls(S.hn, OFFSET));
+      S.depth++;
+      if (S.depth < P.max_depth) {
+        trav_start(T, ro, bd, false, 0.0f);
+        S.phase = PH_BOUNCE;
+        return true;
+      }
+      color = S.rad;
+      finished = true;
+    }
+    if (finished) {
+      const uint32_t batch = P.first_batch + S.s;
+      const float fb = (float)batch, fb1 = (float)(batch + 1u);          // :468
+      acc[0] = (acc[0] * fb + color.x) / fb1;
+      acc[1] = (acc[1] * fb + color.y) / fb1;
+      acc[2] = (acc[2] * fb + color.z) / fb1;
+      acc[3] = (acc[3] * fb + 1.0f) / fb1;
+      S.s++;
+      if (S.s >= P.n_batches) return false;
+      S.phase = PH_BEGIN;
+    }
+  }
+}
+
+template <bool STATS, bool LDS>
+#ifndef PT_SM_MIN_BLOCKS
+#define PT_SM_MIN_BLOCKS 1
+#endif
+__global__ __launch_bounds__(256, PT_SM_MIN_BLOCKS) void render_sm_kernel(RenderParams P) {
+  const int tid = (int)threadIdx.x;
+  if (LDS) {
+    extern __shared__ float4 lds_scene[];
+    const int nn = 2 * P.n_nodes, nt = 3 * P.n_tris;
+    for (int i = tid; i < nn; i += 256) lds_scene[i] = P.nodes[i];
+    for (int i = tid; i < nt; i += 256) lds_scene[nn + i] = P.tris[i];
+    __syncthreads();
+    P.nodes = lds_scene;
+    P.tris = lds_scene + nn;
+  }
+  // one pixel per lane, all its samples in order: 16x16 tile per workgroup,
+  // 8x8 per wave
+  const int tile = (int)blockIdx.x * P.nranks + P.rank;
+  const int wave = tid >> 6, lane = tid & 63;
+  __shared__ int cand_buf[4][kCand][64];
+  int* cand = &cand_buf[wave][0][lane];
+  CamFrame F;
+  F.W = P.width;
+  F.H = P.height;
+  const int bx = tile % P.blocks_x, by = tile / P.blocks_x;
+  F.px = bx * 16 + (wave & 1) * 8 + (lane & 7);
+  F.py = by * 16 + (wave >> 1) * 8 + (lane >> 3);
+  const bool active = tile < P.blocks_total && F.px < F.W && F.py < F.H;
+  F.cpos = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+  F.cdir = mk(P.cam_dir[0], P.cam_dir[1], P.cam_dir[2]);
+  const v3 cup = mk(P.cam_up[0], P.cam_up[1], P.cam_up[2]);
+  F.ndcX0 = (2.0f * (float)F.px / (float)F.W) - 1.0f;
+  F.ndcY0 = (2.0f * (float)F.py / (float)F.H) - 1.0f;
+  F.aspect = (float)F.W / (float)F.H;
+  F.right = uniform(normalize(cross(F.cdir, neg(cup))));
+  F.up = uniform(normalize(cross(F.right, F.cdir)));
+  F.tanFov = uniform(tan_(radians_(P.fov * 0.5f)));
+  const size_t pix = (size_t)F.py * (size_t)F.W + (size_t)F.px;
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (active && !(P.fresh && P.first_batch == 0)) {
+    const float4 a = P.accum[pix];
+    acc[0] = a.x; acc[1] = a.y; acc[2] = a.z; acc[3] = a.w;
+  }
+  Ctr c = {0u, 0u, 0u};
+  PathSt S;
+  S.s = 0;
+  S.phase = PH_BEGIN;
+  Trav T;
+  bool tracing = active && P.n_batches > 0 && sm_run<STATS>(P, F, S, T, c, acc);
+  bool waiting = false;
+  const int batch_min = P.sm_batch;
+  for (;;) {
+    if (tracing && !waiting) {
+      for (int it = 0; it < 4; ++it) {
+        if (trav_step<STATS>(P, T, cand)) {
+          waiting = true;
+          break;
+        }
+      }
+    }
+    const unsigned long long wmask = __ballot(waiting);
+    const unsigned long long tmask = __ballot(tracing && !waiting);
+    if (wmask == 0ull && tmask == 0ull) break;
+    if (tmask == 0ull || (int)__popcll(wmask) >= batch_min) {
+      if (waiting) {
+        waiting = false;
+        tracing = sm_run<STATS>(P, F, S, T, c, acc);
+      }
+    }
+  }
+  if (active && P.n_batches > 0) P.accum[pix] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  if (STATS) {
+    const unsigned long long rays = wave_sum(c.rays), nodes = wave_sum(c.nodes), leaves = wave_sum(c.leaves);
+    const unsigned long long smp = wave_sum(active ? (unsigned long long)P.n_batches : 0ull);
+    if (lane == 0) {
+      atomicAdd(&P.stats[0], rays);
+      atomicAdd(&P.stats[1], nodes);
+      atomicAdd(&P.stats[2], leaves);
+      atomicAdd(&P.stats[3], smp);
+    }
+  }
+}
+
 }  // namespace
 
 hipError_t launch_math(int fn, const float* x, float* y, size_t n, hipStream_t stream) {
@@ -614,16 +1007,22 @@ hipError_t launch_clear(float4* accum, int width, int height, int nranks, int ra
   return hipGetLastError();
 }
 
-hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, hipStream_t stream) {
+hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool state_machine, hipStream_t stream) {
   if (p.spl != 1 && p.spl != 2 && p.spl != 4 && p.spl != 8) return hipErrorInvalidValue;
-  // owned tiles b = rank + i*nranks, each split into spl workgroups
-  const long long grid = (long long)(p.blocks_total + p.nranks - 1 - p.rank) / p.nranks * p.spl;
+  // owned tiles b = rank + i*nranks; the recursive kernel splits each into spl workgroups
+  const long long tiles = (long long)(p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;
+  const long long grid = state_machine ? tiles : tiles * p.spl;
   if (grid <= 0 || p.n_batches == 0) return hipSuccess;
   if (grid > 0x7fffffffll) return hipErrorInvalidValue;
   const size_t lds = lds_scene ? scene_lds_bytes(p) : 0;
   if (lds > kMaxSceneLds) return hipErrorInvalidValue;
-  void (*kern)(RenderParams) = lds_scene ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
-                                         : (stats ? render_kernel<true, false> : render_kernel<false, false>);
+  void (*kern)(RenderParams);
+  if (state_machine)
+    kern = lds_scene ? (stats ? render_sm_kernel<true, true> : render_sm_kernel<false, true>)
+                     : (stats ? render_sm_kernel<true, false> : render_sm_kernel<false, false>);
+  else
+    kern = lds_scene ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
+                     : (stats ? render_kernel<true, false> : render_kernel<false, false>);
   hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), lds, stream, p);
   return hipGetLastError();
 }

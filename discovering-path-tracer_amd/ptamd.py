@@ -20,6 +20,8 @@ PT_NODES_INT_BITS = 0x1
 PT_OPT_SCENE_IN_LDS = 1
 PT_OPT_SAMPLE_LANES = 2
 PT_OPT_FRESH_BATCH0 = 3
+PT_OPT_KERNEL = 4
+PT_OPT_SM_BATCH = 5
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).
 EXPORTS = [

@@ -75,6 +75,55 @@ def test_sample_lanes(spl, nb):
     _assert_same(r.read_accum(), ref, f"spl={spl} nb={nb}")
 
 
+def _sm_cases():
+    gv, gi = scenes.grid_mesh(6)
+    sv, si = scenes.displaced_sphere(2)
+    tv, ti = scenes.random_triangles(1000, seed=1000)
+    two = np.concatenate([scenes.REFERENCE_LIGHT,
+                          ptamd.pack_light([0.5, 0.5, 1.5], [0, 0, -1], [2, 4, 8], [0.5, 1.0])])
+    return [("grid2lights", gv, gi, scenes.camera((0.0, 0.0, 3.0)), two, 3, 2),
+            ("sphere", sv, si, scenes.camera((0.0, 0.5, 3.0)), scenes.REFERENCE_LIGHT, 4, 3),
+            ("random", tv, ti, scenes.camera((0.3, 0.2, 2.2)), scenes.REFERENCE_LIGHT, 4, 3),
+            ("nolight_d2", tv, ti, scenes.camera((0.3, 0.2, 2.2)), np.zeros(0, np.float32), 2, 1),
+            ("depth0", sv, si, scenes.camera((0.0, 3.0, 0.5), up=(0, 0, 1)), scenes.REFERENCE_LIGHT, 0, 3),
+            ("sss0", sv, si, scenes.camera((0.0, 0.5, 3.0)), scenes.REFERENCE_LIGHT, 4, 0)]
+
+
+@pytest.mark.parametrize("batch", [1, 16, 64])
+@pytest.mark.parametrize("lds", [0, 2])
+def test_state_machine_kernel_box(lds, batch):
+    v, i, n = _box()
+    r = _setup(v, i, n, lds=lds)
+    r.set_option(ptamd.PT_OPT_KERNEL, 2)
+    r.set_option(ptamd.PT_OPT_SM_BATCH, batch)
+    r.resize_and_clear(70, 45)
+    r.render(1, 5)
+    ref, _ = _oracle(v, i, n, 70, 45, first=1, nb=5)
+    _assert_same(r.read_accum(), ref, f"state machine box lds={lds} batch={batch}")
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_state_machine_kernel_scenes(case):
+    name, sv, si, cam, lights, depth, sss = _sm_cases()[case]
+    s = ptamd.Scene.from_arrays(sv, si).build_bvh()
+    v, i, n, _, _ = s.arrays()
+    r = _setup(v, i, n, cam=cam, lights=lights, depth=depth, sss=sss, lds=0)
+    r.set_option(ptamd.PT_OPT_KERNEL, 2)
+    r.set_option(ptamd.PT_OPT_SM_BATCH, 8)
+    r.resize_and_clear(56, 40)
+    r.render(0, 3)
+    got = r.read_accum()
+    ref, ost = _oracle(v, i, n, 56, 40, nb=3, depth=depth, sss=sss, cam=cam, lights=lights)
+    _assert_same(got, ref, f"state machine {name}")
+    r.clear()
+    r.set_stats_mode(True)
+    r.reset_stats()
+    r.render(0, 3)
+    st = r.stats()
+    _assert_same(r.read_accum(), ref, f"state machine stats-mode {name}")
+    assert (st["rays"], st["nodes"], st["leaf_tests"]) == tuple(int(x) for x in ost), name
+
+
 def test_dispatch_sequence_equals_fused_render():
     v, i, n = _box()
     r = _setup(v, i, n)
