@@ -301,6 +301,12 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
     uint32_t* i = nullptr;
     ~Staging() { if (v) (void)hipFree(v); if (i) (void)hipFree(i); }
   } st;
+  // one zero node of padding past the end: the traversal loads node k+1
+  // speculatively, also when k is the last node
+  collapsed.push_back(make_float4(0, 0, 0, 0));
+  collapsed.push_back(make_float4(0, 0, 0, 0));
+  threaded.push_back(make_float4(0, 0, 0, 0));
+  threaded.push_back(make_float4(0, 0, 0, 0));
   PT_HIP(hipMalloc((void**)&c->d_nodes, collapsed.size() * sizeof(float4)));
   PT_HIP(hipMalloc((void**)&c->d_nodes_full, threaded.size() * sizeof(float4)));
   PT_HIP(hipMalloc((void**)&c->d_tris, (size_t)T * 3 * sizeof(float4)));
@@ -312,8 +318,8 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   PT_HIP(hipMemcpyAsync(st.i, indices, n_indices * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
   PT_HIP(ptd::launch_setup_tris(st.v, st.i, T, c->d_tris, c->stream));
   PT_HIP(hipStreamSynchronize(c->stream));
-  c->n_nodes = (int)(collapsed.size() / 2);
-  c->n_nodes_full = (int)(threaded.size() / 2);
+  c->n_nodes = (int)(collapsed.size() / 2) - 1;
+  c->n_nodes_full = (int)(threaded.size() / 2) - 1;
   c->n_tris = T;
   c->has_scene = true;
   return PT_OK;
