@@ -21,8 +21,8 @@ import scenes  # noqa: E402
 def load_scene(name):
     if name == "box":
         return ptamd.Scene.load_obj(scenes.BOX_OBJ).build_bvh(), scenes.DEFAULT_CAMERA
-    if name == "sphere":
-        v, i = scenes.displaced_sphere(5)
+    if name.startswith("sphere"):
+        v, i = scenes.displaced_sphere(int(name.split(":")[1]) if ":" in name else 5)
         return ptamd.Scene.from_arrays(v, i).build_bvh(), scenes.camera((0.0, 0.5, 3.0))
     if name.startswith("random:"):
         v, i = scenes.random_triangles(int(name.split(":")[1]), seed=42)
