@@ -153,6 +153,126 @@ void collapse_implied(const std::vector<float4>& full, std::vector<float4>* out)
   }
 }
 
+// ---- primary-ray bundle culling -----------------------------
+// Camera model of raytrace_comp.comp:430-460 in the orthonormal camera frame
+// (right, up, ez = dir/|dir|) centred on the camera position, with the
+// kernel's right = normalize(cross(dir, -up0)), up = normalize(cross(right, dir)):
+//   origin O = (ox, oy, 0),     |ox|, |oy| <= 0.02 * Rg        (aperture, :445-448)
+//   bdir ∝ (a, b, 1),  a = -ndcX*T*A/L, b = -ndcY*T/L          (:456-457)
+//   ndcX = ndcX0 + jx*0.5/W,    |jx| <= Rg                     (:451-454)
+//   F = 3*bdir,  dir ∝ F - O                                   (:459-460)
+// where Rg bounds every Box-Muller radius sqrt(-2 log u1) with u1 >= 1e-38
+// (:220): sqrt(-2 ln 1e-38) = 13.2286.  The ray reaches depth Z at slope
+//   X/Z = a + ox (1/Z - 1/Fz),  Fz = 3/sqrt(1+a^2+b^2),
+// so a point of depth Z > 0 with slope s is reachable from a pixel only if
+// |s - a| <= 0.02 Rg max|1/Z - 1/Fz| for some a of the pixel's jittered range.
+// Every object (root box corners, light rectangle corners — convex sets whose
+// slope hull is the hull of the corners' slopes) therefore maps to an NDC
+// rectangle of pixel origins that can reach it; outside all rectangles every
+// primary ray misses the root box (so traceRay returns no hit) and every light
+// (the pre-pass hits nothing), and the sample is exactly (0,0,0).  All maths
+// in double with margins far above the kernel's float rounding.
+constexpr double kGaussR = 13.25;
+
+struct D3 { double x, y, z; };
+D3 d3(const float* f) { return {f[0], f[1], f[2]}; }
+D3 dsub(D3 a, D3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+D3 dadd(D3 a, D3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+D3 dmul(D3 a, double s) { return {a.x * s, a.y * s, a.z * s}; }
+double ddot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+D3 dcross(D3 a, D3 b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+double dlen(D3 a) { return sqrt(ddot(a, a)); }
+
+// Returns the rectangle count (>= 0) or -1 when no guarantee is derived.
+int cull_rects(const float cam[16], int W, int H, const float* lo, const float* hi, const pt_area_light* lights,
+               int n_lights, float* rects, int max_rects) {
+  if (W <= 0 || H <= 0 || n_lights < 0 || n_lights + 1 > max_rects) return -1;
+  const D3 cpos = d3(cam), cdir = d3(cam + 4), cup = d3(cam + 8);
+  const double fov = cam[12];
+  const double L = dlen(cdir);
+  if (!(L > 1e-6 && L < 1e6) || !(fov > 0.01 && fov < 170.0)) return -1;
+  const D3 rx = dcross(cdir, dmul(cup, -1.0));
+  const double rl = dlen(rx);
+  if (!(rl > 1e-6 * L * dlen(cup))) return -1;
+  const D3 right = dmul(rx, 1.0 / rl);
+  const D3 ux = dcross(right, cdir);
+  const D3 up = dmul(ux, 1.0 / dlen(ux));
+  const D3 ez = dmul(cdir, 1.0 / L);
+  const double T = tan(fov * 0.5 * M_PI / 180.0), A = (double)W / (double)H;
+  const double jx = kGaussR * 0.5 / W, jy = kGaussR * 0.5 / H;              // jitter in NDC
+  const double amax = (1.0 + jx) * T * A / L, bmax = (1.0 + jy) * T / L;
+  const double fz_min = 3.0 / sqrt(1.0 + amax * amax + bmax * bmax), fz_max = 3.0;
+  const double rho = 0.02 * kGaussR * 1.001;
+  int n = 0;
+  auto add_object = [&](const D3* pts, int np) -> bool {
+    double sx0 = INFINITY, sx1 = -INFINITY, sy0 = INFINITY, sy1 = -INFINITY, z0 = INFINITY, z1 = -INFINITY;
+    for (int i = 0; i < np; ++i) {
+      const D3 r = dsub(pts[i], cpos);
+      const double X = ddot(r, right), Y = ddot(r, up), Z = ddot(r, ez);
+      if (!(Z > 1e-4 * (1.0 + dlen(r)))) return false;   // at or behind the camera plane (or NaN)
+      sx0 = fmin(sx0, X / Z); sx1 = fmax(sx1, X / Z);
+      sy0 = fmin(sy0, Y / Z); sy1 = fmax(sy1, Y / Z);
+      z0 = fmin(z0, Z); z1 = fmax(z1, Z);
+    }
+    const double dd = fmax(fmax(fabs(1.0 / z0 - 1.0 / fz_min), fabs(1.0 / z0 - 1.0 / fz_max)),
+                           fmax(fabs(1.0 / z1 - 1.0 / fz_min), fabs(1.0 / z1 - 1.0 / fz_max)));
+    const double del = rho * dd;
+    // slope -> NDC (the maps are decreasing), then the jitter and a margin of
+    // ~1 pixel plus 1e-4 relative for the kernel's float evaluation
+    double x0 = -(sx1 + del) * L / (T * A), x1 = -(sx0 - del) * L / (T * A);
+    double y0 = -(sy1 + del) * L / T, y1 = -(sy0 - del) * L / T;
+    const double mx = 2.0 / W + 1e-4 * (1.0 + fabs(x0) + fabs(x1)), my = 2.0 / H + 1e-4 * (1.0 + fabs(y0) + fabs(y1));
+    x0 -= jx + mx; x1 += jx + mx; y0 -= jy + my; y1 += jy + my;
+    if (!(x0 == x0 && x1 == x1 && y0 == y0 && y1 == y1)) return false;
+    float* o = rects + 4 * n++;
+    o[0] = nextafterf((float)x0, -INFINITY); o[1] = nextafterf((float)x1, INFINITY);
+    o[2] = nextafterf((float)y0, -INFINITY); o[3] = nextafterf((float)y1, INFINITY);
+    return true;
+  };
+  // root box, dilated for the slab test's float rounding
+  {
+    double m = 0.0;
+    for (int k = 0; k < 3; ++k) m = fmax(m, fmax(fabs((double)lo[k]), fabs((double)hi[k])));
+    m = 1e-4 * m + 1e-6;
+    D3 pts[8];
+    for (int i = 0; i < 8; ++i)
+      pts[i] = {(i & 1 ? hi[0] + m : lo[0] - m), (i & 2 ? hi[1] + m : lo[1] - m), (i & 4 ? hi[2] + m : lo[2] - m)};
+    if (!add_object(pts, 8)) return -1;
+  }
+  // light rectangles: pos ± right*half0 ± up*half1 with the frame of
+  // setup_lights_kernel (:261-264), halves dilated
+  for (int l = 0; l < n_lights; ++l) {
+    const pt_area_light& li = lights[l];
+    const D3 nr = d3(li.normal);
+    const double nl = dlen(nr);
+    if (!(nl > 0.0)) return -1;
+    const D3 nn = dmul(nr, 1.0 / nl);
+    // the kernel picks the basis from its float normalize; near the switch
+    // point either basis may be taken, and the rectangle's orientation is
+    // then unknown — use its circumscribed square (both orientations inside)
+    const D3 basis = fabs(nn.y) < 0.999 ? D3{0, 1, 0} : D3{1, 0, 0};
+    const D3 lr = dmul(dcross(nn, basis), 1.0 / dlen(dcross(nn, basis)));
+    const D3 lu = dcross(lr, nn);
+    double h0 = fabs((double)li.size[0]) * 0.5, h1 = fabs((double)li.size[1]) * 0.5;
+    const D3 pos = d3(li.position);
+    const double pm = fmax(fmax(fabs(pos.x), fabs(pos.y)), fabs(pos.z));
+    if (fabs(fabs(nn.y) - 0.999) < 1e-4) h0 = h1 = fmax(h0, h1) * 1.41422;
+    h0 = h0 * 1.0001 + 1e-4 * pm + 1e-6;
+    h1 = h1 * 1.0001 + 1e-4 * pm + 1e-6;
+    if (!(h0 < 1e30 && h1 < 1e30)) return -1;
+    D3 pts[8];
+    for (int i = 0; i < 4; ++i) {
+      const D3 c = dadd(dadd(pos, dmul(lr, i & 1 ? h0 : -h0)), dmul(lu, i & 2 ? h1 : -h1));
+      // a thin slab around the plane covers the float plane-intersection error
+      const double th = 1e-4 * (pm + h0 + h1) + 1e-6;
+      pts[2 * i] = dadd(c, dmul(nn, th));
+      pts[2 * i + 1] = dadd(c, dmul(nn, -th));
+    }
+    if (!add_object(pts, 8)) return -1;
+  }
+  return n;
+}
+
 }  // namespace
 
 struct pt_context {
@@ -183,6 +303,9 @@ struct pt_context {
   int opt_fresh = 0;          // PT_OPT_FRESH_BATCH0
   int opt_kernel = 0;         // PT_OPT_KERNEL: 0 auto, 1 path-recursive, 2 lane state machine
   int opt_sm_batch = 1;       // PT_OPT_SM_BATCH
+  int opt_cull = 1;           // PT_OPT_PRIMARY_CULL
+  float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};   // root AABB of the uploaded tree
+  std::vector<pt_area_light> lights_host;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   bool timed = false;
   // ring of event pairs, one per render launch since pt_reset_launch_times
@@ -289,6 +412,8 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   int rc = thread_bvh(nodes, n_nodes, (flags & PT_NODES_INT_BITS) != 0, n_indices / 3, &threaded);
   if (rc) return rc;
   collapse_implied(threaded, &collapsed);
+  float lo[3] = {threaded[0].x, threaded[0].y, threaded[0].z};   // node 0 is the root
+  float hi[3] = {threaded[1].x, threaded[1].y, threaded[1].z};
   PT_HIP(hipSetDevice(c->device));
   PT_HIP(hipStreamSynchronize(c->stream));
   dev_free(c->d_nodes);
@@ -321,6 +446,8 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   c->n_nodes = (int)(collapsed.size() / 2) - 1;
   c->n_nodes_full = (int)(threaded.size() / 2) - 1;
   c->n_tris = T;
+  memcpy(c->root_lo, lo, sizeof lo);
+  memcpy(c->root_hi, hi, sizeof hi);
   c->has_scene = true;
   return PT_OK;
 }
@@ -334,6 +461,7 @@ int pt_upload_lights(pt_context* c, const pt_area_light* lights, size_t n) {
   dev_free(c->d_lights);
   dev_free(c->d_lights_dev);
   c->n_lights = 0;
+  c->lights_host.clear();
   if (n) {
     PT_HIP(hipMalloc((void**)&c->d_lights, n * sizeof(ptd::LightRec)));
     PT_HIP(hipMalloc((void**)&c->d_lights_dev, n * sizeof(ptd::LightDev)));
@@ -342,6 +470,7 @@ int pt_upload_lights(pt_context* c, const pt_area_light* lights, size_t n) {
     PT_HIP(hipStreamSynchronize(c->stream));
   }
   c->n_lights = (int)n;
+  c->lights_host.assign(lights, lights + n);
   return PT_OK;
 }
 
@@ -474,6 +603,10 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   // shading-bound), the lane state machine once traversal dominates
   const bool sm = c->opt_kernel == 2 || (c->opt_kernel == 0 && !lds);
   if (sm) p.spl = 1;
+  p.n_cull = -1;
+  if (c->opt_cull && !c->stats_mode && !sm)
+    p.n_cull = cull_rects(c->cam, c->width, c->height, c->root_lo, c->root_hi, c->lights_host.data(),
+                          c->n_lights, &p.cull[0][0], ptd::kMaxCullRects);
   PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream));
   PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
   PT_HIP(hipEventRecord(c->ev1, c->stream));
@@ -490,6 +623,10 @@ int pt_set_option(pt_context* c, int key, int value) {
     case PT_OPT_KERNEL:
       if (value < 0 || value > 2) return fail(PT_ERR_INVALID, "PT_OPT_KERNEL takes 0, 1 or 2");
       c->opt_kernel = value;
+      return PT_OK;
+    case PT_OPT_PRIMARY_CULL:
+      if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_PRIMARY_CULL takes 0 or 1");
+      c->opt_cull = value;
       return PT_OK;
     case PT_OPT_SM_BATCH:
       if (value < 1 || value > 64) return fail(PT_ERR_INVALID, "PT_OPT_SM_BATCH takes 1..64");
@@ -710,6 +847,15 @@ int pt_pack_light(const float pos[3], const float nrm[3], const float inten[3], 
   pt::Light l({{pos[0], pos[1], pos[2]}}, {{nrm[0], nrm[1], nrm[2]}}, {{inten[0], inten[1], inten[2]}},
               {{size[0], size[1]}});
   memcpy(out, &l.getLights()[0], sizeof *out);
+  return PT_OK;
+}
+
+int pt_primary_cull_rects(const float cam[16], int w, int h, const float root_min[3], const float root_max[3],
+                          const pt_area_light* lights, int n_lights, float* rects, int max_rects, int* n_rects) {
+  if (!cam || !root_min || !root_max || !rects || !n_rects || (n_lights > 0 && !lights))
+    return fail(PT_ERR_INVALID, "null argument");
+  if (max_rects < 1) return fail(PT_ERR_INVALID, "max_rects must be >= 1");
+  *n_rects = cull_rects(cam, w, h, root_min, root_max, lights, n_lights, rects, max_rects);
   return PT_OK;
 }
 

@@ -50,7 +50,12 @@ struct RenderParams {
   int spl;                      // sample lanes per pixel: 1, 2, 4 or 8
   int fresh;                    // first_batch == 0 starts from +0 without reading accum
   int sm_batch;                 // state-machine kernel: lanes that must be waiting before shading runs
+  // primary-ray culling (pt_primary_cull_rects): -1 = trace every pixel; else
+  // a pixel traces only if its NDC origin lies in one of cull[0..n_cull)
+  int n_cull;
+  float cull[8][4];
 };
+constexpr int kMaxCullRects = 8;
 
 hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices, int n_tris, float4* d_tris,
                              hipStream_t stream);

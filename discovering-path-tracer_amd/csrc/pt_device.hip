@@ -431,6 +431,35 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
     const float ndcX0 = (2.0f * (float)px / (float)W) - 1.0f;
     const float ndcY0 = (2.0f * (float)py / (float)H) - 1.0f;
     const float aspect = (float)W / (float)H;
+    // Primary-ray culling (pt_primary_cull_rects): outside every rectangle no
+    // primary ray of this pixel can reach the root box or a light, so each
+    // sample is (0,0,0) — the value the trace below would produce.
+    bool live = true, fold = true;
+    if (P.n_cull >= 0) {
+      live = false;
+#pragma unroll
+      for (int r = 0; r < kMaxCullRects; ++r)   // static indices: P stays in SGPRs/kernarg
+        live = live || (r < P.n_cull && ndcX0 >= P.cull[r][0] && ndcX0 <= P.cull[r][1] && ndcY0 >= P.cull[r][2] &&
+                        ndcY0 <= P.cull[r][3]);
+    }
+    // A culled pixel's colours are all (0,0,0,1), so its running mean has a
+    // closed form: (acc*b + 0)/(b+1) stays +0 once it is +-0 (and becomes +0
+    // after a batch-0 fold of any finite acc, acc*0 + 0 = +0), likewise
+    // (acc*b + 1)/(b+1) stays exactly 1.  Lanes whose channels satisfy that
+    // skip the per-sample fold; any other state folds generally.
+    if (!live && active && P.n_batches > 0) {
+      bool ok = true;
+#pragma unroll
+      for (int ch = 0; ch < 4; ++ch)
+        if (ch % spl == j)
+          ok = ok && (acc[ch] == (ch < 3 ? 0.0f : 1.0f) || (P.first_batch == 0 && __builtin_isfinite(acc[ch])));
+      if (ok) {
+#pragma unroll
+        for (int ch = 0; ch < 4; ++ch)
+          if (ch % spl == j) acc[ch] = ch < 3 ? 0.0f : 1.0f;
+        fold = false;
+      }
+    }
     // Camera frame: identical in every lane, so keep one copy in SGPRs.
     const v3 right = uniform(normalize(cross(cdir, neg(cup))));
     const v3 up = uniform(normalize(cross(right, cdir)));
@@ -438,7 +467,7 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
     for (uint32_t base = 0; base < P.n_batches; base += (uint32_t)spl) {
      const uint32_t s = base + (uint32_t)j;
      float4 col4 = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
-     if (active && s < P.n_batches) {
+     if (active && live && s < P.n_batches) {
       const uint32_t batch = P.first_batch + s;
       const uint32_t seed = (batch * (uint32_t)H + (uint32_t)py) * (uint32_t)W + (uint32_t)px;   // :435
       uint32_t rng = seed;
@@ -458,12 +487,21 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
       th = (2.0f * 0x1.921fb6p+1f) * u2;
       sincos_(th, &sn, &cs);
       const float jx = r * cs, jy = r * sn;
+#ifdef PT_EXP_FASTDIV
+      const float ndcX = ndcX0 + __fdividef(jx * 0.5f, (float)W);
+      const float ndcY = ndcY0 + __fdividef(jy * 0.5f, (float)H);
+#else
       const float ndcX = ndcX0 + (jx * 0.5f) / (float)W;                 // :453-454
       const float ndcY = ndcY0 + (jy * 0.5f) / (float)H;
+#endif
       const v3 bdir = normalize(sub(add(cdir, muls(neg(right), (ndcX * tanFov) * aspect)), muls(up, ndcY * tanFov)));
       const v3 focal = add(cpos, muls(bdir, 3.0f));                       // :459
       const v3 dir = normalize(sub(focal, origin));                       // :460
+#ifdef PT_EXP_NOGEN
+      const v3 col = path_trace<STATS, !LDS>(P, cpos, normalize(mk(ndcX0, ndcY0, -1.0f)), seed, c, cand);
+#else
       const v3 col = path_trace<STATS, !LDS>(P, origin, dir, seed, c, cand);
+#endif
       col4 = make_float4(col.x, col.y, col.z, 1.0f);                      // vec4(color, 1.0)
      }
      // hand the chunk's colours to the folding lanes of the same pixel
@@ -471,7 +509,12 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
      __builtin_amdgcn_wave_barrier();
      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-     if (active) {
+#ifdef PT_EXP_NOFOLD
+     if (active) { acc[j] += col4.x; }
+     if (0) {
+#else
+     if (active && fold) {
+#endif
       const uint32_t m = min((uint32_t)spl, P.n_batches - base);
       const int first_lane = lane - j;
       for (uint32_t t = 0; t < m; ++t) {
@@ -480,7 +523,11 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
         const float* cc = (const float*)&col_buf[wave][first_lane + (int)t];
 #pragma unroll
         for (int ch = 0; ch < 4; ++ch)
+#ifdef PT_EXP_FASTDIV
+          if (ch % spl == j) acc[ch] = __fdividef(acc[ch] * fb + cc[ch], fb1);
+#else
           if (ch % spl == j) acc[ch] = (acc[ch] * fb + cc[ch]) / fb1;
+#endif
       }
      }
      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -22,6 +22,7 @@ PT_OPT_SAMPLE_LANES = 2
 PT_OPT_FRESH_BATCH0 = 3
 PT_OPT_KERNEL = 4
 PT_OPT_SM_BATCH = 5
+PT_OPT_PRIMARY_CULL = 6
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).
 EXPORTS = [
@@ -32,7 +33,7 @@ EXPORTS = [
     "pt_launch_times_ms", "pt_reset_launch_times", "pt_selftest_math",
     "pt_scene_load_obj", "pt_scene_parse_obj", "pt_scene_from_arrays", "pt_scene_build_bvh",
     "pt_scene_counts", "pt_scene_copy", "pt_scene_upload", "pt_scene_free", "pt_pack_light",
-    "pt_default_camera",
+    "pt_default_camera", "pt_primary_cull_rects",
 ]
 
 
@@ -86,6 +87,7 @@ def lib():
             "pt_scene_copy": ([vp, vp, vp, vp, vp, vp], i32), "pt_scene_upload": ([vp, vp], i32),
             "pt_scene_free": ([vp], i32), "pt_pack_light": ([vp, vp, vp, vp, vp], i32),
             "pt_default_camera": ([vp], i32),
+            "pt_primary_cull_rects": ([vp, i32, i32, vp, vp, vp, i32, vp, i32, ctypes.POINTER(i32)], i32),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -190,6 +192,21 @@ def partition_owned(width, height, nranks, rank):
     bx = (width + 15) // 16
     ys, xs = np.mgrid[0:height, 0:width]
     return ((ys // 16) * bx + xs // 16) % nranks == rank
+
+
+def primary_cull_rects(camera_ubo, width, height, root_min, root_max, lights16, max_rects=8):
+    """pt_primary_cull_rects: NDC rectangles {x0,x1,y0,y1} outside which no
+    primary ray reaches the root box or a light; None when not derivable."""
+    cam = np.ascontiguousarray(camera_ubo, np.float32).reshape(16)
+    lo = np.ascontiguousarray(root_min, np.float32).reshape(3)
+    hi = np.ascontiguousarray(root_max, np.float32).reshape(3)
+    l = np.ascontiguousarray(lights16, np.float32).reshape(-1)
+    out = np.zeros((max_rects, 4), np.float32)
+    n = ctypes.c_int(0)
+    _check(lib().pt_primary_cull_rects(cam.ctypes.data, width, height, lo.ctypes.data, hi.ctypes.data,
+                                       l.ctypes.data if l.size else None, l.size // 16, out.ctypes.data,
+                                       max_rects, ctypes.byref(n)), "pt_primary_cull_rects")
+    return None if n.value < 0 else out[:n.value].copy()
 
 
 def default_camera():

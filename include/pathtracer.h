@@ -164,7 +164,27 @@ int pt_tiles_unpack(pt_context* ctx, const void* src_device, int src_rank, void*
  * lanes of the wave need shading (1..64, default 1).  Output is identical. */
 #define PT_OPT_KERNEL 4
 #define PT_OPT_SM_BATCH 5
+/* PT_OPT_PRIMARY_CULL: 1 (default) = a pixel whose every possible primary
+ * ray provably misses the scene's root box and every light (outside all of
+ * pt_primary_cull_rects' rectangles) is not ray-generated: each of its samples
+ * is (0,0,0) exactly as the reference computes it (pre-pass misses, depth-0
+ * traceRay misses, background 0).  0 = generate and trace every sample.
+ * Path-recursive kernel only; output is identical either way. */
+#define PT_OPT_PRIMARY_CULL 6
 int pt_set_option(pt_context* ctx, int key, int value);
+
+/* Screen regions that primary rays can reach the scene or a light from.
+ * Writes up to max_rects NDC rectangles {x0, x1, y0, y1} (one per object:
+ * the root box, then each light) to rects and their count to *n_rects; a
+ * pixel whose (2px/W - 1, 2py/H - 1) lies outside all of them has no primary
+ * ray (any aperture draw, any jitter draw — Box-Muller radii are bounded by
+ * 13.23 since u1 >= 1e-38, raytrace_comp.comp:220) that hits the root box or
+ * a light.  *n_rects = -1 when no such guarantee is derived (object at or
+ * behind the camera plane, degenerate camera, more lights than max_rects-1):
+ * every pixel is then traced.  Pure host function. */
+int pt_primary_cull_rects(const float camera_ubo[16], int width, int height, const float root_min[3],
+                          const float root_max[3], const pt_area_light* lights, int n_lights, float* rects,
+                          int max_rects, int* n_rects);
 
 /* ---- instrumentation --------------------------------------------------- */
 /* Stats mode runs the reference-exhaustive traversal with counters (output is

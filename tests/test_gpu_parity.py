@@ -300,3 +300,51 @@ def test_errors_are_reported():
     bad[0, 7] = 99.0                # right child out of range
     with pytest.raises(ptamd.PTError):
         r.upload_scene(v, i, bad)
+
+
+CULL_CAMS = [
+    scenes.DEFAULT_CAMERA,
+    scenes.camera((3.0, 2.0, 4.0)),
+    scenes.camera((0.0, 0.5, 12.0), fov=100.0),
+    scenes.camera((1.0, -1.0, 7.0), fov=20.0),
+    np.array([0, 0, 14, 0, 0, 0, -2, 0, 0.3, 1, 0.2, 0, 45, 0, 0, 0], np.float32),
+    scenes.camera((0.0, 0.0, 0.5)),   # inside the box: culling not derivable
+]
+
+
+@pytest.mark.parametrize("cam", range(len(CULL_CAMS)))
+@pytest.mark.parametrize("W,H", [(96, 54), (17, 13)])
+def test_primary_culling_is_exact(cam, W, H):
+    """PT_OPT_PRIMARY_CULL on (default) and off give the oracle's frame."""
+    v, i, n = _box()
+    lights = np.concatenate([scenes.REFERENCE_LIGHT,
+                             np.array([1.5, 0.5, 2.0, 0, -1, 0, 0, 0, 3, 2, 1, 0, 0.5, 1.0, 0, 0], np.float32)])
+    ref, _ = _oracle(v, i, n, W, H, nb=4, cam=CULL_CAMS[cam], lights=lights)
+    for cull in (1, 0):
+        r = _setup(v, i, n, cam=CULL_CAMS[cam], lights=lights)
+        r.set_option(ptamd.PT_OPT_PRIMARY_CULL, cull)
+        r.resize_and_clear(W, H)
+        r.render(0, 4)
+        _assert_same(r.read_accum(), ref, f"cull={cull} cam {cam} {W}x{H}")
+
+
+def test_primary_culling_with_stale_accumulator():
+    """Culled pixels fold a non-trivial prior state exactly: camera switched
+    without a clear (first batch > 0 and first batch 0 over a finite image)."""
+    v, i, n = _box()
+    W, H = 64, 48
+    camA, camB, camC = CULL_CAMS[1], CULL_CAMS[0], CULL_CAMS[2]
+    ref, _ = _oracle(v, i, n, W, H, first=0, nb=2, cam=camA)
+    ref, _ = _oracle(v, i, n, W, H, first=2, nb=3, cam=camB, accum=ref)
+    ref2, _ = _oracle(v, i, n, W, H, first=0, nb=2, cam=camC, accum=ref.copy())
+    for spl in (1, 2, 4):
+        r = _setup(v, i, n, cam=camA)
+        r.set_option(ptamd.PT_OPT_SAMPLE_LANES, spl)
+        r.resize_and_clear(W, H)
+        r.render(0, 2)
+        r.set_camera(camB)
+        r.render(2, 3)
+        _assert_same(r.read_accum(), ref, f"spl {spl} first>0 over stale")
+        r.set_camera(camC)
+        r.render(0, 2)
+        _assert_same(r.read_accum(), ref2, f"spl {spl} first=0 over stale")

@@ -45,20 +45,22 @@ def main():
     for spec in a.variants:
         name, _, kv = spec.partition(":")
         r = ptamd.Renderer(0)
-        depth, sss = 4, 3
+        depth, sss, nlights = 4, 3, 1
         for item in filter(None, kv.split(",")):
             k, v = item.split("=")
             if k == "depth":
                 depth = int(v)
             elif k == "sss":
                 sss = int(v)
+            elif k == "nl":      # number of lights (0 or 1)
+                nlights = int(v)
             elif k == "nr":      # emulate one rank of an N-GPU tile split: nr=N (rank 0)
                 r.set_partition(int(v), 0)
             else:
                 key = ptamd.PT_OPT_SCENE_IN_LDS if k == "lds" else int(k[3:])
                 r.set_option(key, int(v))
         r.upload(scene)
-        r.upload_lights(scenes.REFERENCE_LIGHT)
+        r.upload_lights(scenes.REFERENCE_LIGHT if nlights else scenes.REFERENCE_LIGHT[:0])
         r.set_camera(cam)
         r.set_params(depth, sss)
         r.resize_and_clear(a.w, a.h)
