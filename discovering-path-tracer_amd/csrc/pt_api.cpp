@@ -16,6 +16,7 @@
 
 #include "../../include/pathtracer.h"
 #include "pt_device.h"
+#include "pt_math.h"
 #include "scene/bvh.h"
 #include "scene/camera.h"
 #include "scene/light.h"
@@ -575,6 +576,16 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
     p.cam_up[i] = c->cam[8 + i];
   }
   p.fov = c->cam[12];
+  {
+    using namespace ptm;
+    const v3 cdir = mk(p.cam_dir[0], p.cam_dir[1], p.cam_dir[2]);
+    const v3 cup = mk(p.cam_up[0], p.cam_up[1], p.cam_up[2]);
+    const v3 right = normalize(cross(cdir, neg(cup)));
+    const v3 up = normalize(cross(right, cdir));
+    p.cam_right[0] = right.x; p.cam_right[1] = right.y; p.cam_right[2] = right.z;
+    p.cam_upv[0] = up.x; p.cam_upv[1] = up.y; p.cam_upv[2] = up.z;
+    p.tan_fov = tan_(radians_(p.fov * 0.5f));
+  }
   p.blocks_x = (c->width + 15) / 16;
   p.blocks_total = p.blocks_x * ((c->height + 15) / 16);
   p.nranks = c->nranks;

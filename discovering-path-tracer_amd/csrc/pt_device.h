@@ -45,6 +45,10 @@ struct RenderParams {
   uint32_t first_batch, n_batches;
   int max_depth, sss_bounces;
   float cam_pos[3], cam_dir[3], cam_up[3], fov;
+  // camera frame of main() (:430-432) computed on the host with pt_math.h:
+  // right = normalize(cross(dir, -up)), up' = normalize(cross(right, dir)),
+  // tan(radians(fov * 0.5))
+  float cam_right[3], cam_upv[3], tan_fov;
   int blocks_x, blocks_total;   // 16x16-pixel blocks
   int nranks, rank;             // block b is rendered iff b % nranks == rank
   int spl;                      // sample lanes per pixel: 1, 2, 4 or 8

@@ -352,17 +352,40 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
   return rad;
 }
 
-// Values every lane computes identically (from kernel arguments only): read
-// lane 0's bits into an SGPR so the compiler keeps one scalar copy.
-__device__ __forceinline__ float uniform(float x) {
-  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
-}
-__device__ __forceinline__ v3 uniform(v3 a) { return mk(uniform(a.x), uniform(a.y), uniform(a.z)); }
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
+}
+
+// Running mean of n_batches constant colours (0,0,0,1) over this lane's
+// channels (c = j mod spl), op for op the fold below.  Closed form where it is
+// exact: (acc*b + 0)/(b+1) stays +0 once acc is +-0, and a batch-0 fold of
+// any finite acc gives acc*0 + 0 = +0; (acc*b + 1)/(b+1) likewise stays 1.
+__device__ __forceinline__ void fold_constant(const RenderParams& P, float* acc, int spl, int j) {
+  if (P.n_batches == 0) return;
+#pragma unroll
+  for (int ch = 0; ch < 4; ++ch) {
+    if (ch % spl != j) continue;
+    const float k = ch < 3 ? 0.0f : 1.0f;
+    if (acc[ch] == k || (P.first_batch == 0 && __builtin_isfinite(acc[ch]))) {
+      acc[ch] = k;
+    } else {
+      for (uint32_t t = 0; t < P.n_batches; ++t) {
+        const uint32_t batch = P.first_batch + t;
+        acc[ch] = (acc[ch] * (float)batch + k) / (float)(batch + 1u);
+      }
+    }
+  }
+}
+
+// This lane's channels (c = j mod spl) of the pixel's running mean.
+__device__ __forceinline__ void store_lane(float4* px, const float* acc, int spl, int j) {
+  float* a = (float*)px;
+#pragma unroll
+  for (int ch = 0; ch < 4; ++ch)
+    if (ch % spl == j) a[ch] = acc[ch];
 }
 
 // LDS=true stages the whole scene (threaded nodes + triangle records) in LDS
@@ -374,15 +397,6 @@ template <bool STATS, bool LDS>
 #endif
 __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(RenderParams P) {
   const int tid = (int)threadIdx.x;
-  if (LDS) {
-    extern __shared__ float4 lds_scene[];
-    const int nn = 2 * P.n_nodes, nt = 3 * P.n_tris;
-    for (int i = tid; i < nn; i += 256) lds_scene[i] = P.nodes[i];
-    for (int i = tid; i < nt; i += 256) lds_scene[nn + i] = P.tris[i];
-    __syncthreads();
-    P.nodes = lds_scene;
-    P.tris = lds_scene + nn;
-  }
   // Work mapping.  A 16x16 pixel tile (the partition unit) is split into
   // SPL workgroups; lane l of wave w handles pixel q = w*(64/SPL) + l/SPL of
   // its workgroup and sample slot j = l % SPL, so the SPL lanes of a pixel
@@ -406,6 +420,31 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
   const bool active = tile < P.blocks_total && px < P.width && py < P.height;   // :425-428
   Ctr c = {0u, 0u, 0u};
   const int W = P.width, H = P.height;
+  // Per-pixel constants of main() (:430-432, :446-447, :457), hoisted out of
+  // the sample loop — same values every sample.
+  const float ndcX0 = (2.0f * (float)px / (float)W) - 1.0f;
+  const float ndcY0 = (2.0f * (float)py / (float)H) - 1.0f;
+  // Primary-ray culling (pt_primary_cull_rects): outside every rectangle no
+  // primary ray of this pixel can reach the root box or a light, so each
+  // sample is (0,0,0) — the value the trace below would produce.  A workgroup
+  // with no live pixel skips the scene staging and the sample loop.
+  bool live = true;
+  bool wg_live = true;
+  if (P.n_cull >= 0) {
+    const int gx0 = bx * 16, gy0 = by * 16 + part * (16 / spl);
+    const float wx0 = (2.0f * (float)gx0 / (float)W) - 1.0f, wx1 = (2.0f * (float)(gx0 + 15) / (float)W) - 1.0f;
+    const float wy0 = (2.0f * (float)gy0 / (float)H) - 1.0f;
+    const float wy1 = (2.0f * (float)(gy0 + 16 / spl - 1) / (float)H) - 1.0f;
+    live = false;
+    wg_live = false;
+#pragma unroll
+    for (int r = 0; r < kMaxCullRects; ++r) {   // static indices: P stays in SGPRs/kernarg
+      live = live || (r < P.n_cull && ndcX0 >= P.cull[r][0] && ndcX0 <= P.cull[r][1] && ndcY0 >= P.cull[r][2] &&
+                      ndcY0 <= P.cull[r][3]);
+      wg_live = wg_live || (r < P.n_cull && wx1 >= P.cull[r][0] && wx0 <= P.cull[r][1] && wy1 >= P.cull[r][2] &&
+                            wy0 <= P.cull[r][3]);
+    }
+  }
   const size_t pix = (size_t)py * (size_t)W + (size_t)px;
   uint32_t nsamp = 0;
   if (active && (uint32_t)j < P.n_batches)
@@ -422,48 +461,30 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
     for (int ch = 0; ch < 4; ++ch)
       if (ch % spl == j) acc[ch] = a[ch];
   }
+  // A culled pixel's colours are all (0,0,0,1): its lanes fold them without
+  // the colour hand-off (fold_constant), the live pixels' lanes below.
+  if (!live && active) fold_constant(P, acc, spl, j);
+  if (!wg_live) {   // uniform per workgroup; stats mode never culls
+    if (active) store_lane(P.accum + pix, acc, spl, j);
+    return;
+  }
+  if (LDS) {
+    extern __shared__ float4 lds_scene[];
+    const int nn = 2 * P.n_nodes, nt = 3 * P.n_tris;
+    for (int i = tid; i < nn; i += 256) lds_scene[i] = P.nodes[i];
+    for (int i = tid; i < nt; i += 256) lds_scene[nn + i] = P.tris[i];
+    __syncthreads();
+    P.nodes = lds_scene;
+    P.tris = lds_scene + nn;
+  }
   {
     const v3 cpos = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
     const v3 cdir = mk(P.cam_dir[0], P.cam_dir[1], P.cam_dir[2]);
-    const v3 cup = mk(P.cam_up[0], P.cam_up[1], P.cam_up[2]);
-    // Per-pixel constants of main() (:430-432, :446-447, :457), hoisted out
-    // of the sample loop — same values every sample.
-    const float ndcX0 = (2.0f * (float)px / (float)W) - 1.0f;
-    const float ndcY0 = (2.0f * (float)py / (float)H) - 1.0f;
     const float aspect = (float)W / (float)H;
-    // Primary-ray culling (pt_primary_cull_rects): outside every rectangle no
-    // primary ray of this pixel can reach the root box or a light, so each
-    // sample is (0,0,0) — the value the trace below would produce.
-    bool live = true, fold = true;
-    if (P.n_cull >= 0) {
-      live = false;
-#pragma unroll
-      for (int r = 0; r < kMaxCullRects; ++r)   // static indices: P stays in SGPRs/kernarg
-        live = live || (r < P.n_cull && ndcX0 >= P.cull[r][0] && ndcX0 <= P.cull[r][1] && ndcY0 >= P.cull[r][2] &&
-                        ndcY0 <= P.cull[r][3]);
-    }
-    // A culled pixel's colours are all (0,0,0,1), so its running mean has a
-    // closed form: (acc*b + 0)/(b+1) stays +0 once it is +-0 (and becomes +0
-    // after a batch-0 fold of any finite acc, acc*0 + 0 = +0), likewise
-    // (acc*b + 1)/(b+1) stays exactly 1.  Lanes whose channels satisfy that
-    // skip the per-sample fold; any other state folds generally.
-    if (!live && active && P.n_batches > 0) {
-      bool ok = true;
-#pragma unroll
-      for (int ch = 0; ch < 4; ++ch)
-        if (ch % spl == j)
-          ok = ok && (acc[ch] == (ch < 3 ? 0.0f : 1.0f) || (P.first_batch == 0 && __builtin_isfinite(acc[ch])));
-      if (ok) {
-#pragma unroll
-        for (int ch = 0; ch < 4; ++ch)
-          if (ch % spl == j) acc[ch] = ch < 3 ? 0.0f : 1.0f;
-        fold = false;
-      }
-    }
-    // Camera frame: identical in every lane, so keep one copy in SGPRs.
-    const v3 right = uniform(normalize(cross(cdir, neg(cup))));
-    const v3 up = uniform(normalize(cross(right, cdir)));
-    const float tanFov = uniform(tan_(radians_(P.fov * 0.5f)));
+    // Camera frame (:430-432): computed once on the host with the same ops.
+    const v3 right = mk(P.cam_right[0], P.cam_right[1], P.cam_right[2]);
+    const v3 up = mk(P.cam_upv[0], P.cam_upv[1], P.cam_upv[2]);
+    const float tanFov = P.tan_fov;
     for (uint32_t base = 0; base < P.n_batches; base += (uint32_t)spl) {
      const uint32_t s = base + (uint32_t)j;
      float4 col4 = make_float4(0.0f, 0.0f, 0.0f, 1.0f);
@@ -487,21 +508,12 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
       th = (2.0f * 0x1.921fb6p+1f) * u2;
       sincos_(th, &sn, &cs);
       const float jx = r * cs, jy = r * sn;
-#ifdef PT_EXP_FASTDIV
-      const float ndcX = ndcX0 + __fdividef(jx * 0.5f, (float)W);
-      const float ndcY = ndcY0 + __fdividef(jy * 0.5f, (float)H);
-#else
       const float ndcX = ndcX0 + (jx * 0.5f) / (float)W;                 // :453-454
       const float ndcY = ndcY0 + (jy * 0.5f) / (float)H;
-#endif
       const v3 bdir = normalize(sub(add(cdir, muls(neg(right), (ndcX * tanFov) * aspect)), muls(up, ndcY * tanFov)));
       const v3 focal = add(cpos, muls(bdir, 3.0f));                       // :459
       const v3 dir = normalize(sub(focal, origin));                       // :460
-#ifdef PT_EXP_NOGEN
-      const v3 col = path_trace<STATS, !LDS>(P, cpos, normalize(mk(ndcX0, ndcY0, -1.0f)), seed, c, cand);
-#else
       const v3 col = path_trace<STATS, !LDS>(P, origin, dir, seed, c, cand);
-#endif
       col4 = make_float4(col.x, col.y, col.z, 1.0f);                      // vec4(color, 1.0)
      }
      // hand the chunk's colours to the folding lanes of the same pixel
@@ -509,12 +521,7 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
      __builtin_amdgcn_wave_barrier();
      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#ifdef PT_EXP_NOFOLD
-     if (active) { acc[j] += col4.x; }
-     if (0) {
-#else
-     if (active && fold) {
-#endif
+     if (active && live) {
       const uint32_t m = min((uint32_t)spl, P.n_batches - base);
       const int first_lane = lane - j;
       for (uint32_t t = 0; t < m; ++t) {
@@ -523,11 +530,7 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
         const float* cc = (const float*)&col_buf[wave][first_lane + (int)t];
 #pragma unroll
         for (int ch = 0; ch < 4; ++ch)
-#ifdef PT_EXP_FASTDIV
-          if (ch % spl == j) acc[ch] = __fdividef(acc[ch] * fb + cc[ch], fb1);
-#else
           if (ch % spl == j) acc[ch] = (acc[ch] * fb + cc[ch]) / fb1;
-#endif
       }
      }
      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -535,12 +538,7 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
-  if (active) {
-    float* a = (float*)&P.accum[pix];
-#pragma unroll
-    for (int ch = 0; ch < 4; ++ch)
-      if (ch % spl == j) a[ch] = acc[ch];
-  }
+  if (active) store_lane(P.accum + pix, acc, spl, j);
   if (STATS) {
     const unsigned long long rays = wave_sum(c.rays), nodes = wave_sum(c.nodes), leaves = wave_sum(c.leaves);
     const unsigned long long smp = wave_sum((unsigned long long)nsamp);
@@ -986,13 +984,12 @@ __global__ __launch_bounds__(256, PT_SM_MIN_BLOCKS) void render_sm_kernel(Render
   const bool active = tile < P.blocks_total && F.px < F.W && F.py < F.H;
   F.cpos = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
   F.cdir = mk(P.cam_dir[0], P.cam_dir[1], P.cam_dir[2]);
-  const v3 cup = mk(P.cam_up[0], P.cam_up[1], P.cam_up[2]);
   F.ndcX0 = (2.0f * (float)F.px / (float)F.W) - 1.0f;
   F.ndcY0 = (2.0f * (float)F.py / (float)F.H) - 1.0f;
   F.aspect = (float)F.W / (float)F.H;
-  F.right = uniform(normalize(cross(F.cdir, neg(cup))));
-  F.up = uniform(normalize(cross(F.right, F.cdir)));
-  F.tanFov = uniform(tan_(radians_(P.fov * 0.5f)));
+  F.right = mk(P.cam_right[0], P.cam_right[1], P.cam_right[2]);   // host-computed frame (:430-432)
+  F.up = mk(P.cam_upv[0], P.cam_upv[1], P.cam_upv[2]);
+  F.tanFov = P.tan_fov;
   const size_t pix = (size_t)F.py * (size_t)F.W + (size_t)F.px;
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   if (active && !(P.fresh && P.first_batch == 0)) {

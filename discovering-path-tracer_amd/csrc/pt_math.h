@@ -42,9 +42,6 @@ PT_FN float floor_(float a) { return __builtin_floorf(a); }
 // log(1+f) = f - (hfsq - s*(hfsq+R)), s = f/(2+f).  Subnormals (1e-38 is one:
 // raytrace_comp.comp:220) are pre-scaled by 2^25.
 PT_FN float log_(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(PT_EXP_FASTLOG)
-  return __logf(x);
-#endif
   uint32_t ix = f2u(x);
   int k = 0;
   if (ix < 0x00800000u) {               // +0 or +subnormal
@@ -141,9 +138,6 @@ PT_FN float cos_(float x) {
 // sin and cos of one argument sharing the reduction: bitwise the same as
 // sin_(x) and cos_(x).
 PT_FN void sincos_(float x, float* s, float* c) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(PT_EXP_FASTSC)
-  *s = __sinf(x); *c = __cosf(x); return;
-#endif
   int q;
   const float r = reduce_(x, &q);
   const float ks = ksin_(r), kc = kcos_(r);
@@ -204,11 +198,7 @@ PT_FN v3 cross(v3 a, v3 b) {
   return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 PT_FN float length(v3 a) { return sqrt_(dot(a, a)); }
-PT_FN v3 normalize(v3 a) {
-#if defined(__HIP_DEVICE_COMPILE__) && defined(PT_EXP_FASTNORM)
-  return muls(a, __builtin_amdgcn_rsqf(dot(a, a)));
-#endif
-  return muls(a, 1.0f / sqrt_(dot(a, a))); }
+PT_FN v3 normalize(v3 a) { return muls(a, 1.0f / sqrt_(dot(a, a))); }
 
 // GLSL radians(): deg * float(pi/180).
 PT_FN float radians_(float deg) { return deg * 0x1.1df46ap-6f; }
