@@ -758,6 +758,22 @@ int pt_selftest_math(int device, int fn, const float* x, float* y, size_t n) {
   return PT_OK;
 }
 
+int pt_selftest_exhaustive(int device, int fn, unsigned long long* mismatches, uint32_t* first_bad) {
+  if (!mismatches || !first_bad) return fail(PT_ERR_INVALID, "null argument");
+  if (fn < 0 || fn > 3) return fail(PT_ERR_INVALID, "fn must be 0..3");
+  PT_HIP(hipSetDevice(device));
+  unsigned long long* d_bad = nullptr;
+  PT_HIP(hipMalloc((void**)&d_bad, 16));
+  hipError_t e = hipMemset(d_bad, 0, 8);
+  if (e == hipSuccess) e = hipMemset((char*)d_bad + 8, 0xff, 4);
+  if (e == hipSuccess) e = ptd::launch_exhaustive(fn, d_bad, (uint32_t*)((char*)d_bad + 8), nullptr);
+  if (e == hipSuccess) e = hipMemcpy(mismatches, d_bad, 8, hipMemcpyDeviceToHost);
+  if (e == hipSuccess) e = hipMemcpy(first_bad, (char*)d_bad + 8, 4, hipMemcpyDeviceToHost);
+  (void)hipFree(d_bad);
+  if (e != hipSuccess) return fail(PT_ERR_HIP, std::string("pt_selftest_exhaustive: ") + hipGetErrorString(e));
+  return PT_OK;
+}
+
 // ---------------------------------------------------------------- scene ----
 
 int pt_scene_load_obj(const char* path, pt_scene** out) {

@@ -75,5 +75,6 @@ inline size_t scene_lds_bytes(const RenderParams& p) {
 }
 hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool state_machine, hipStream_t stream);
 hipError_t launch_math(int fn, const float* x, float* y, size_t n, hipStream_t stream);
+hipError_t launch_exhaustive(int fn, unsigned long long* bad, uint32_t* first_bad, hipStream_t stream);
 
 }  // namespace ptd

@@ -59,7 +59,7 @@ __device__ __forceinline__ bool tri_test(v3 o, v3 d, float4 A, float4 B, float4 
   const v3 p = cross(d, e2);
   const float det = dot(e1, p);
   if (fabs_(det) < EPS) return false;
-  const float inv = 1.0f / det;
+  const float inv = rcp_(det);
   const v3 s = sub(o, v0);
   const float u = inv * dot(s, p);
   if (u < 0.0f || u > 1.0f) return false;
@@ -100,7 +100,7 @@ __device__ __forceinline__ void test_candidates(const RenderParams& P, v3 o, v3 
 
 template <bool STATS, bool PF>
 __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* cand) {
-  const v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const v3 inv = mk(rcp_(d.x), rcp_(d.y), rcp_(d.z));
   float best = 1e30f;
   int bt = -1;
   if (STATS) c.rays++;
@@ -150,7 +150,7 @@ __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* can
 // 2/4/8 candidates measured 1-15 % slower on box.obj).
 template <bool STATS, bool PF>
 __device__ bool occluded(const RenderParams& P, v3 o, v3 d, float limit, Ctr& c) {
-  const v3 inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const v3 inv = mk(rcp_(d.x), rcp_(d.y), rcp_(d.z));
   bool occ = false;
   if (STATS) c.rays++;
   int k = 0;
@@ -187,6 +187,24 @@ __device__ bool occluded(const RenderParams& P, v3 o, v3 d, float limit, Ctr& c)
     k = next;
   }
   return occ;
+}
+
+// Lights are read-only for the whole launch and indexed by a wave-uniform
+// loop counter: reading them through the constant address space lets the
+// compiler use scalar loads (scalar cache, one load per wave) instead of a
+// per-lane vector load whose latency every shadow ray waited on.
+__device__ __forceinline__ LightDev load_light(const RenderParams& P, int i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef const __attribute__((address_space(4))) float* ConstF;
+  const ConstF f = (ConstF)(P.lights + i);
+  LightDev L;
+  float* o = (float*)&L;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(LightDev) / 4); ++k) o[k] = f[k];
+  return L;
+#else
+  return P.lights[i];
+#endif
 }
 
 // sampleAreaLight (:255-268); the light's frame (:261-264) is precomputed per
@@ -267,7 +285,7 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
   bool have_h0 = false;
   Ctr c0 = {0u, 0u, 0u};
   for (int i = 0; i < P.n_lights; ++i) {                // :311-328
-    const LightDev L = P.lights[i];
+    const LightDev L = load_light(P, i);
     float tl;
     if (intersect_area_light(ro, rd, L, &tl)) {
       if (!have_h0) {
@@ -301,14 +319,14 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
     const v3 albedo = mk(0.8f, 0.8f, 0.8f);
     v3 direct = mk(0.0f, 0.0f, 0.0f);
     for (int i = 0; i < P.n_lights; ++i) {              // :345-366
-      const LightDev L = P.lights[i];
+      const LightDev L = load_light(P, i);
       const v3 lp = sample_area_light(L, &rng);
       const v3 ld = normalize(sub(lp, hp));
       const float diff = fmax_(dot(hn, ld), 0.0f);
       const float dist = length(sub(lp, hp));
       if (!occluded<STATS, PF>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c)) {
         const float d2 = dist * dist;
-        const v3 contrib = muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), 1.0f / fmax_(d2, 0.01f));
+        const v3 contrib = muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), rcp_(fmax_(d2, 0.01f)));
         direct = add(direct, mul(albedo, contrib));
       }
     }
@@ -327,7 +345,7 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
       const v3 sn = tri_normal(P, sh.tri);
       v3 sl = mk(0.0f, 0.0f, 0.0f);
       for (int i = 0; i < P.n_lights; ++i) {
-        const LightDev L = P.lights[i];
+        const LightDev L = load_light(P, i);
         const v3 lp = sample_area_light(L, &rng);
         const v3 ed = normalize(sub(lp, cp));
         const float ediff = fmax_(dot(sn, ed), 0.0f);
@@ -335,7 +353,7 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
         if (!occluded<STATS, PF>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c)) {
           const float d2 = edist * edist;
           sl = add(sl, muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])),
-                            1.0f / fmax_(d2, 0.01f)));
+                            rcp_(fmax_(d2, 0.01f))));
         }
       }
       rad = add(rad, muls(mul(mul(thr, sss_thr), sl), 1.0f + sss_radius * 0.5f));
@@ -638,10 +656,39 @@ __global__ __launch_bounds__(256) void math_kernel(int fn, const float* __restri
     case 5: r = acos_(v); break;
     case 6: r = sqrt_(v); break;
     case 7: { uint32_t s = __float_as_uint(v); r = rng_next(&s); break; }
-    case 8: r = 1.0f / v; break;
+    case 8: r = rcp_(v); break;
     default: r = v; break;
   }
   y[i] = r;
+}
+
+// Exhaustive equivalence of the device's fast-quotient math with the IEEE
+// definitions (pt_math.h): every one of the 2^32 input bit patterns.
+// fn 0 rcp_ vs 1/x, 1 log_, 2 exp_, 3 acos_ (each vs its FAST=false
+// form).  NaN results compare equal when both are NaN.
+__global__ __launch_bounds__(256) void exhaustive_kernel(int fn, unsigned long long* bad, uint32_t* first_bad) {
+  unsigned long long nbad = 0;
+  uint32_t first = 0xffffffffu;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32); i += stride) {
+    const float x = __uint_as_float((uint32_t)i);
+    float a, b;
+    switch (fn) {
+      case 0: a = rcp_(x); b = 1.0f / x; break;
+      case 1: a = log_(x); b = log_impl<false>(x); break;
+      case 2: a = exp_(x); b = exp_impl<false>(x); break;
+      default: a = acos_(x); b = acos_impl<false>(x); break;
+    }
+    const bool same = __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
+    if (!same) {
+      ++nbad;
+      first = min(first, (uint32_t)i);
+    }
+  }
+  if (nbad) {
+    atomicAdd(bad, nbad);
+    atomicMin(first_bad, first);
+  }
 }
 
 // ===========================================================================
@@ -681,7 +728,7 @@ struct PathSt {
 __device__ __forceinline__ void trav_start(Trav& T, v3 o, v3 d, bool shadow, float limit) {
   T.o = o;
   T.d = d;
-  T.inv = mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  T.inv = mk(rcp_(d.x), rcp_(d.y), rcp_(d.z));
   T.k = 0;
   T.shadow = shadow ? 1 : 0;
   T.lim = shadow ? limit : 1e30f;
@@ -792,7 +839,7 @@ __device__ bool sm_run(const RenderParams& P, const CamFrame& F, PathSt& S, Trav
         bool need = P.max_depth > 0;
         for (int i = 0; i < P.n_lights && !need; ++i) {
           float tl;
-          need = intersect_area_light(o, d, P.lights[i], &tl);
+          need = intersect_area_light(o, d, load_light(P, i), &tl);
         }
         if (need) {
           trav_start(T, o, d, false, 0.0f);
@@ -806,7 +853,7 @@ __device__ bool sm_run(const RenderParams& P, const CamFrame& F, PathSt& S, Trav
         // light pre-pass (:311-328) on the same ray, then depth 0 (:333)
         bool lit = false;
         for (int i = 0; i < P.n_lights; ++i) {
-          const LightDev L = P.lights[i];
+          const LightDev L = load_light(P, i);
           float tl;
           if (intersect_area_light(T.o, T.d, L, &tl)) {
             if (STATS) { c.rays++; c.nodes += T.cn; c.leaves += T.cl; }
@@ -846,13 +893,13 @@ __device__ bool sm_run(const RenderParams& P, const CamFrame& F, PathSt& S, Trav
           S.li++;
         }
         if (S.li < P.n_lights) {                                            // :345-366
-          const LightDev L = P.lights[S.li];
+          const LightDev L = load_light(P, S.li);
           const v3 lp = sample_area_light(L, &S.rng);
           const v3 ld = normalize(sub(lp, S.hp));
           const float diff = fmax_(dot(S.hn, ld), 0.0f);
           const float dist = length(sub(lp, S.hp));
           const float d2 = dist * dist;
-          S.pend = muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), 1.0f / fmax_(d2, 0.01f));
+          S.pend = muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), rcp_(fmax_(d2, 0.01f)));
           trav_start(T, add(S.hp, muls(S.hn, OFFSET)), ld, true, dist - OFFSET);
           S.k = 0;
           return true;
@@ -881,13 +928,13 @@ __device__ bool sm_run(const RenderParams& P, const CamFrame& F, PathSt& S, Trav
         S.li = 0;
         S.phase = PH_SSS_SHADOW;
         if (P.n_lights > 0) {
-          const LightDev L = P.lights[0];
+          const LightDev L = load_light(P, 0);
           const v3 lp = sample_area_light(L, &S.rng);
           const v3 ed = normalize(sub(lp, S.cp));
           const float ediff = fmax_(dot(S.sn, ed), 0.0f);
           const float edist = length(sub(lp, S.cp));
           const float d2 = edist * edist;
-          S.pend = muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])), 1.0f / fmax_(d2, 0.01f));
+          S.pend = muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])), rcp_(fmax_(d2, 0.01f)));
           trav_start(T, add(S.cp, muls(S.sn, OFFSET)), ed, true, edist - OFFSET);
           return true;
         }
@@ -900,13 +947,13 @@ __device__ bool sm_run(const RenderParams& P, const CamFrame& F, PathSt& S, Trav
           S.li++;
         }
         if (S.li < P.n_lights) {
-          const LightDev L = P.lights[S.li];
+          const LightDev L = load_light(P, S.li);
           const v3 lp = sample_area_light(L, &S.rng);
           const v3 ed = normalize(sub(lp, S.cp));
           const float ediff = fmax_(dot(S.sn, ed), 0.0f);
           const float edist = length(sub(lp, S.cp));
           const float d2 = edist * edist;
-          S.pend = muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])), 1.0f / fmax_(d2, 0.01f));
+          S.pend = muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])), rcp_(fmax_(d2, 0.01f)));
           trav_start(T, add(S.cp, muls(S.sn, OFFSET)), ed, true, edist - OFFSET);
           return true;
         }
@@ -1041,6 +1088,11 @@ __global__ __launch_bounds__(256, PT_SM_MIN_BLOCKS) void render_sm_kernel(Render
 hipError_t launch_math(int fn, const float* x, float* y, size_t n, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   math_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(fn, x, y, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_exhaustive(int fn, unsigned long long* bad, uint32_t* first_bad, hipStream_t stream) {
+  exhaustive_kernel<<<8192, 256, 0, stream>>>(fn, bad, first_bad);
   return hipGetLastError();
 }
 

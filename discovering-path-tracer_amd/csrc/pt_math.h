@@ -37,11 +37,55 @@ PT_FN float fabs_(float a) { return __builtin_fabsf(a); }
 PT_FN float sqrt_(float a) { return __builtin_sqrtf(a); }
 PT_FN float floor_(float a) { return __builtin_floorf(a); }
 
+// ------------------------------------------------- fast exact quotients ----
+// Device code may evaluate a quotient through the hardware reciprocal
+// estimate plus fma refinement instead of the ~11-instruction IEEE division
+// sequence, but only where the result is identical to the IEEE quotient:
+// rcp_ is checked against 1.0f/x for all 2^32 inputs, and every unary
+// function below that uses qdiv_ internally is checked against its IEEE
+// definition (FAST=false) for all 2^32 inputs (tests/test_math.py,
+// pt_selftest_exhaustive).  Host code (and FAST=false) divides.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define PT_FAST_DEV 1
+#else
+#define PT_FAST_DEV 0
+#endif
+
+// RN(1/x): estimate y ~ 1/x (1 ulp), e = 1 - x*y exactly enough in one fma,
+// y + e*y rounds to 1/x.  Zeros, infinities, NaNs, subnormal x and |x| so
+// large that 1/x is subnormal take the IEEE division.
+PT_FN float rcp_(float x) {
+#if PT_FAST_DEV
+  const float ax = __builtin_fabsf(x);
+  if (ax >= 0x1p-126f && ax <= 0x1p126f) {
+    const float y = __builtin_amdgcn_rcpf(x);
+    const float e = __builtin_fmaf(-x, y, 1.0f);
+    return __builtin_fmaf(e, y, y);
+  }
+#endif
+  return 1.0f / x;
+}
+
+// a/b via q = a*RN(1/b) and one remainder correction (Markstein); used only
+// inside functions verified exhaustively against their IEEE definitions.
+PT_FN float qdiv_(float a, float b) {
+#if PT_FAST_DEV
+  const float y = rcp_(b);
+  const float q = a * y;
+  const float r = __builtin_fmaf(-b, q, a);
+  return __builtin_fmaf(r, y, q);
+#else
+  return a / b;
+#endif
+}
+#define PT_DIV(FAST, a, b) ((FAST) ? qdiv_((a), (b)) : (a) / (b))
+
 // ---------------------------------------------------------------- logf ----
 // fdlibm e_logf.c algorithm: x = 2^k (1+f), f in [sqrt(2)/2-1, sqrt(2)-1),
 // log(1+f) = f - (hfsq - s*(hfsq+R)), s = f/(2+f).  Subnormals (1e-38 is one:
 // raytrace_comp.comp:220) are pre-scaled by 2^25.
-PT_FN float log_(float x) {
+template <bool FAST>
+PT_FN float log_impl(float x) {
   uint32_t ix = f2u(x);
   int k = 0;
   if (ix < 0x00800000u) {               // +0 or +subnormal
@@ -60,7 +104,7 @@ PT_FN float log_(float x) {
   x = u2f(ix | (i ^ 0x3f800000u));
   k += (int)(i >> 23);
   const float f = x - 1.0f;
-  const float s = f / (2.0f + f);
+  const float s = PT_DIV(FAST, f, 2.0f + f);
   const float dk = (float)k;
   const float z = s * s;
   const float w = z * z;
@@ -70,11 +114,13 @@ PT_FN float log_(float x) {
   const float hfsq = 0.5f * f * f;
   return dk * 0x1.62e3p-1f - ((hfsq - (s * (hfsq + R) + dk * 0x1.2fefa2p-17f)) - f);
 }
+PT_FN float log_(float x) { return log_impl<PT_FAST_DEV>(x); }
 
 // ---------------------------------------------------------------- expf ----
 // fdlibm e_expf.c algorithm: k = round(x/ln2), r = hi - lo, rational kernel,
 // then scale by 2^k (two steps below the normal range).
-PT_FN float exp_(float x) {
+template <bool FAST>
+PT_FN float exp_impl(float x) {
   if (x != x) return x;
   if (x > 88.72283935546875f) return __builtin_inff();
   if (x < -103.972084045410156f) return 0.0f;
@@ -85,13 +131,14 @@ PT_FN float exp_(float x) {
   const float r = hi - lo;
   const float t = r * r;
   const float c = r - t * (0x1.555556p-3f + t * (-0x1.6c16c2p-9f + t * (0x1.1566aap-14f + t * (-0x1.bbd41cp-20f + t * 0x1.637698p-25f))));
-  const float y = 1.0f - ((lo - (r * c) / (2.0f - c)) - hi);
+  const float y = 1.0f - ((lo - PT_DIV(FAST, r * c, 2.0f - c)) - hi);
   if (k >= -125) {
     if (k > 127) return y * u2f((uint32_t)(127 + 127) << 23) * u2f((uint32_t)(k - 127 + 127) << 23);
     return y * u2f((uint32_t)(k + 127) << 23);
   }
   return (y * u2f((uint32_t)(k + 100 + 127) << 23)) * 0x1.0p-100f;
 }
+PT_FN float exp_(float x) { return exp_impl<PT_FAST_DEV>(x); }
 
 // ------------------------------------------------------- sin/cos kernels ----
 // fdlibm k_sin/k_cos polynomials on |r| <= pi/4.
@@ -152,12 +199,14 @@ PT_FN float tan_(float x) { return sin_(x) / cos_(x); }
 
 // ---------------------------------------------------------------- acosf ----
 // fdlibm e_acosf.c algorithm (rational approximation of asin, three ranges).
+template <bool FAST>
 PT_FN float acos_rat_(float z) {
   const float p = z * (0x1.555556p-3f + z * (-0x1.4d612p-2f + z * (0x1.9c155p-3f + z * (-0x1.48228cp-5f + z * (0x1.9efe08p-11f + z * 0x1.23de1p-15f)))));
   const float q = 1.0f + z * (-0x1.33a272p+1f + z * (0x1.02ae5ap+1f + z * (-0x1.6066c2p-1f + z * 0x1.3b8c5cp-4f)));
-  return p / q;
+  return PT_DIV(FAST, p, q);
 }
-PT_FN float acos_(float x) {
+template <bool FAST>
+PT_FN float acos_impl(float x) {
   const float pio2_hi = 0x1.921fb4p+0f, pio2_lo = 0x1.4442d0p-24f, pi_ = 0x1.921fb4p+1f;
   const uint32_t ix = f2u(x) & 0x7fffffffu;
   if (ix == 0x3f800000u) return (f2u(x) >> 31) ? pi_ + 2.0f * pio2_lo : 0.0f;
@@ -165,24 +214,25 @@ PT_FN float acos_(float x) {
   if (ix < 0x3f000000u) {                      // |x| < 0.5
     if (ix <= 0x32800000u) return pio2_hi + pio2_lo;
     const float z = x * x;
-    const float r = acos_rat_(z);
+    const float r = acos_rat_<FAST>(z);
     return pio2_hi - (x - (pio2_lo - x * r));
   }
   if (f2u(x) >> 31) {                          // x <= -0.5
     const float z = (1.0f + x) * 0.5f;
     const float s = sqrt_(z);
-    const float r = acos_rat_(z);
+    const float r = acos_rat_<FAST>(z);
     const float w = r * s - pio2_lo;
     return pi_ - 2.0f * (s + w);
   }
   const float z = (1.0f - x) * 0.5f;           // x >= 0.5
   const float s = sqrt_(z);
   const float df = u2f(f2u(s) & 0xfffff000u);
-  const float c = (z - df * df) / (s + df);
-  const float r = acos_rat_(z);
+  const float c = PT_DIV(FAST, z - df * df, s + df);
+  const float r = acos_rat_<FAST>(z);
   const float w = r * s + c;
   return 2.0f * (df + w);
 }
+PT_FN float acos_(float x) { return acos_impl<PT_FAST_DEV>(x); }
 
 // -------------------------------------------------------------- vec3 ops ----
 struct v3 { float x, y, z; };
@@ -198,7 +248,7 @@ PT_FN v3 cross(v3 a, v3 b) {
   return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
 PT_FN float length(v3 a) { return sqrt_(dot(a, a)); }
-PT_FN v3 normalize(v3 a) { return muls(a, 1.0f / sqrt_(dot(a, a))); }
+PT_FN v3 normalize(v3 a) { return muls(a, rcp_(sqrt_(dot(a, a)))); }
 
 // GLSL radians(): deg * float(pi/180).
 PT_FN float radians_(float deg) { return deg * 0x1.1df46ap-6f; }

@@ -30,7 +30,7 @@ EXPORTS = [
     "pt_upload_scene", "pt_upload_lights", "pt_set_camera", "pt_set_params", "pt_resize_and_clear",
     "pt_bind_accum", "pt_clear_accum", "pt_accum_device_ptr", "pt_read_accum", "pt_dispatch", "pt_render",
     "pt_set_partition", "pt_tiles_owned", "pt_tiles_pack", "pt_tiles_unpack", "pt_set_option", "pt_set_stats_mode", "pt_get_stats", "pt_reset_stats", "pt_last_launch_ms",
-    "pt_launch_times_ms", "pt_reset_launch_times", "pt_selftest_math",
+    "pt_launch_times_ms", "pt_reset_launch_times", "pt_selftest_math", "pt_selftest_exhaustive",
     "pt_scene_load_obj", "pt_scene_parse_obj", "pt_scene_from_arrays", "pt_scene_build_bvh",
     "pt_scene_counts", "pt_scene_copy", "pt_scene_upload", "pt_scene_free", "pt_pack_light",
     "pt_default_camera", "pt_primary_cull_rects",
@@ -79,6 +79,7 @@ def lib():
             "pt_reset_stats": ([vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
             "pt_launch_times_ms": ([vp, vp, sz, psz], i32), "pt_reset_launch_times": ([vp], i32),
             "pt_selftest_math": ([i32, i32, vp, vp, sz], i32),
+            "pt_selftest_exhaustive": ([i32, i32, ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(u32)], i32),
             "pt_scene_load_obj": ([ctypes.c_char_p, ctypes.POINTER(vp)], i32),
             "pt_scene_parse_obj": ([ctypes.c_char_p, sz, ctypes.POINTER(vp)], i32),
             "pt_scene_from_arrays": ([vp, sz, vp, sz, ctypes.POINTER(vp)], i32),
@@ -90,6 +91,8 @@ def lib():
             "pt_primary_cull_rects": ([vp, i32, i32, vp, vp, vp, i32, vp, i32, ctypes.POINTER(i32)], i32),
         }
         for name, (args, res) in sig.items():
+            if not hasattr(L, name):   # older library (A/B timing); calls to it fail loudly
+                continue
             f = getattr(L, name)
             f.argtypes = args
             f.restype = res
@@ -184,6 +187,17 @@ def device_math(fn, x, device=0):
     y = np.empty_like(x)
     _check(lib().pt_selftest_math(device, fn, x.ctypes.data, y.ctypes.data, x.size), "pt_selftest_math")
     return y
+
+
+def device_math_exhaustive(fn, device=0):
+    """pt_selftest_exhaustive: (mismatching inputs, smallest such bit pattern)
+    of the device's fast-quotient fn (0 rcp, 1 log, 2 exp, 3 acos)
+    against its IEEE definition over all 2^32 inputs."""
+    bad = ctypes.c_ulonglong(0)
+    first = ctypes.c_uint32(0)
+    _check(lib().pt_selftest_exhaustive(device, fn, ctypes.byref(bad), ctypes.byref(first)),
+           "pt_selftest_exhaustive")
+    return bad.value, first.value
 
 
 def partition_owned(width, height, nranks, rank):

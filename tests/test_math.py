@@ -107,3 +107,13 @@ def test_device_rng_bitwise_equals_oracle():
     assert np.array_equal(dev[:2000].view(np.uint32), ref.view(np.uint32))
     ref_all = O.math(FN["rng"], seeds.view(np.float32))
     assert np.array_equal(dev.view(np.uint32), ref_all.view(np.uint32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fn,name", [(0, "rcp"), (1, "log"), (2, "exp"), (3, "acos")])
+def test_device_fast_quotients_exhaustive(fn, name):
+    """The device evaluates these through rcp/fma quotients instead of IEEE
+    division; all 2^32 inputs must give the IEEE definition's bits (pt_math.h)."""
+    import ptamd
+    bad, first = ptamd.device_math_exhaustive(fn)
+    assert bad == 0, f"{name}: {bad} of 2^32 inputs differ, first 0x{first:08x}"
