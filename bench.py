@@ -32,6 +32,9 @@ sys.path.insert(0, os.path.join(ROOT, "discovering-path-tracer_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# VALU issue peak: 1024 SIMDs x 2.4 GHz, one wave64 f32 instruction per 2
+# cycles per SIMD (MI355X_MICROARCH.md constants: v_fma_f32 2 cyc on SIMD-32)
+VALU_PEAK_GINST = 1024 * 2.4 / 2
 DEPTH, SSS = 4, 3
 
 
@@ -65,7 +68,8 @@ def profiled_traffic():
     """HBM bytes per launch of the current kernel source from the newest
     committed rocprofv3 PMC summary (tools/gpu_profile.sh ->
     tools/summarize_profile.py): FETCH_SIZE (x2, gfx950) + WRITE_SIZE.
-    None if no summary was taken of this exact pt_device.hip."""
+    None if no summary was taken of this exact pt_device.hip.  Also returns
+    the summary's VALU wave-instruction count per launch when present."""
     import glob
     import hashlib
     src = os.path.join(ROOT, "discovering-path-tracer_amd", "csrc", "pt_device.hip")
@@ -77,7 +81,8 @@ def profiled_traffic():
         except ValueError:
             continue
         if d.get("pt_device_hip_sha1") == h and "hbm_bytes_per_launch" in d:
-            best = (os.path.relpath(p, ROOT), d["hbm_bytes_per_launch"]["total"])
+            best = (os.path.relpath(p, ROOT), d["hbm_bytes_per_launch"]["total"],
+                    d.get("sq_per_launch", {}).get("SQ_INSTS_VALU"))
     return best
 
 
@@ -109,6 +114,8 @@ def main():
     ap.add_argument("--collective", choices=["gather", "reduce"], default="gather")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="N>1: compare the assembled frame with a 1-GPU render")
+    ap.add_argument("--compare-no-cull", action="store_true",
+                    help="N=1: also time the same steps with primary-ray culling off (reported as primary_cull_off)")
     args = ap.parse_args()
     W, H, SPP = args.width, args.height, args.spp
 
@@ -254,6 +261,23 @@ def main():
         t = allreduce_max(torch.tensor([dt, kernel_ms], dtype=torch.float64, device=dev))
         dt, kernel_ms = float(t[0]), float(t[1])
 
+    no_cull = None
+    if world == 1 and args.compare_no_cull:
+        # the same frames with primary-ray culling off (every pixel generated
+        # and traced), for reference next to the default
+        r.set_option(ptamd.PT_OPT_PRIMARY_CULL, 0)
+        for _ in range(args.warmup):
+            step()
+        r.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        r.synchronize()
+        dt_nc = time.perf_counter() - t1
+        r.set_option(ptamd.PT_OPT_PRIMARY_CULL, 1)
+        no_cull = {"ms_per_step": round(dt_nc / args.steps * 1e3, 4),
+                   "value": round(rays_per_frame * args.steps / dt_nc / 1e6, 3)}
+
     verified = None
     if args.verify and dist is not None and rank == 0:
         # the assembled frame must be bitwise the single-GPU frame
@@ -296,6 +320,7 @@ def main():
                        "sss_bounces": SSS,
                        "parallelism": f"tiles{world}-{args.collective}" if world > 1 else "single",
                        "rays_per_frame": int(rays_per_frame),
+                       "primary_cull": True,
                        "msamples_per_s": round(W * H * SPP * args.steps / dt / 1e6, 3)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -304,6 +329,16 @@ def main():
                          "kernel": "render_kernel<false,*>", "kernel_ms": round(kernel_ms, 4),
                          "algorithmic_bytes_per_launch": int(own_bytes)},
         }
+        if prof is not None and prof[2]:
+            # the box frame is bound by vector-instruction issue, not HBM (its
+            # scene lives in LDS): VALU wave-instructions per launch from the
+            # committed PMC profile over the measured kernel time
+            gi = prof[2] / (kernel_ms * 1e-3) / 1e9
+            out_line["roofline_valu"] = {"bound": "valu_issue", "achieved": round(gi, 2), "peak": VALU_PEAK_GINST,
+                                         "unit": "G wave-instr/s", "frac": round(gi / VALU_PEAK_GINST, 4),
+                                         "valu_wave_instr_per_launch": int(prof[2]), "source": prof[0]}
+        if no_cull is not None:
+            out_line["primary_cull_off"] = no_cull
         if verified is not None:
             out_line["verified_bitwise_vs_single_gpu"] = verified
         if world == 1 and not args.no_cpu_baseline:

@@ -595,11 +595,12 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   if (c->opt_sample_lanes) {
     p.spl = c->opt_sample_lanes;
   } else {
-    // auto: 2 sample lanes per pixel on a whole frame; finer work units as
-    // the frame is split over more GPUs (each GPU's share gets smaller while
-    // its heaviest workgroup does not) — measured on box.obj 1080p 8spp.
-    // Never more lanes than samples.
-    int want = c->nranks >= 4 ? 8 : c->nranks >= 2 ? 4 : 2;
+    // auto: 4 sample lanes per pixel on a whole frame or a 1/2-1/3 share,
+    // 8 on smaller shares (each GPU's share of the frame shrinks while its
+    // heaviest workgroup does not) — measured on box.obj 1080p 8spp with
+    // primary culling: N=1 spl 1/2/4/8 = 0.524/0.469/0.455/0.544 ms,
+    // 1/8 share 0.315/0.186/0.127/0.093 ms.  Never more lanes than samples.
+    int want = c->nranks >= 4 ? 8 : 4;
     while (want > 1 && (uint32_t)want > n_batches) want >>= 1;
     p.spl = want;
   }
@@ -610,9 +611,10 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   const bool fits = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
   if (c->opt_scene_lds == 2 && !fits) return fail(PT_ERR_UNSUPPORTED, "scene too large for the LDS variant");
   const bool lds = c->opt_scene_lds == 2 || (c->opt_scene_lds == 1 && fits);
-  // auto: the path-recursive kernel while the scene fits in LDS (short walks,
-  // shading-bound), the lane state machine once traversal dominates
-  const bool sm = c->opt_kernel == 2 || (c->opt_kernel == 0 && !lds);
+  // auto: the path-recursive kernel.  The lane state machine is kept as an
+  // option; it was measured slower on every scene (1080p: displaced sphere
+  // 8 spp 1022 vs 596 ms, 1M-triangle cloud 1 spp 191 vs 127 ms).
+  const bool sm = c->opt_kernel == 2;
   if (sm) p.spl = 1;
   p.n_cull = -1;
   if (c->opt_cull && !c->stats_mode && !sm)

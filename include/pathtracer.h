@@ -158,8 +158,8 @@ int pt_tiles_unpack(pt_context* ctx, const void* src_device, int src_rank, void*
  * pt_clear_accum + pt_render give, minus a clear and a read of the image.
  * 0 (default) = read the accumulator, as the reference does (prev * 0). */
 #define PT_OPT_FRESH_BATCH0 3
-/* PT_OPT_KERNEL: 0 auto (path-recursive while the scene fits in LDS, lane
- * state machine otherwise), 1 path-recursive, 2 lane state machine.
+/* PT_OPT_KERNEL: 0 auto (path-recursive), 1 path-recursive, 2 lane state
+ * machine (slower on every scene measured; kept for comparison).
  * PT_OPT_SM_BATCH: state machine only — finished rays wait until this many
  * lanes of the wave need shading (1..64, default 1).  Output is identical. */
 #define PT_OPT_KERNEL 4

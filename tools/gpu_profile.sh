@@ -11,8 +11,9 @@ STEPS=${STEPS:-20}
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
   python3 bench.py --steps $STEPS --warmup 2 --no-cpu-baseline > $OUT/bench_trace.log 2>&1 || { echo "trace rc=$?"; tail -20 $OUT/bench_trace.log; exit 1; }
 tail -2 $OUT/bench_trace.log
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$c -o run -- \
-    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/bench_$c.log 2>&1 || { echo "pmc $c rc=$?"; tail -20 $OUT/bench_$c.log; exit 1; }
+for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES"; do
+  n=${c%% *}
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$n -o run -- \
+    python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline > $OUT/bench_$n.log 2>&1 || { echo "pmc $c rc=$?"; tail -20 $OUT/bench_$n.log; exit 1; }
 done
 find $OUT -name '*.csv' | head -20

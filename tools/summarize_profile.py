@@ -34,6 +34,14 @@ def main(tag, kernel_substr="render_kernel<false, "):
                 if kernel_substr in r["Kernel_Name"] and r["Counter_Name"] == c]
         if vals:
             pmc[c] = sum(vals) / len(vals)
+    sq = {}
+    path = os.path.join(src, "pmc_SQ_INSTS_VALU", "run_counter_collection.csv")
+    if os.path.exists(path):
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"):
+            vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+                    if kernel_substr in r["Kernel_Name"] and r["Counter_Name"] == c]
+            if vals:
+                sq[c] = sum(vals) / len(vals)
     import hashlib
     src_hash = hashlib.sha1(open(os.path.join(ROOT, "discovering-path-tracer_amd", "csrc", "pt_device.hip"),
                                  "rb").read()).hexdigest()
@@ -43,6 +51,8 @@ def main(tag, kernel_substr="render_kernel<false, "):
         write = pmc["WRITE_SIZE"] * 1024
         out["hbm_bytes_per_launch"] = {"fetch_corrected": fetch, "write": write, "total": fetch + write,
                                        "raw_fetch_kib": pmc["FETCH_SIZE"], "raw_write_kib": pmc["WRITE_SIZE"]}
+    if sq:
+        out["sq_per_launch"] = sq
     for log in ("bench_trace.log",):
         p = os.path.join(src, log)
         if os.path.exists(p):
