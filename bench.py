@@ -35,7 +35,6 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # VALU issue peak: 1024 SIMDs x 2.4 GHz, one wave64 f32 instruction per 2
 # cycles per SIMD (MI355X_MICROARCH.md constants: v_fma_f32 2 cyc on SIMD-32)
 VALU_PEAK_GINST = 1024 * 2.4 / 2
-DEPTH, SSS = 4, 3
 
 
 def algorithmic_bytes(st):
@@ -86,7 +85,7 @@ def profiled_traffic():
     return best
 
 
-def cpu_baseline(v, i, n, cam, light, W, H, spp):
+def cpu_baseline(v, i, n, cam, light, W, H, spp, DEPTH, SSS):
     """The oracle (scalar C++ restatement of raytrace_comp.comp) on this host,
     all cores, on a bounded sample of the same workload."""
     import oracle_lib
@@ -111,6 +110,8 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=8)
+    ap.add_argument("--depth", type=int, default=4, help="MAX_DEPTH (reference 4; SURVEY §8d config 4 uses 8)")
+    ap.add_argument("--sss", type=int, default=3, help="SSS_MAX_BOUNCES (reference 3)")
     ap.add_argument("--collective", choices=["gather", "reduce"], default="gather")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="N>1: compare the assembled frame with a 1-GPU render")
@@ -118,6 +119,7 @@ def main():
                     help="N=1: also time the same steps with primary-ray culling off (reported as primary_cull_off)")
     args = ap.parse_args()
     W, H, SPP = args.width, args.height, args.spp
+    DEPTH, SSS = args.depth, args.sss
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -300,7 +302,7 @@ def main():
         # per-GPU launch: rank 0's share of the algorithmic bytes over the slowest rank's kernel time
         own_bytes = algorithmic_bytes({"nodes": mine[1], "leaf_tests": mine[2], "samples": mine[3]})
         achieved = own_bytes / (kernel_ms * 1e-3) / 1e9
-        default_cfg = args.scene == "box" and (W, H, SPP) == (1920, 1080, 8)
+        default_cfg = args.scene == "box" and (W, H, SPP, DEPTH, SSS) == (1920, 1080, 8, 4, 3)
         prof = profiled_traffic() if (world == 1 and default_cfg) else None
         wl = f"{scene_desc} {W}x{H} {SPP}spp {DEPTH} bounces {SSS} sss"
         out_line = {
@@ -342,7 +344,7 @@ def main():
         if verified is not None:
             out_line["verified_bitwise_vs_single_gpu"] = verified
         if world == 1 and not args.no_cpu_baseline:
-            out_line["cpu_baseline"] = cpu_baseline(v, i, n, cam, light, W, H, SPP)
+            out_line["cpu_baseline"] = cpu_baseline(v, i, n, cam, light, W, H, SPP, DEPTH, SSS)
         print(json.dumps(out_line), flush=True)
     if dist is not None:
         dist.barrier()
