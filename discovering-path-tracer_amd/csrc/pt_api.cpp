@@ -865,6 +865,116 @@ int pt_scene_upload(pt_context* c, const pt_scene* s) {
                          s->obj.materialIds.size(), s->flags);
 }
 
+// ---- binary scene cache ---------------------------------
+// Skips OBJ parsing and the BVH build for large meshes.  Layout: "PTSCENE1",
+// u32 version, u32 flags (PT_NODES_INT_BITS), u64 counts of vertex floats,
+// OBJ indices, BVH-order indices, nodes, uv floats, material ids, u64 shapes,
+// then the six arrays, then a u64 FNV-1a hash of everything before it (taken
+// over 8-byte words, the tail bytewise).
+namespace {
+constexpr char kCacheMagic[8] = {'P', 'T', 'S', 'C', 'E', 'N', 'E', '1'};
+constexpr uint32_t kCacheVersion = 1;
+
+struct Fnv {
+  uint64_t h = 1469598103934665603ull;
+  void add(const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+      uint64_t w;
+      memcpy(&w, b + i, 8);
+      h = (h ^ w) * 1099511628211ull;
+    }
+    for (; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  }
+};
+}  // namespace
+
+int pt_scene_save(const pt_scene* s, const char* path) {
+  if (!s || !path) return fail(PT_ERR_INVALID, "null argument");
+  if (s->nodes.empty()) return fail(PT_ERR_INVALID, "build the BVH first (pt_scene_build_bvh)");
+  FILE* f = fopen(path, "wb");
+  if (!f) return fail(PT_ERR_IO, std::string("cannot create ") + path);
+  Fnv h;
+  bool ok = true;
+  auto put = [&](const void* p, size_t n) {
+    if (n && ok) ok = fwrite(p, 1, n, f) == n;
+    h.add(p, n);
+  };
+  const uint64_t counts[7] = {s->obj.vertices.size(), s->obj.indices.size(), s->bvh_indices.size(), s->nodes.size(),
+                              s->obj.texcoords.size(), s->obj.materialIds.size(), (uint64_t)s->obj.shapes};
+  put(kCacheMagic, 8);
+  put(&kCacheVersion, 4);
+  put(&s->flags, 4);
+  put(counts, sizeof counts);
+  put(s->obj.vertices.data(), counts[0] * 4);
+  put(s->obj.indices.data(), counts[1] * 4);
+  put(s->bvh_indices.data(), counts[2] * 4);
+  put(s->nodes.data(), counts[3] * sizeof(pt::BVHNode));
+  put(s->obj.texcoords.data(), counts[4] * 4);
+  put(s->obj.materialIds.data(), counts[5] * 4);
+  const uint64_t digest = h.h;
+  if (ok) ok = fwrite(&digest, 1, 8, f) == 8;
+  if (fclose(f) != 0) ok = false;
+  if (!ok) return fail(PT_ERR_IO, std::string("write failed: ") + path);
+  return PT_OK;
+}
+
+int pt_scene_load_cache(const char* path, pt_scene** out) {
+  if (!path || !out) return fail(PT_ERR_INVALID, "null argument");
+  *out = nullptr;
+  FILE* f = fopen(path, "rb");
+  if (!f) return fail(PT_ERR_IO, std::string("cannot open ") + path);
+  Fnv h;
+  bool ok = true;
+  auto get = [&](void* p, size_t n) {
+    if (n && ok) ok = fread(p, 1, n, f) == n;
+    if (ok) h.add(p, n);
+  };
+  char magic[8];
+  uint32_t version = 0, flags = 0;
+  uint64_t counts[7] = {0};
+  get(magic, 8);
+  get(&version, 4);
+  get(&flags, 4);
+  get(counts, sizeof counts);
+  if (!ok || memcmp(magic, kCacheMagic, 8) != 0 || version != kCacheVersion) {
+    fclose(f);
+    return fail(PT_ERR_IO, std::string("not a scene cache (or another version): ") + path);
+  }
+  const uint64_t nt = counts[1] / 3;
+  if (counts[0] % 3 || counts[1] % 3 || counts[1] == 0 || counts[2] != counts[1] || counts[3] != 2 * nt - 1 ||
+      counts[5] > (1ull << 34) || counts[0] > (1ull << 36) || counts[4] > (1ull << 36)) {
+    fclose(f);
+    return fail(PT_ERR_IO, std::string("inconsistent scene cache header: ") + path);
+  }
+  pt_scene* s = new pt_scene();
+  s->flags = flags;
+  s->obj.vertices.resize(counts[0]);
+  s->obj.indices.resize(counts[1]);
+  s->bvh_indices.resize(counts[2]);
+  s->nodes.resize(counts[3]);
+  s->obj.texcoords.resize(counts[4]);
+  s->obj.materialIds.resize(counts[5]);
+  s->obj.shapes = (size_t)counts[6];
+  get(s->obj.vertices.data(), counts[0] * 4);
+  get(s->obj.indices.data(), counts[1] * 4);
+  get(s->bvh_indices.data(), counts[2] * 4);
+  get(s->nodes.data(), counts[3] * sizeof(pt::BVHNode));
+  get(s->obj.texcoords.data(), counts[4] * 4);
+  get(s->obj.materialIds.data(), counts[5] * 4);
+  uint64_t digest = 0;
+  const uint64_t want = h.h;
+  if (ok) ok = fread(&digest, 1, 8, f) == 8;
+  fclose(f);
+  if (!ok || digest != want) {
+    delete s;
+    return fail(PT_ERR_IO, std::string("scene cache truncated or corrupt: ") + path);
+  }
+  *out = s;
+  return PT_OK;
+}
+
 int pt_scene_free(pt_scene* s) {
   delete s;
   return PT_OK;

@@ -78,6 +78,85 @@ float next_real(const char** tok) {
   return (float)v;
 }
 
+// pnpoly point-in-polygon crossing test (tiny_obj_loader.h:1438-1450), in
+// the same float evaluation order.
+bool point_in_tri(const float* px, const float* py, float tx, float ty) {
+  bool in = false;
+  for (int i = 0, j = 2; i < 3; j = i++) {
+    if (((py[i] > ty) != (py[j] > ty)) && (tx < (px[j] - px[i]) * (ty - py[i]) / (py[j] - py[i]) + px[i]))
+      in = !in;
+  }
+  return in;
+}
+
+// tinyobj's built-in ear clipping for faces of 5+ corners
+// (tiny_obj_loader.h:1740-1955, TINYOBJLOADER_USE_MAPBOX_EARCUT undefined as
+// in the reference build): project on the two axes picked from the first
+// corner with a non-degenerate cross product, then repeatedly cut the ear at
+// the current guess vertex — skipping reflex corners (cross * area < 0, area
+// from the first two projected corners only, as tinyobj computes it) and
+// corners whose triangle contains another remaining vertex — and finally
+// emit the last three.  A face it cannot finish keeps only the ears found.
+void ear_clip(const std::vector<int>& face, const float* v, std::vector<uint32_t>* tris) {
+  const size_t n = face.size();
+  int ax0 = 1, ax1 = 2;
+  for (size_t k = 0; k < n; ++k) {
+    const float* a = v + 3 * face[k % n];
+    const float* b = v + 3 * face[(k + 1) % n];
+    const float* c = v + 3 * face[(k + 2) % n];
+    const float e0x = b[0] - a[0], e0y = b[1] - a[1], e0z = b[2] - a[2];
+    const float e1x = c[0] - b[0], e1y = c[1] - b[1], e1z = c[2] - b[2];
+    const float cx = fabsf(e0y * e1z - e0z * e1y);
+    const float cy = fabsf(e0z * e1x - e0x * e1z);
+    const float cz = fabsf(e0x * e1y - e0y * e1x);
+    const float eps = 1.19209290e-07f;   // numeric_limits<float>::epsilon()
+    if (cx > eps || cy > eps || cz > eps) {
+      if (!(cx > cy && cx > cz)) {
+        ax0 = 0;
+        if (cz > cx && cz > cy) ax1 = 1;
+      }
+      break;
+    }
+  }
+  std::vector<int> rem = face;
+  size_t guess = 0, left = n, prev = n;
+  while (rem.size() > 3 && left > 0) {
+    const size_t m = rem.size();
+    if (guess >= m) guess -= m;
+    if (prev != m) {
+      prev = m;
+      left = m;
+    } else {
+      --left;
+    }
+    int ind[3];
+    float px[3], py[3];
+    for (int k = 0; k < 3; ++k) {
+      ind[k] = rem[(guess + k) % m];
+      px[k] = v[3 * ind[k] + ax0];
+      py[k] = v[3 * ind[k] + ax1];
+    }
+    const float cross = (px[1] - px[0]) * (py[2] - py[1]) - (py[1] - py[0]) * (px[2] - px[1]);
+    const float area = (px[0] * py[1] - py[0] * px[1]) * 0.5f;
+    if (cross * area < 0.0f) {   // reflex corner
+      ++guess;
+      continue;
+    }
+    bool overlap = false;
+    for (size_t o = 3; o < m && !overlap; ++o) {
+      const int w = rem[(guess + o) % m];
+      overlap = point_in_tri(px, py, v[3 * w + ax0], v[3 * w + ax1]);
+    }
+    if (overlap) {
+      ++guess;
+      continue;
+    }
+    tris->insert(tris->end(), {(uint32_t)ind[0], (uint32_t)ind[1], (uint32_t)ind[2]});
+    rem.erase(rem.begin() + (long)((guess + 1) % m));
+  }
+  if (rem.size() == 3) tris->insert(tris->end(), {(uint32_t)rem[0], (uint32_t)rem[1], (uint32_t)rem[2]});
+}
+
 }  // namespace
 
 int parse_obj(const char* text, size_t len, ObjScene* out, std::string* err) {
@@ -152,9 +231,10 @@ int parse_obj(const char* text, size_t len, ObjScene* out, std::string* err) {
         else
           out->indices.insert(out->indices.end(), {(uint32_t)a, (uint32_t)b, (uint32_t)d, (uint32_t)b, (uint32_t)c, (uint32_t)d});
         out->materialIds.insert(out->materialIds.end(), {mat, mat});
-      } else {
-        if (err) *err = "faces with more than 4 corners (tinyobj ear clipping) are not supported, line " + std::to_string(line_no);
-        return -3;
+      } else {                                                    // :1740-1955
+        const size_t before = out->indices.size();
+        ear_clip(face, out->vertices.data(), &out->indices);
+        out->materialIds.insert(out->materialIds.end(), (out->indices.size() - before) / 3, mat);
       }
     }
   }

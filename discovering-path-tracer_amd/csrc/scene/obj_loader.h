@@ -6,8 +6,8 @@
 // quads are split on the shorter diagonal exactly as :1509-1604, so the
 // triangle order — which the BVH builder's unstable sort depends on — is the
 // reference's.  Faces with more than four corners take tinyobj's built-in
-// ear-clipping path (:1740+), which is not yet restated: they are rejected
-// with an error rather than triangulated differently.
+// ear-clipping path (:1740-1955), restated here (the reference build does not
+// define TINYOBJLOADER_USE_MAPBOX_EARCUT).
 #pragma once
 #include <stdint.h>
 #include <string>

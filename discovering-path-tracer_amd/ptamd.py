@@ -33,7 +33,7 @@ EXPORTS = [
     "pt_launch_times_ms", "pt_reset_launch_times", "pt_selftest_math", "pt_selftest_exhaustive",
     "pt_scene_load_obj", "pt_scene_parse_obj", "pt_scene_from_arrays", "pt_scene_build_bvh",
     "pt_scene_counts", "pt_scene_copy", "pt_scene_upload", "pt_scene_free", "pt_pack_light",
-    "pt_default_camera", "pt_primary_cull_rects",
+    "pt_default_camera", "pt_primary_cull_rects", "pt_scene_save", "pt_scene_load_cache",
 ]
 
 
@@ -89,6 +89,8 @@ def lib():
             "pt_scene_free": ([vp], i32), "pt_pack_light": ([vp, vp, vp, vp, vp], i32),
             "pt_default_camera": ([vp], i32),
             "pt_primary_cull_rects": ([vp, i32, i32, vp, vp, vp, i32, vp, i32, ctypes.POINTER(i32)], i32),
+            "pt_scene_save": ([vp, ctypes.c_char_p], i32),
+            "pt_scene_load_cache": ([ctypes.c_char_p, ctypes.POINTER(vp)], i32),
         }
         for name, (args, res) in sig.items():
             if not hasattr(L, name):   # older library (A/B timing); calls to it fail loudly
@@ -134,6 +136,17 @@ class Scene:
         h = ctypes.c_void_p()
         _check(lib().pt_scene_from_arrays(_ptr(v), v.size, _ptr(i), i.size, ctypes.byref(h)), "pt_scene_from_arrays")
         return cls(h)
+
+    @classmethod
+    def load_cache(cls, path):
+        """pt_scene_load_cache: a scene written by save() (BVH included)."""
+        h = ctypes.c_void_p()
+        _check(lib().pt_scene_load_cache(str(path).encode(), ctypes.byref(h)), "pt_scene_load_cache")
+        return cls(h)
+
+    def save(self, path):
+        _check(lib().pt_scene_save(self._h, str(path).encode()), "pt_scene_save")
+        return self
 
     def build_bvh(self, int_bits=False, threads=0):
         self.int_bits = int_bits

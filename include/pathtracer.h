@@ -226,6 +226,11 @@ int pt_scene_copy(const pt_scene* scene, float* vertices, uint32_t* indices, pt_
                   float* uvs, uint32_t* mat_indices);
 int pt_scene_upload(pt_context* ctx, const pt_scene* scene);
 int pt_scene_free(pt_scene* scene);
+/* Binary scene cache (skip OBJ parse + BVH build for large
+ * meshes): everything pt_scene_copy returns, with an FNV-1a checksum.  Load
+ * fails with PT_ERR_IO on a missing, foreign, truncated or corrupt file. */
+int pt_scene_save(const pt_scene* scene, const char* path);
+int pt_scene_load_cache(const char* path, pt_scene** out);
 /* Light lights(positions, normals, intensities, sizes) packing (Light.cpp:16-33) */
 int pt_pack_light(const float position[3], const float normal[3], const float intensity[3],
                   const float size[2], pt_area_light* out);

@@ -6,7 +6,7 @@
 //
 // What it restates (citations are path:line in the reference tree):
 //   * OBJ ingest with tinyobjloader v2.0.0's number parser and triangulation
-//     (external/tiny_obj_loader.h:897-1028, 1509-1612), tris and quads only;
+//     (external/tiny_obj_loader.h:897-1028, 1509-1612, ear clipping 1740-1955);
 //   * the median-split BVH builder (src/BoundingVolumeHierarchy.cpp:5-117),
 //     with glm's min/max/division semantics spelt out (glm is an un-vendored,
 //     unpinned submodule: external/glm is empty);
@@ -161,6 +161,72 @@ static bool obj_corner(const char** tok, int nv, int* vi) {
   return true;
 }
 
+// tinyobj built-in ear clipping, faces of 5+ corners
+// (external/tiny_obj_loader.h:1740-1955; pnpoly :1438-1450).  Restated loop
+// for loop: axis pair from the first non-degenerate corner, ears cut at the
+// guess vertex unless reflex (cross*area < 0) or containing another vertex.
+static int oracle_pnpoly3(const float* vx, const float* vy, float tx, float ty) {
+  int c = 0;
+  for (int i = 0, j = 2; i < 3; j = i++)
+    if (((vy[i] > ty) != (vy[j] > ty)) && (tx < (vx[j] - vx[i]) * (ty - vy[i]) / (vy[j] - vy[i]) + vx[i])) c = !c;
+  return c;
+}
+
+static void obj_earclip(const std::vector<int>& f, const std::vector<float>& v, std::vector<uint32_t>* idx,
+                        std::vector<uint32_t>* mat) {
+  size_t n = f.size();
+  size_t axes[2] = {1, 2};
+  for (size_t k = 0; k < n; ++k) {
+    size_t i0 = f[k % n], i1 = f[(k + 1) % n], i2 = f[(k + 2) % n];
+    float e0x = v[i1 * 3 + 0] - v[i0 * 3 + 0], e0y = v[i1 * 3 + 1] - v[i0 * 3 + 1], e0z = v[i1 * 3 + 2] - v[i0 * 3 + 2];
+    float e1x = v[i2 * 3 + 0] - v[i1 * 3 + 0], e1y = v[i2 * 3 + 1] - v[i1 * 3 + 1], e1z = v[i2 * 3 + 2] - v[i1 * 3 + 2];
+    float cx = fabsf(e0y * e1z - e0z * e1y), cy = fabsf(e0z * e1x - e0x * e1z), cz = fabsf(e0x * e1y - e0y * e1x);
+    const float eps = FLT_EPSILON;
+    if (cx > eps || cy > eps || cz > eps) {
+      if (cx > cy && cx > cz) {
+      } else {
+        axes[0] = 0;
+        if (cz > cx && cz > cy) axes[1] = 1;
+      }
+      break;
+    }
+  }
+  std::vector<int> rem(f);
+  size_t guess = 0, iters = n, prev_n = n;
+  int ind[3];
+  float vx[3], vy[3];
+  while (rem.size() > 3 && iters > 0) {
+    size_t np = rem.size();
+    if (guess >= np) guess -= np;
+    if (prev_n != np) { prev_n = np; iters = np; } else { iters--; }
+    for (int k = 0; k < 3; ++k) {
+      ind[k] = rem[(guess + k) % np];
+      vx[k] = v[(size_t)ind[k] * 3 + axes[0]];
+      vy[k] = v[(size_t)ind[k] * 3 + axes[1]];
+    }
+    float e0x = vx[1] - vx[0], e0y = vy[1] - vy[0], e1x = vx[2] - vx[1], e1y = vy[2] - vy[1];
+    float cross = e0x * e1y - e0y * e1x;
+    float area = (vx[0] * vy[1] - vy[0] * vx[1]) * 0.5f;
+    if (cross * area < 0.0f) { guess += 1; continue; }
+    bool overlap = false;
+    for (size_t ov = 3; ov < np; ++ov) {
+      size_t id = (guess + ov) % np;
+      size_t ovi = (size_t)rem[id];
+      if (oracle_pnpoly3(vx, vy, v[ovi * 3 + axes[0]], v[ovi * 3 + axes[1]])) { overlap = true; break; }
+    }
+    if (overlap) { guess += 1; continue; }
+    for (int k = 0; k < 3; ++k) idx->push_back((uint32_t)ind[k]);
+    mat->push_back(0);
+    size_t r = (guess + 1) % np;
+    while (r + 1 < np) { rem[r] = rem[r + 1]; r += 1; }
+    rem.pop_back();
+  }
+  if (rem.size() == 3) {
+    for (int k = 0; k < 3; ++k) idx->push_back((uint32_t)rem[k]);
+    mat->push_back(0);
+  }
+}
+
 static int obj_parse(const char* text, size_t len, ObjOut* out) {
   std::string buf(text, len);
   size_t pos = 0;
@@ -211,7 +277,7 @@ static int obj_parse(const char* text, size_t len, ObjOut* out) {
         for (int k = 0; k < 6; ++k) out->idx.push_back(a[k]);
         out->mat.push_back(0); out->mat.push_back(0);
       } else {
-        return -3;   // n-gon ear clipping (:1740+) not restated
+        obj_earclip(f, out->v, &out->idx, &out->mat);   // :1740-1955
       }
     }
   }

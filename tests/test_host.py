@@ -102,6 +102,14 @@ OBJ_CASES = {
                b"v 0.1 0.2 0.3\nf 1 2 3\nf 2 3 4\n",
     "shapes_and_comments": b"# c\no A\nv 0 0 0\nv 1 0 0\nv 0 1 0\ng B\nusemtl x\nv 0 0 1\n  f 1 2 3\nf 2 3 4\n",
     "crlf": b"v 0 0 0\r\nv 1 0 0\r\nv 0 1 0\r\nf 1 2 3\r\n",
+    # n-gons: tinyobj ear clipping (tiny_obj_loader.h:1740-1955)
+    "ngon_convex_xy": b"v 0 0 0\nv 2 0 0\nv 3 1 0\nv 1 3 0\nv -1 1 0\nf 1 2 3 4 5\n",
+    "ngon_concave_offset": b"v 1 1 0\nv 5 1 0\nv 5 5 0\nv 3 2 0\nv 1 5 0\nv 0.5 3 0\nf 1 2 3 4 5 6\nf 6 5 4 3 2 1\n",
+    "ngon_planes": b"v 0 0 0\nv 0 2 0\nv 0 3 1\nv 0 1 3\nv 0 -1 1\nv 1 0 0\nv 3 0 1\nv 2 0 3\nv 0.5 0 2\nv 0 0 1\n"
+                   b"f 1 2 3 4 5\nf 6 7 8 9 10 1\n",
+    "ngon_collinear_start": b"v 0 0 0\nv 1 0 0\nv 2 0 0\nv 2 2 1\nv 0 2 1\nv -1 1 0.5\nv -0.5 0.2 0.1\nf 1 2 3 4 5 6 7\n",
+    "ngon_star": b"v 0 3 0\nv 1 1 0\nv 3 1 0\nv 1.5 -0.5 0\nv 2 -3 0\nv 0 -1.5 0\nv -2 -3 0\nv -1.5 -0.5 0\n"
+                 b"v -3 1 0\nv -1 1 0\nf 1 2 3 4 5 6 7 8 9 10\n",
 }
 
 
@@ -122,9 +130,17 @@ def test_obj_box_and_errors():
     with pytest.raises(ptamd.PTError):
         ptamd.Scene.load_obj("/nonexistent.obj")
     with pytest.raises(ptamd.PTError):
-        ptamd.Scene.parse_obj(b"v 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nv 2 2 0\nf 1 2 3 4 5\n")   # n-gon
-    with pytest.raises(ptamd.PTError):
         ptamd.Scene.parse_obj(b"v 0 0 0\nf 1 2 3\n")   # index out of range
+
+
+def test_ngon_ear_clipping_known_answer():
+    # convex pentagon with corner 0 at the origin: every ear is accepted at
+    # guess 0, so tinyobj produces the fan (0,1,2) (0,2,3) (0,3,4)
+    v, i, _, _, m = ptamd.Scene.parse_obj(OBJ_CASES["ngon_convex_xy"]).arrays()
+    assert i.tolist() == [0, 1, 2, 0, 2, 3, 0, 3, 4] and m.size == 3
+    # a 10-corner star keeps every corner and yields n-2 triangles
+    v, i, _, _, m = ptamd.Scene.parse_obj(OBJ_CASES["ngon_star"]).arrays()
+    assert i.size == 3 * 8 and sorted(set(i.tolist())) == list(range(10))
 
 
 def test_light_and_camera_packing():
@@ -138,3 +154,32 @@ def test_partition_masks_tile_the_frame():
     for n in (1, 2, 3, 8):
         m = np.stack([ptamd.partition_owned(W, H, n, r) for r in range(n)])
         assert np.all(m.sum(0) == 1)
+
+
+def test_scene_cache_round_trip(tmp_path):
+    s = ptamd.Scene.load_obj(scenes.BOX_OBJ).build_bvh()
+    p = tmp_path / "box.ptscene"
+    s.save(p)
+    t = ptamd.Scene.load_cache(p)
+    for a, b in zip(s.arrays(), t.arrays()):
+        assert a.dtype == b.dtype and np.array_equal(a.view(np.uint32), b.view(np.uint32))
+    # int-encoded trees keep their flag; a bigger random mesh round-trips too
+    tv, ti = scenes.random_triangles(5000, seed=3)
+    s2 = ptamd.Scene.from_arrays(tv, ti).build_bvh(int_bits=True)
+    s2.save(tmp_path / "r.ptscene")
+    t2 = ptamd.Scene.load_cache(tmp_path / "r.ptscene")
+    assert all(np.array_equal(a.view(np.uint32), b.view(np.uint32)) for a, b in zip(s2.arrays(), t2.arrays()))
+    # corruption, truncation, foreign files and missing files are errors
+    raw = bytearray(p.read_bytes())
+    raw[100] ^= 1
+    (tmp_path / "bad.ptscene").write_bytes(bytes(raw))
+    (tmp_path / "short.ptscene").write_bytes(p.read_bytes()[:-9])
+    for bad in ("bad.ptscene", "short.ptscene"):
+        with pytest.raises(ptamd.PTError):
+            ptamd.Scene.load_cache(tmp_path / bad)
+    with pytest.raises(ptamd.PTError):
+        ptamd.Scene.load_cache(scenes.BOX_OBJ)
+    with pytest.raises(ptamd.PTError):
+        ptamd.Scene.load_cache(tmp_path / "missing.ptscene")
+    with pytest.raises(ptamd.PTError):
+        ptamd.Scene.load_obj(scenes.BOX_OBJ).save(tmp_path / "nobvh.ptscene")   # BVH not built
