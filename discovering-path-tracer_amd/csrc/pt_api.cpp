@@ -308,6 +308,21 @@ struct pt_context {
   float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};   // root AABB of the uploaded tree
   std::vector<pt_area_light> lights_host;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // progressive loop (VulkanRayTracer::mainLoop, :717-865)
+  float prog_cam[16] = {0};
+  bool prog_has_cam = false;
+  uint32_t prog_batch = 0;
+  // double-buffered asynchronous readback: device snapshot -> pinned host
+  struct Readback {
+    float4* dev = nullptr;
+    void* host = nullptr;
+    size_t bytes = 0;
+    hipEvent_t snap = nullptr, done = nullptr;
+    int ticket = 0;        // 0 = free
+    int w = 0, h = 0;
+  } rb[2];
+  hipStream_t copy_stream = nullptr;
+  int rb_next_ticket = 1;
   bool timed = false;
   // ring of event pairs, one per render launch since pt_reset_launch_times
   static constexpr int kRing = 512;
@@ -371,6 +386,13 @@ int pt_destroy(pt_context* c) {
   dev_free(c->d_lights_dev);
   if (c->own_accum) dev_free(c->d_accum);
   dev_free(c->d_stats);
+  for (auto& r : c->rb) {
+    dev_free(r.dev);
+    if (r.host) (void)hipHostFree(r.host);
+    if (r.snap) (void)hipEventDestroy(r.snap);
+    if (r.done) (void)hipEventDestroy(r.done);
+  }
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   for (int i = 0; i < pt_context::kRing; ++i)
@@ -629,6 +651,91 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
 }
 
 int pt_dispatch(pt_context* c, uint32_t sample_batch) { return pt_render(c, sample_batch, 1); }
+
+// ---- progressive loop + asynchronous readback -----------
+// The reference's mainLoop (VulkanRayTracer.cpp:717-865) resets sampleBatch to
+// 0 whenever any camera field changes (:739-754; batch 0 weights the old image
+// by 0), dispatches one 1-spp batch, waits on two fences and copies the image
+// out, up to 1024 batches (:719, :857).  Here a camera change resets the
+// counter the same way, pending batches go out as one fused launch, and a
+// readback snapshots the image on the render stream (device-to-device) and
+// copies it to pinned host memory on a second stream, so rendering goes on
+// while the previous frame travels over PCIe.
+int pt_progressive_camera(pt_context* c, const float ubo[16], int* reset) {
+  if (!c || !ubo) return fail(PT_ERR_INVALID, "null argument");
+  const bool changed = !c->prog_has_cam || memcmp(ubo, c->prog_cam, sizeof c->prog_cam) != 0;
+  if (changed) {
+    memcpy(c->prog_cam, ubo, sizeof c->prog_cam);
+    c->prog_has_cam = true;
+    c->prog_batch = 0;
+    const int rc = pt_set_camera(c, ubo);
+    if (rc) return rc;
+  }
+  if (reset) *reset = changed ? 1 : 0;
+  return PT_OK;
+}
+
+int pt_progressive_advance(pt_context* c, uint32_t max_new, uint32_t limit, uint32_t* first, uint32_t* count) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  if (!c->prog_has_cam) return fail(PT_ERR_INVALID, "no camera (pt_progressive_camera)");
+  const uint32_t room = limit > c->prog_batch ? limit - c->prog_batch : 0u;
+  const uint32_t n = max_new < room ? max_new : room;
+  if (first) *first = c->prog_batch;
+  if (count) *count = n;
+  if (n == 0) return PT_OK;
+  const int rc = pt_render(c, c->prog_batch, n);
+  if (rc) return rc;
+  c->prog_batch += n;
+  return PT_OK;
+}
+
+int pt_readback_begin(pt_context* c, int* ticket) {
+  if (!c || !ticket) return fail(PT_ERR_INVALID, "null argument");
+  if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
+  PT_HIP(hipSetDevice(c->device));
+  if (!c->copy_stream) PT_HIP(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  // the free slot, else the older one (its unread result is dropped)
+  int slot = c->rb[0].ticket == 0 ? 0 : c->rb[1].ticket == 0 ? 1 : (c->rb[0].ticket < c->rb[1].ticket ? 0 : 1);
+  pt_context::Readback& r = c->rb[slot];
+  if (r.ticket) PT_HIP(hipEventSynchronize(r.done));
+  const size_t bytes = (size_t)c->width * c->height * sizeof(float4);
+  if (r.bytes != bytes) {
+    dev_free(r.dev);
+    if (r.host) (void)hipHostFree(r.host);
+    r.host = nullptr;
+    r.bytes = 0;
+    PT_HIP(hipMalloc((void**)&r.dev, bytes));
+    PT_HIP(hipHostMalloc(&r.host, bytes, hipHostMallocDefault));
+    r.bytes = bytes;
+  }
+  if (!r.snap) PT_HIP(hipEventCreateWithFlags(&r.snap, hipEventDisableTiming));
+  if (!r.done) PT_HIP(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
+  PT_HIP(hipMemcpyAsync(r.dev, c->d_accum, bytes, hipMemcpyDeviceToDevice, c->stream));
+  PT_HIP(hipEventRecord(r.snap, c->stream));
+  PT_HIP(hipStreamWaitEvent(c->copy_stream, r.snap, 0));
+  PT_HIP(hipMemcpyAsync(r.host, r.dev, bytes, hipMemcpyDeviceToHost, c->copy_stream));
+  PT_HIP(hipEventRecord(r.done, c->copy_stream));
+  r.w = c->width;
+  r.h = c->height;
+  r.ticket = c->rb_next_ticket++;
+  *ticket = r.ticket;
+  return PT_OK;
+}
+
+int pt_readback_end(pt_context* c, int ticket, float* rgba, size_t n) {
+  if (!c || !rgba) return fail(PT_ERR_INVALID, "null argument");
+  for (auto& r : c->rb) {
+    if (r.ticket != ticket || ticket == 0) continue;
+    const size_t need = (size_t)r.w * r.h * 4;
+    if (n < need) return fail(PT_ERR_INVALID, "output buffer too small: need " + std::to_string(need) + " floats");
+    PT_HIP(hipSetDevice(c->device));
+    PT_HIP(hipEventSynchronize(r.done));
+    memcpy(rgba, r.host, need * sizeof(float));
+    r.ticket = 0;
+    return PT_OK;
+  }
+  return fail(PT_ERR_INVALID, "unknown or already collected readback ticket " + std::to_string(ticket));
+}
 
 int pt_set_option(pt_context* c, int key, int value) {
   if (!c) return fail(PT_ERR_INVALID, "null context");

@@ -34,6 +34,7 @@ EXPORTS = [
     "pt_scene_load_obj", "pt_scene_parse_obj", "pt_scene_from_arrays", "pt_scene_build_bvh",
     "pt_scene_counts", "pt_scene_copy", "pt_scene_upload", "pt_scene_free", "pt_pack_light",
     "pt_default_camera", "pt_primary_cull_rects", "pt_scene_save", "pt_scene_load_cache",
+    "pt_progressive_camera", "pt_progressive_advance", "pt_readback_begin", "pt_readback_end",
 ]
 
 
@@ -90,6 +91,10 @@ def lib():
             "pt_default_camera": ([vp], i32),
             "pt_primary_cull_rects": ([vp, i32, i32, vp, vp, vp, i32, vp, i32, ctypes.POINTER(i32)], i32),
             "pt_scene_save": ([vp, ctypes.c_char_p], i32),
+            "pt_progressive_camera": ([vp, vp, ctypes.POINTER(i32)], i32),
+            "pt_progressive_advance": ([vp, u32, u32, ctypes.POINTER(u32), ctypes.POINTER(u32)], i32),
+            "pt_readback_begin": ([vp, ctypes.POINTER(i32)], i32),
+            "pt_readback_end": ([vp, i32, vp, sz], i32),
             "pt_scene_load_cache": ([ctypes.c_char_p, ctypes.POINTER(vp)], i32),
         }
         for name, (args, res) in sig.items():
@@ -288,6 +293,29 @@ class Renderer:
 
     def tiles_unpack(self, src_device_ptr, src_rank, frame_device_ptr):
         _check(lib().pt_tiles_unpack(self._c, src_device_ptr, src_rank, frame_device_ptr), "pt_tiles_unpack")
+
+    def progressive_camera(self, ubo16):
+        """Camera for the progressive loop; True if it reset the sample counter."""
+        u = np.ascontiguousarray(ubo16, np.float32).reshape(16)
+        reset = ctypes.c_int(0)
+        _check(lib().pt_progressive_camera(self._c, u.ctypes.data, ctypes.byref(reset)), "pt_progressive_camera")
+        return bool(reset.value)
+
+    def progressive_advance(self, max_new, limit=1024):
+        first, count = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        _check(lib().pt_progressive_advance(self._c, max_new, limit, ctypes.byref(first), ctypes.byref(count)),
+               "pt_progressive_advance")
+        return first.value, count.value
+
+    def readback_begin(self):
+        t = ctypes.c_int(0)
+        _check(lib().pt_readback_begin(self._c, ctypes.byref(t)), "pt_readback_begin")
+        return t.value
+
+    def readback_end(self, ticket):
+        out = np.empty(self.width * self.height * 4, np.float32)
+        _check(lib().pt_readback_end(self._c, ticket, out.ctypes.data, out.size), "pt_readback_end")
+        return out
 
     def set_option(self, key, value):
         _check(lib().pt_set_option(self._c, key, value), "pt_set_option")

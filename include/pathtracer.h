@@ -129,6 +129,24 @@ int pt_dispatch(pt_context* ctx, uint32_t sample_batch);
  * launch; bit-identical to that many pt_dispatch calls. */
 int pt_render(pt_context* ctx, uint32_t first_batch, uint32_t n_batches);
 
+/* ---- progressive loop (VulkanRayTracer::mainLoop, :717-865) ------------ */
+/* Sets the camera; if any of its 16 floats differs from the last one given
+ * here, the sample counter restarts at 0 (:739-754 — batch 0 weights the old
+ * image by 0, so no clear is needed).  *reset (optional) reports it. */
+int pt_progressive_camera(pt_context* ctx, const float camera_ubo[16], int* reset);
+/* Enqueues min(max_new, limit - counter) further batches as one fused launch
+ * (the reference renders up to limit = 1024, :719) and advances the counter;
+ * *first and *count (optional) report what was enqueued.  Bit-identical to
+ * that many pt_dispatch calls. */
+int pt_progressive_advance(pt_context* ctx, uint32_t max_new, uint32_t limit, uint32_t* first, uint32_t* count);
+/* Asynchronous double-buffered readback (replaces the per-batch fence waits
+ * and copyStorageImage, :826-846): begin snapshots the image as of the work
+ * enqueued so far and copies it to pinned host memory on a second stream;
+ * end waits for that copy and writes W*H*4 floats.  Two readbacks may be in
+ * flight; a third begin recycles the oldest unclaimed one. */
+int pt_readback_begin(pt_context* ctx, int* ticket);
+int pt_readback_end(pt_context* ctx, int ticket, float* rgba, size_t n_floats);
+
 /* ---- multi-GPU screen-space partition ------------------ */
 /* Pixels are grouped into 16x16 blocks, numbered row-major; this context
  * renders block b iff b % nranks == rank.  pt_clear_accum then writes +0 to

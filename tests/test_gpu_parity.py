@@ -348,3 +348,34 @@ def test_primary_culling_with_stale_accumulator():
         r.set_camera(camC)
         r.render(0, 2)
         _assert_same(r.read_accum(), ref2, f"spl {spl} first=0 over stale")
+
+
+def test_progressive_loop_camera_reset_and_async_readback():
+    """mainLoop semantics (VulkanRayTracer.cpp:717-865): a camera change
+    restarts at batch 0 over the old image (prev*0), batches are capped, and
+    readbacks return the image as of their begin while rendering goes on."""
+    v, i, n = _box()
+    W, H = 64, 48
+    camA, camB = scenes.camera((3.0, 2.0, 4.0)), scenes.DEFAULT_CAMERA
+    r = _setup(v, i, n, cam=camA)
+    r.resize_and_clear(W, H)
+    assert r.progressive_camera(camA) is True
+    assert r.progressive_advance(2) == (0, 2)
+    t1 = r.readback_begin()                       # image after camA batches 0-1
+    assert r.progressive_advance(1) == (2, 1)
+    assert r.progressive_camera(camA) is False    # unchanged camera: no reset
+    assert r.progressive_camera(camB) is True     # reset to batch 0 over the camA image
+    assert r.progressive_advance(5, limit=4) == (0, 4)   # capped
+    assert r.progressive_advance(5, limit=4) == (4, 0)
+    t2 = r.readback_begin()
+    img2 = r.readback_end(t2)
+    img1 = r.readback_end(t1)
+    refA, _ = _oracle(v, i, n, W, H, first=0, nb=2, cam=camA)
+    _assert_same(img1, refA, "readback after camA 0-1")
+    acc = refA.copy()
+    acc, _ = _oracle(v, i, n, W, H, first=2, nb=1, cam=camA, accum=acc)
+    acc, _ = _oracle(v, i, n, W, H, first=0, nb=4, cam=camB, accum=acc)
+    _assert_same(img2, acc, "camB 0-3 over camA image")
+    _assert_same(r.read_accum(), acc, "accumulator")
+    with pytest.raises(ptamd.PTError):
+        r.readback_end(t2)                        # already collected

@@ -1,6 +1,6 @@
 set -e
-run() { tag=$1; shift; timeout -k 10 600 python3 bench.py "$@" --no-cpu-baseline > gpurun_out/bench_$tag.log 2>&1 || { echo "$tag rc=$?"; tail -20 gpurun_out/bench_$tag.log; exit 1; }; echo "$tag $(grep '^{' gpurun_out/bench_$tag.log | tail -1)"; }
-run sphere --scene sphere --steps 3 --warmup 1
-run sphere4k --scene sphere --width 3840 --height 2160 --spp 16 --depth 8 --steps 1 --warmup 1
-run syn1m --scene synthetic:1000000 --steps 2 --warmup 1
-run syn10m --scene synthetic:10000000 --spp 1 --steps 1 --warmup 1
+timeout -k 10 600 python3 -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+cd discovering-path-tracer_amd
+timeout -k 10 120 ./pt_render ../tests/golden/box.obj -w 1920 -h 1080 -progressive 64 -chunk 8 -orbit-at 24 -cache /tmp/box.ptscene -o /tmp/p.pfm
+timeout -k 10 120 ./pt_render ../tests/golden/box.obj -w 1920 -h 1080 -progressive 64 -chunk 1 -cache /tmp/box.ptscene
