@@ -11,6 +11,7 @@
 #include <math.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -1079,6 +1080,106 @@ int pt_scene_load_cache(const char* path, pt_scene** out) {
     return fail(PT_ERR_IO, std::string("scene cache truncated or corrupt: ") + path);
   }
   *out = s;
+  return PT_OK;
+}
+
+// ---- image output ----------------------------------------
+namespace {
+uint32_t crc32_update(uint32_t crc, const unsigned char* p, size_t n) {
+  static uint32_t table[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320u ^ (c >> 1) : c >> 1;
+      table[i] = c;
+    }
+    init = true;
+  }
+  for (size_t i = 0; i < n; ++i) crc = table[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
+  return crc;
+}
+
+void put_be32(std::vector<unsigned char>* o, uint32_t v) {
+  for (int s = 24; s >= 0; s -= 8) o->push_back((unsigned char)(v >> s));
+}
+
+void png_chunk(FILE* f, const char* type, const std::vector<unsigned char>& data, bool* ok) {
+  std::vector<unsigned char> buf;
+  put_be32(&buf, (uint32_t)data.size());
+  buf.insert(buf.end(), type, type + 4);
+  buf.insert(buf.end(), data.begin(), data.end());
+  const uint32_t crc = crc32_update(0xffffffffu, buf.data() + 4, buf.size() - 4) ^ 0xffffffffu;
+  put_be32(&buf, crc);
+  if (*ok) *ok = fwrite(buf.data(), 1, buf.size(), f) == buf.size();
+}
+
+// linear -> 8-bit sRGB after clamping to [0,1]: what an sRGB swapchain shows
+// for the reference's RGBA32F image (VulkanRenderer copies it to a texture
+// that color_frag.frag outputs unchanged)
+unsigned char srgb8(float x) {
+  if (!(x > 0.0f)) return 0;
+  if (x >= 1.0f) return 255;
+  const double e = x <= 0.0031308f ? 12.92 * x : 1.055 * pow((double)x, 1.0 / 2.4) - 0.055;
+  return (unsigned char)(e * 255.0 + 0.5);
+}
+}  // namespace
+
+int pt_write_image(const char* path, const float* rgba, int w, int h, int format) {
+  if (!path || !rgba) return fail(PT_ERR_INVALID, "null argument");
+  if (w <= 0 || h <= 0) return fail(PT_ERR_INVALID, "bad resolution");
+  if (format != PT_IMAGE_PFM && format != PT_IMAGE_PNG) return fail(PT_ERR_INVALID, "unknown image format");
+  FILE* f = fopen(path, "wb");
+  if (!f) return fail(PT_ERR_IO, std::string("cannot create ") + path);
+  bool ok = true;
+  if (format == PT_IMAGE_PFM) {
+    // rows bottom-to-top: row y = 0 of the accumulation buffer is written first
+    ok = fprintf(f, "PF\n%d %d\n-1.0\n", w, h) > 0;
+    std::vector<float> rgb((size_t)w * 3);
+    for (int y = 0; y < h && ok; ++y) {
+      for (int x = 0; x < w; ++x)
+        for (int c = 0; c < 3; ++c) rgb[(size_t)x * 3 + c] = rgba[((size_t)y * w + x) * 4 + c];
+      ok = fwrite(rgb.data(), 4, rgb.size(), f) == rgb.size();
+    }
+  } else {
+    // 8-bit RGB PNG, zlib stream of stored (uncompressed) deflate blocks;
+    // rows top-to-bottom, so the accumulation buffer's last row comes first
+    static const unsigned char sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    ok = fwrite(sig, 1, 8, f) == 8;
+    std::vector<unsigned char> ihdr;
+    put_be32(&ihdr, (uint32_t)w);
+    put_be32(&ihdr, (uint32_t)h);
+    ihdr.insert(ihdr.end(), {8, 2, 0, 0, 0});   // 8-bit, truecolour, deflate, filter 0, no interlace
+    png_chunk(f, "IHDR", ihdr, &ok);
+    std::vector<unsigned char> raw;
+    raw.reserve((size_t)h * (1 + 3 * (size_t)w));
+    for (int y = h - 1; y >= 0; --y) {
+      raw.push_back(0);   // filter: none
+      for (int x = 0; x < w; ++x)
+        for (int c = 0; c < 3; ++c) raw.push_back(srgb8(rgba[((size_t)y * w + x) * 4 + c]));
+    }
+    std::vector<unsigned char> z = {0x78, 0x01};
+    uint32_t a = 1, b = 0;   // Adler-32
+    for (size_t i = 0; i < raw.size(); ++i) {
+      a = (a + raw[i]) % 65521u;
+      b = (b + a) % 65521u;
+    }
+    for (size_t off = 0; off < raw.size() || off == 0; off += 65535) {
+      const size_t n = std::min<size_t>(65535, raw.size() - off);
+      z.push_back(off + n >= raw.size() ? 1 : 0);
+      z.push_back((unsigned char)(n & 0xff));
+      z.push_back((unsigned char)(n >> 8));
+      z.push_back((unsigned char)(~n & 0xff));
+      z.push_back((unsigned char)((~n >> 8) & 0xff));
+      z.insert(z.end(), raw.begin() + (long)off, raw.begin() + (long)(off + n));
+      if (raw.empty()) break;
+    }
+    put_be32(&z, (b << 16) | a);
+    png_chunk(f, "IDAT", z, &ok);
+    png_chunk(f, "IEND", {}, &ok);
+  }
+  if (fclose(f) != 0) ok = false;
+  if (!ok) return fail(PT_ERR_IO, std::string("write failed: ") + path);
   return PT_OK;
 }
 

@@ -4,7 +4,7 @@
 // `spp` progressive 1-spp batches (or one fused launch) and writes a PFM.
 //
 //   pt_render scene.obj [-w 1920] [-h 1080] [-spp 8] [-depth 4] [-sss 3]
-//             [-fused] [-o out.pfm] [-device 0] [-cache scene.ptscene]
+//             [-fused] [-o out.pfm] [-png out.png] [-device 0] [-cache scene.ptscene]
 //             [-progressive N [-chunk K] [-orbit-at B]]
 //
 // -progressive runs the reference's interactive loop (mainLoop, :717-865)
@@ -41,7 +41,7 @@ int main(int argc, char** argv) {
   pt_params params{4, 3};
   bool fused = false;
   int progressive = 0, chunk = 8, orbit_at = -1;
-  std::string cache_path;
+  std::string cache_path, png_path;
   for (int i = 2; i < argc; ++i) {
     auto next = [&](void) { return (i + 1 < argc) ? argv[++i] : (char*)"0"; };
     if (!strcmp(argv[i], "-w")) W = atoi(next());
@@ -53,6 +53,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "-fused")) fused = true;
     else if (!strcmp(argv[i], "-o")) out_path = next();
     else if (!strcmp(argv[i], "-cache")) cache_path = next();
+    else if (!strcmp(argv[i], "-png")) png_path = next();
     else if (!strcmp(argv[i], "-progressive")) progressive = atoi(next());
     else if (!strcmp(argv[i], "-chunk")) chunk = atoi(next());
     else if (!strcmp(argv[i], "-orbit-at")) orbit_at = atoi(next());
@@ -137,19 +138,11 @@ int main(int argc, char** argv) {
   auto r1 = std::chrono::steady_clock::now();
   if (progressive == 0)
     printf("rendered %dx%d x %d spp in %.3f ms\n", W, H, spp, std::chrono::duration<double, std::milli>(r1 - r0).count());
-  if (!out_path.empty()) {
+  if (!out_path.empty() || !png_path.empty()) {
     std::vector<float> rgba((size_t)W * H * 4);
     check(pt_read_accum(ctx, rgba.data(), rgba.size()), "read");
-    FILE* f = fopen(out_path.c_str(), "wb");
-    if (!f) { perror("fopen"); return 1; }
-    fprintf(f, "PF\n%d %d\n-1.0\n", W, H);   // rows bottom-to-top = row 0 first
-    std::vector<float> rgb((size_t)W * 3);
-    for (int y = 0; y < H; ++y) {
-      for (int x = 0; x < W; ++x)
-        for (int c = 0; c < 3; ++c) rgb[(size_t)x * 3 + c] = rgba[((size_t)y * W + x) * 4 + c];
-      fwrite(rgb.data(), 4, rgb.size(), f);
-    }
-    fclose(f);
+    if (!out_path.empty()) check(pt_write_image(out_path.c_str(), rgba.data(), W, H, PT_IMAGE_PFM), "write pfm");
+    if (!png_path.empty()) check(pt_write_image(png_path.c_str(), rgba.data(), W, H, PT_IMAGE_PNG), "write png");
   }
   pt_destroy(ctx);
   pt_scene_free(scene);

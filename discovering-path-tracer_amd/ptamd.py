@@ -34,7 +34,7 @@ EXPORTS = [
     "pt_scene_load_obj", "pt_scene_parse_obj", "pt_scene_from_arrays", "pt_scene_build_bvh",
     "pt_scene_counts", "pt_scene_copy", "pt_scene_upload", "pt_scene_free", "pt_pack_light",
     "pt_default_camera", "pt_primary_cull_rects", "pt_scene_save", "pt_scene_load_cache",
-    "pt_progressive_camera", "pt_progressive_advance", "pt_readback_begin", "pt_readback_end",
+    "pt_progressive_camera", "pt_progressive_advance", "pt_readback_begin", "pt_readback_end", "pt_write_image",
 ]
 
 
@@ -95,6 +95,7 @@ def lib():
             "pt_progressive_advance": ([vp, u32, u32, ctypes.POINTER(u32), ctypes.POINTER(u32)], i32),
             "pt_readback_begin": ([vp, ctypes.POINTER(i32)], i32),
             "pt_readback_end": ([vp, i32, vp, sz], i32),
+            "pt_write_image": ([ctypes.c_char_p, vp, i32, i32, i32], i32),
             "pt_scene_load_cache": ([ctypes.c_char_p, ctypes.POINTER(vp)], i32),
         }
         for name, (args, res) in sig.items():
@@ -239,6 +240,15 @@ def primary_cull_rects(camera_ubo, width, height, root_min, root_max, lights16, 
                                        l.ctypes.data if l.size else None, l.size // 16, out.ctypes.data,
                                        max_rects, ctypes.byref(n)), "pt_primary_cull_rects")
     return None if n.value < 0 else out[:n.value].copy()
+
+
+def write_image(path, rgba, width, height, fmt="png"):
+    """pt_write_image: PFM (float) or 8-bit sRGB PNG of an accumulation image."""
+    a = np.ascontiguousarray(rgba, np.float32).reshape(-1)
+    if a.size != width * height * 4:
+        raise PTError("rgba must hold width*height*4 floats")
+    _check(lib().pt_write_image(str(path).encode(), a.ctypes.data, width, height, 1 if fmt == "png" else 0),
+           "pt_write_image")
 
 
 def default_camera():

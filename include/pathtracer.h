@@ -252,6 +252,13 @@ int pt_scene_load_cache(const char* path, pt_scene** out);
 /* Light lights(positions, normals, intensities, sizes) packing (Light.cpp:16-33) */
 int pt_pack_light(const float position[3], const float normal[3], const float intensity[3],
                   const float size[2], pt_area_light* out);
+/* Writes a W x H RGBA32F accumulation image (row y = 0 first in memory) for
+ * inspection: PT_IMAGE_PFM = float RGB PFM (rows
+ * bottom-to-top, i.e. row 0 first); PT_IMAGE_PNG = 8-bit sRGB PNG of the
+ * colours clamped to [0,1], top row = last buffer row. */
+#define PT_IMAGE_PFM 0
+#define PT_IMAGE_PNG 1
+int pt_write_image(const char* path, const float* rgba, int width, int height, int format);
 /* Camera getters for the reference's default orbit camera, as the UBO
  * (Camera.cpp:4-10, 84-106): pos (0,0,5) dir (0,0,-1) up (0,1,0) fov 60. */
 int pt_default_camera(float camera_ubo[16]);

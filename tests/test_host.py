@@ -183,3 +183,39 @@ def test_scene_cache_round_trip(tmp_path):
         ptamd.Scene.load_cache(tmp_path / "missing.ptscene")
     with pytest.raises(ptamd.PTError):
         ptamd.Scene.load_obj(scenes.BOX_OBJ).save(tmp_path / "nobvh.ptscene")   # BVH not built
+
+
+def test_write_image_png_and_pfm(tmp_path):
+    import struct
+    import zlib
+    W, H = 70, 9
+    rgba = np.zeros((H, W, 4), np.float32)
+    rgba[..., 0] = np.linspace(-0.5, 1.5, W)[None, :]
+    rgba[..., 1] = np.linspace(0, 1, H)[:, None]
+    rgba[..., 2] = 0.0031308
+    ptamd.write_image(tmp_path / "a.png", rgba, W, H, "png")
+    data = (tmp_path / "a.png").read_bytes()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, chunks = 8, {}
+    while pos < len(data):
+        n, = struct.unpack(">I", data[pos:pos + 4])
+        typ, body = data[pos + 4:pos + 8], data[pos + 8:pos + 8 + n]
+        crc, = struct.unpack(">I", data[pos + 8 + n:pos + 12 + n])
+        assert crc == zlib.crc32(typ + body)
+        chunks[typ] = body
+        pos += 12 + n
+    assert struct.unpack(">IIBBBBB", chunks[b"IHDR"]) == (W, H, 8, 2, 0, 0, 0)
+    raw = np.frombuffer(zlib.decompress(chunks[b"IDAT"]), np.uint8).reshape(H, 1 + 3 * W)
+    assert np.all(raw[:, 0] == 0)
+    img = raw[:, 1:].reshape(H, W, 3)[::-1]          # top row = last buffer row
+    lin = np.clip(rgba[..., :3].astype(np.float64), 0, 1)
+    srgb = np.where(lin <= 0.0031308, 12.92 * lin, 1.055 * lin ** (1 / 2.4) - 0.055)
+    assert np.max(np.abs(img.astype(int) - np.floor(srgb * 255 + 0.5).astype(int))) <= 1
+    ptamd.write_image(tmp_path / "a.pfm", rgba, W, H, "pfm")
+    pfm = (tmp_path / "a.pfm").read_bytes()
+    head = f"PF\n{W} {H}\n-1.0\n".encode()
+    assert pfm.startswith(head)
+    body = np.frombuffer(pfm[len(head):], np.float32).reshape(H, W, 3)
+    assert np.array_equal(body, rgba[..., :3])
+    with pytest.raises(ptamd.PTError):
+        ptamd.write_image(tmp_path / "no_such_dir" / "x.png", rgba, W, H)
