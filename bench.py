@@ -159,7 +159,12 @@ def main():
     r.set_camera(cam)
     r.set_params(DEPTH, SSS)
     r.set_partition(world, rank)
-    r.set_stream(torch.cuda.current_stream(dev).cuda_stream)   # order with torch's collectives
+    # One explicit stream for the renderer and every torch op/collective: the
+    # legacy default stream has handle 0, which pt_set_stream reads as "the
+    # context's own stream", so it cannot be shared by handle.
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    r.set_stream(stream.cuda_stream)   # order with torch's collectives
     r.resize_and_clear(W, H)
 
     # Stats pass (untimed): the reference's exact traversal counts for one frame.
@@ -294,7 +299,9 @@ def main():
         got = (out if args.collective == "gather" else frame).cpu().numpy().reshape(-1)
         verified = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
         if not verified:
-            raise SystemExit("bench --verify: assembled frame differs from the single-GPU frame")
+            bad = np.flatnonzero(got.view(np.uint32) != want.view(np.uint32))
+            raise SystemExit(f"bench --verify: assembled frame differs from the single-GPU frame in {bad.size} "
+                             f"floats; first at pixel {bad[0] // 4} ch {bad[0] % 4}: {got[bad[0]]} vs {want[bad[0]]}")
 
     if rank == 0:
         ms_per_step = dt / args.steps * 1e3

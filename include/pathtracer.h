@@ -86,8 +86,9 @@ const char* pt_last_error(void);
  * and VulkanRayTracer::initComputePipeline's pipeline creation (:624-672). */
 int pt_create(int device_ordinal, pt_context** out);
 int pt_destroy(pt_context* ctx);
-/* Launch on a caller-owned hipStream_t (e.g. torch's current stream); NULL
- * returns to the context's own stream. */
+/* Launch on a caller-owned hipStream_t (e.g. a torch.cuda.Stream's handle);
+ * NULL returns to the context's own stream — so the legacy default stream
+ * (handle 0) cannot be selected: share a created stream instead. */
 int pt_set_stream(pt_context* ctx, void* hip_stream);
 int pt_synchronize(pt_context* ctx);
 
