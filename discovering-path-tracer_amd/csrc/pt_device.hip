@@ -116,7 +116,7 @@ __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* can
     if (STATS) c.nodes++;
     const int raw = __float_as_int(a.w);
     // bit 31: bounds identical to the parent's, which this ray hit -> hit
-    const bool h = raw < 0 ? true : slab(o, inv, a, b);
+    const bool h = (raw < 0) | slab(o, inv, a, b);   // branch-free: one LDS round trip per node
     const int tri = __float_as_int(b.w);
     if (h && tri >= 0) {
       if (STATS) c.leaves++;
@@ -165,7 +165,7 @@ __device__ bool occluded(const RenderParams& P, v3 o, v3 d, float limit, Ctr& c)
     if (STATS) c.nodes++;
     const int raw = __float_as_int(a.w);
     // bit 31: bounds identical to the parent's, which this ray hit -> hit
-    const bool h = raw < 0 ? true : slab(o, inv, a, b);
+    const bool h = (raw < 0) | slab(o, inv, a, b);   // branch-free: one LDS round trip per node
     const int tri = __float_as_int(b.w);
     if (h && tri >= 0) {
       if (STATS) c.leaves++;
