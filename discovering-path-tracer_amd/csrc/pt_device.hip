@@ -118,13 +118,14 @@ __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* can
     // bit 31: bounds identical to the parent's, which this ray hit -> hit
     const bool h = (raw < 0) | slab(o, inv, a, b);   // branch-free: one LDS round trip per node
     const int tri = __float_as_int(b.w);
-    if (h && tri >= 0) {
-      if (STATS) c.leaves++;
-      cand[nc * 64] = tri;
-      if (++nc == kCand) {
-        test_candidates(P, o, d, cand, nc, &best, &bt);
-        nc = 0;
-      }
+    // slot nc is free: write it unconditionally, keep it only for a hit leaf
+    cand[nc * 64] = tri;
+    const bool leaf_hit = h && tri >= 0;
+    if (STATS) c.leaves += leaf_hit ? 1u : 0u;
+    nc += leaf_hit ? 1 : 0;
+    if (nc == kCand) {
+      test_candidates(P, o, d, cand, nc, &best, &bt);
+      nc = 0;
     }
     const int next = (h && tri < 0) ? k + 1 : (raw & 0x7fffffff);
     if (PF && next == k + 1) {

@@ -13,7 +13,8 @@
 // GLSL built-ins have implementation-defined precision, so the reference
 // leaves sin/cos/acos/log/exp/tan unspecified.  We pin them to the classic
 // fdlibm-style float kernels (range reduction + minimax polynomial / rational
-// approximation, ≈1 ulp on the domains the shader uses) — the oracle's
+// approximation, ≈1 ulp on the domains the shader uses; polynomials as
+// explicit fma Horner chains) — the oracle's
 // oracle/glsl_math.h states the same algorithms and tests/test_math.py
 // checks the two agree bitwise and stay within a few ulp of libm.
 #pragma once
@@ -36,6 +37,8 @@ PT_FN float fmax_(float a, float b) { return __builtin_fmaxf(a, b); }
 PT_FN float fabs_(float a) { return __builtin_fabsf(a); }
 PT_FN float sqrt_(float a) { return __builtin_sqrtf(a); }
 PT_FN float floor_(float a) { return __builtin_floorf(a); }
+// explicit fused multiply-add (one rounding; -ffp-contract=off never forms it)
+PT_FN float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 
 // ------------------------------------------------- fast exact quotients ----
 // Device code may evaluate a quotient through the hardware reciprocal
@@ -108,11 +111,11 @@ PT_FN float log_impl(float x) {
   const float dk = (float)k;
   const float z = s * s;
   const float w = z * z;
-  const float t1 = w * (0x1.99999ap-2f + w * (0x1.c71c52p-3f + w * 0x1.39a09ep-3f));
-  const float t2 = z * (0x1.555556p-1f + w * (0x1.24924ap-2f + w * (0x1.74664ap-3f + w * 0x1.2f112ep-3f)));
+  const float t1 = w * fma_(w, fma_(w, 0x1.39a09ep-3f, 0x1.c71c52p-3f), 0x1.99999ap-2f);
+  const float t2 = z * fma_(w, fma_(w, fma_(w, 0x1.2f112ep-3f, 0x1.74664ap-3f), 0x1.24924ap-2f), 0x1.555556p-1f);
   const float R = t2 + t1;
   const float hfsq = 0.5f * f * f;
-  return dk * 0x1.62e3p-1f - ((hfsq - (s * (hfsq + R) + dk * 0x1.2fefa2p-17f)) - f);
+  return fma_(dk, 0x1.62e3p-1f, -((hfsq - fma_(s, hfsq + R, dk * 0x1.2fefa2p-17f)) - f));
 }
 PT_FN float log_(float x) { return log_impl<PT_FAST_DEV>(x); }
 
@@ -126,11 +129,12 @@ PT_FN float exp_impl(float x) {
   if (x < -103.972084045410156f) return 0.0f;
   const float kf = floor_(x * 0x1.715476p+0f + 0.5f);
   const int k = (int)kf;
-  const float hi = x - kf * 0x1.62e4p-1f;
+  const float hi = fma_(-kf, 0x1.62e4p-1f, x);
   const float lo = kf * 0x1.7f7d1cp-20f;
   const float r = hi - lo;
   const float t = r * r;
-  const float c = r - t * (0x1.555556p-3f + t * (-0x1.6c16c2p-9f + t * (0x1.1566aap-14f + t * (-0x1.bbd41cp-20f + t * 0x1.637698p-25f))));
+  const float c = fma_(-t, fma_(t, fma_(t, fma_(t, fma_(t, 0x1.637698p-25f, -0x1.bbd41cp-20f), 0x1.1566aap-14f),
+                                      -0x1.6c16c2p-9f), 0x1.555556p-3f), r);
   const float y = 1.0f - ((lo - PT_DIV(FAST, r * c, 2.0f - c)) - hi);
   if (k >= -125) {
     if (k > 127) return y * u2f((uint32_t)(127 + 127) << 23) * u2f((uint32_t)(k - 127 + 127) << 23);
@@ -145,22 +149,24 @@ PT_FN float exp_(float x) { return exp_impl<PT_FAST_DEV>(x); }
 PT_FN float ksin_(float x) {
   const float z = x * x;
   const float v = z * x;
-  const float r = 0x1.111112p-7f + z * (-0x1.a01a02p-13f + z * (0x1.71de36p-19f + z * (-0x1.ae5e68p-26f + z * 0x1.5d93a6p-33f)));
-  return x + v * (-0x1.555556p-3f + z * r);
+  const float r = fma_(z, fma_(z, fma_(z, fma_(z, 0x1.5d93a6p-33f, -0x1.ae5e68p-26f), 0x1.71de36p-19f),
+                               -0x1.a01a02p-13f), 0x1.111112p-7f);
+  return fma_(v, fma_(z, r, -0x1.555556p-3f), x);
 }
 PT_FN float kcos_(float x) {
   const float z = x * x;
-  const float r = z * (0x1.555556p-5f + z * (-0x1.6c16c2p-10f + z * (0x1.a01a02p-16f + z * (-0x1.27e4f8p-22f + z * (0x1.1ee9ecp-29f + z * -0x1.8fae9cp-37f)))));
+  const float r = z * fma_(z, fma_(z, fma_(z, fma_(z, fma_(z, -0x1.8fae9cp-37f, 0x1.1ee9ecp-29f), -0x1.27e4f8p-22f),
+                                          0x1.a01a02p-16f), -0x1.6c16c2p-10f), 0x1.555556p-5f);
   const float hz = 0.5f * z;
   const float w = 1.0f - hz;
-  return w + (((1.0f - w) - hz) + z * r);
+  return w + fma_(z, r, (1.0f - w) - hz);
 }
 // Cody–Waite reduction by pi/2 in three parts (12+12+24 bits): exact products
 // for |quadrant| < 4096, i.e. |x| < ~6400 — the shader only feeds [0, 2*pi].
 PT_FN float reduce_(float x, int* q) {
   const float jf = floor_(x * 0x1.45f306p-1f + 0.5f);
   *q = (int)jf;
-  return ((x - jf * 0x1.92p+0f) - jf * 0x1.fb4p-12f) - jf * 0x1.4442d2p-24f;
+  return fma_(-jf, 0x1.4442d2p-24f, fma_(-jf, 0x1.fb4p-12f, fma_(-jf, 0x1.92p+0f, x)));
 }
 PT_FN float sin_(float x) {
   int q;
@@ -201,8 +207,9 @@ PT_FN float tan_(float x) { return sin_(x) / cos_(x); }
 // fdlibm e_acosf.c algorithm (rational approximation of asin, three ranges).
 template <bool FAST>
 PT_FN float acos_rat_(float z) {
-  const float p = z * (0x1.555556p-3f + z * (-0x1.4d612p-2f + z * (0x1.9c155p-3f + z * (-0x1.48228cp-5f + z * (0x1.9efe08p-11f + z * 0x1.23de1p-15f)))));
-  const float q = 1.0f + z * (-0x1.33a272p+1f + z * (0x1.02ae5ap+1f + z * (-0x1.6066c2p-1f + z * 0x1.3b8c5cp-4f)));
+  const float p = z * fma_(z, fma_(z, fma_(z, fma_(z, fma_(z, 0x1.23de1p-15f, 0x1.9efe08p-11f), -0x1.48228cp-5f),
+                                          0x1.9c155p-3f), -0x1.4d612p-2f), 0x1.555556p-3f);
+  const float q = fma_(z, fma_(z, fma_(z, fma_(z, 0x1.3b8c5cp-4f, -0x1.6066c2p-1f), 0x1.02ae5ap+1f), -0x1.33a272p+1f), 1.0f);
   return PT_DIV(FAST, p, q);
 }
 template <bool FAST>
@@ -215,21 +222,21 @@ PT_FN float acos_impl(float x) {
     if (ix <= 0x32800000u) return pio2_hi + pio2_lo;
     const float z = x * x;
     const float r = acos_rat_<FAST>(z);
-    return pio2_hi - (x - (pio2_lo - x * r));
+    return pio2_hi - (x - fma_(-x, r, pio2_lo));
   }
   if (f2u(x) >> 31) {                          // x <= -0.5
     const float z = (1.0f + x) * 0.5f;
     const float s = sqrt_(z);
     const float r = acos_rat_<FAST>(z);
-    const float w = r * s - pio2_lo;
+    const float w = fma_(r, s, -pio2_lo);
     return pi_ - 2.0f * (s + w);
   }
   const float z = (1.0f - x) * 0.5f;           // x >= 0.5
   const float s = sqrt_(z);
   const float df = u2f(f2u(s) & 0xfffff000u);
-  const float c = PT_DIV(FAST, z - df * df, s + df);
+  const float c = PT_DIV(FAST, fma_(-df, df, z), s + df);
   const float r = acos_rat_<FAST>(z);
-  const float w = r * s + c;
+  const float w = fma_(r, s, c);
   return 2.0f * (df + w);
 }
 PT_FN float acos_(float x) { return acos_impl<PT_FAST_DEV>(x); }

@@ -4,8 +4,9 @@
 // (src/shaders/raytrace_comp.comp).  GLSL leaves the precision of
 // sin/cos/acos/log/exp/tan and the NaN behaviour of min/max to the driver, so
 // the reference output itself is not reproducible bit for bit; this file fixes
-// ONE definition (fdlibm float algorithms, fixed evaluation order, compiled
-// with -ffp-contract=off, no fast-math, denormals on) and the product's
+// ONE definition (fdlibm float algorithms with their polynomials evaluated as
+// explicit fma Horner chains, fixed evaluation order, compiled with
+// -ffp-contract=off, no fast-math, denormals on) and the product's
 // discovering-path-tracer_amd/csrc/pt_math.h must match it bit for bit
 // (tests/test_math.py).  The transcendental kernels are also checked against
 // libm in double precision, which pins them to the true functions within a
@@ -29,6 +30,9 @@ static inline float gm_fmax(float a, float b) {
   if (b != b) return a;
   return (a < b) ? b : a;
 }
+// Fused multiply-add, rounded once (polynomial kernels below are Horner
+// chains of fma: fewer roundings than mul+add, one GPU instruction per term).
+static inline float gm_fma(float a, float b, float c) { return fmaf(a, b, c); }
 static inline float gm_abs(float a) { return gm_u2f(gm_f2u(a) & 0x7fffffffu); }
 static inline float gm_sqrt(float a) { return sqrtf(a); }   // correctly rounded (SSE sqrtss)
 static inline float gm_floor(float a) { return floorf(a); }
@@ -57,11 +61,11 @@ static inline float gm_log(float x) {
   float dk = (float)k;
   float z = s * s;
   float w = z * z;
-  float t1 = w * (0x1.99999ap-2f + w * (0x1.c71c52p-3f + w * 0x1.39a09ep-3f));
-  float t2 = z * (0x1.555556p-1f + w * (0x1.24924ap-2f + w * (0x1.74664ap-3f + w * 0x1.2f112ep-3f)));
+  float t1 = w * gm_fma(w, gm_fma(w, 0x1.39a09ep-3f, 0x1.c71c52p-3f), 0x1.99999ap-2f);
+  float t2 = z * gm_fma(w, gm_fma(w, gm_fma(w, 0x1.2f112ep-3f, 0x1.74664ap-3f), 0x1.24924ap-2f), 0x1.555556p-1f);
   float R = t2 + t1;
   float hfsq = 0.5f * f * f;
-  return dk * 0x1.62e3p-1f - ((hfsq - (s * (hfsq + R) + dk * 0x1.2fefa2p-17f)) - f);
+  return gm_fma(dk, 0x1.62e3p-1f, -((hfsq - gm_fma(s, hfsq + R, dk * 0x1.2fefa2p-17f)) - f));
 }
 
 // exp: fdlibm e_expf.c — k = round(x/ln2), r = hi - lo, rational kernel, 2^k.
@@ -71,11 +75,12 @@ static inline float gm_exp(float x) {
   if (x < -103.972084045410156f) return 0.0f;
   float kf = gm_floor(x * 0x1.715476p+0f + 0.5f);
   int k = (int)kf;
-  float hi = x - kf * 0x1.62e4p-1f;
+  float hi = gm_fma(-kf, 0x1.62e4p-1f, x);
   float lo = kf * 0x1.7f7d1cp-20f;
   float r = hi - lo;
   float t = r * r;
-  float c = r - t * (0x1.555556p-3f + t * (-0x1.6c16c2p-9f + t * (0x1.1566aap-14f + t * (-0x1.bbd41cp-20f + t * 0x1.637698p-25f))));
+  float c = gm_fma(-t, gm_fma(t, gm_fma(t, gm_fma(t, gm_fma(t, 0x1.637698p-25f, -0x1.bbd41cp-20f), 0x1.1566aap-14f),
+                                        -0x1.6c16c2p-9f), 0x1.555556p-3f), r);
   float y = 1.0f - ((lo - (r * c) / (2.0f - c)) - hi);
   if (k >= -125) {
     if (k > 127) return y * gm_u2f((uint32_t)(127 + 127) << 23) * gm_u2f((uint32_t)(k - 127 + 127) << 23);
@@ -89,20 +94,22 @@ static inline float gm_exp(float x) {
 static inline float gm_ksin(float x) {
   float z = x * x;
   float v = z * x;
-  float r = 0x1.111112p-7f + z * (-0x1.a01a02p-13f + z * (0x1.71de36p-19f + z * (-0x1.ae5e68p-26f + z * 0x1.5d93a6p-33f)));
-  return x + v * (-0x1.555556p-3f + z * r);
+  float r = gm_fma(z, gm_fma(z, gm_fma(z, gm_fma(z, 0x1.5d93a6p-33f, -0x1.ae5e68p-26f), 0x1.71de36p-19f),
+                             -0x1.a01a02p-13f), 0x1.111112p-7f);
+  return gm_fma(v, gm_fma(z, r, -0x1.555556p-3f), x);
 }
 static inline float gm_kcos(float x) {
   float z = x * x;
-  float r = z * (0x1.555556p-5f + z * (-0x1.6c16c2p-10f + z * (0x1.a01a02p-16f + z * (-0x1.27e4f8p-22f + z * (0x1.1ee9ecp-29f + z * -0x1.8fae9cp-37f)))));
+  float r = z * gm_fma(z, gm_fma(z, gm_fma(z, gm_fma(z, gm_fma(z, -0x1.8fae9cp-37f, 0x1.1ee9ecp-29f), -0x1.27e4f8p-22f),
+                                          0x1.a01a02p-16f), -0x1.6c16c2p-10f), 0x1.555556p-5f);
   float hz = 0.5f * z;
   float w = 1.0f - hz;
-  return w + (((1.0f - w) - hz) + z * r);
+  return w + gm_fma(z, r, (1.0f - w) - hz);
 }
 static inline float gm_reduce(float x, int* q) {
   float jf = gm_floor(x * 0x1.45f306p-1f + 0.5f);
   *q = (int)jf;
-  return ((x - jf * 0x1.92p+0f) - jf * 0x1.fb4p-12f) - jf * 0x1.4442d2p-24f;
+  return gm_fma(-jf, 0x1.4442d2p-24f, gm_fma(-jf, 0x1.fb4p-12f, gm_fma(-jf, 0x1.92p+0f, x)));
 }
 static inline float gm_sin(float x) {
   int q;
@@ -128,8 +135,9 @@ static inline float gm_tan(float x) { return gm_sin(x) / gm_cos(x); }
 
 // acos: fdlibm e_acosf.c (rational asin kernel, three argument ranges).
 static inline float gm_acos_rat(float z) {
-  float p = z * (0x1.555556p-3f + z * (-0x1.4d612p-2f + z * (0x1.9c155p-3f + z * (-0x1.48228cp-5f + z * (0x1.9efe08p-11f + z * 0x1.23de1p-15f)))));
-  float q = 1.0f + z * (-0x1.33a272p+1f + z * (0x1.02ae5ap+1f + z * (-0x1.6066c2p-1f + z * 0x1.3b8c5cp-4f)));
+  float p = z * gm_fma(z, gm_fma(z, gm_fma(z, gm_fma(z, gm_fma(z, 0x1.23de1p-15f, 0x1.9efe08p-11f), -0x1.48228cp-5f),
+                                          0x1.9c155p-3f), -0x1.4d612p-2f), 0x1.555556p-3f);
+  float q = gm_fma(z, gm_fma(z, gm_fma(z, gm_fma(z, 0x1.3b8c5cp-4f, -0x1.6066c2p-1f), 0x1.02ae5ap+1f), -0x1.33a272p+1f), 1.0f);
   return p / q;
 }
 static inline float gm_acos(float x) {
@@ -141,21 +149,21 @@ static inline float gm_acos(float x) {
     if (ix <= 0x32800000u) return pio2_hi + pio2_lo;
     float z = x * x;
     float r = gm_acos_rat(z);
-    return pio2_hi - (x - (pio2_lo - x * r));
+    return pio2_hi - (x - gm_fma(-x, r, pio2_lo));
   }
   if (gm_f2u(x) >> 31) {
     float z = (1.0f + x) * 0.5f;
     float s = gm_sqrt(z);
     float r = gm_acos_rat(z);
-    float w = r * s - pio2_lo;
+    float w = gm_fma(r, s, -pio2_lo);
     return pi_ - 2.0f * (s + w);
   }
   float z = (1.0f - x) * 0.5f;
   float s = gm_sqrt(z);
   float df = gm_u2f(gm_f2u(s) & 0xfffff000u);
-  float c = (z - df * df) / (s + df);
+  float c = gm_fma(-df, df, z) / (s + df);
   float r = gm_acos_rat(z);
-  float w = r * s + c;
+  float w = gm_fma(r, s, c);
   return 2.0f * (df + w);
 }
 

@@ -1,6 +1,8 @@
 """Regenerates tests/golden/oracle_frames.json — SHA-256 of oracle frames of
 box.obj plus their traversal counters.  Run only when the oracle is changed
-on purpose (and say why in the commit)."""
+on purpose (and say why in the commit).  History: v1 frames used mul+add
+polynomials; v2 (fma Horner chains) changed low-order bits only — identical
+traversal counters and mean colour to 7 digits."""
 import hashlib
 import json
 import os
@@ -20,6 +22,8 @@ for W, H, spp, depth, sss in [(256, 256, 1, 1, 3), (256, 256, 1, 4, 3), (160, 90
     cases.append({"W": W, "H": H, "spp": spp, "depth": depth, "sss": sss,
                   "sha256": hashlib.sha256(acc.tobytes()).hexdigest(), "stats": st.tolist(),
                   "mean_rgb": float(acc.reshape(-1, 4)[:, :3].mean())})
-json.dump({"generator": "tests/golden/make_golden.py", "cases": cases}, open(os.path.join(HERE, "oracle_frames.json"), "w"),
+json.dump({"generator": "tests/golden/make_golden.py",
+           "math_definition": "oracle/glsl_math.h v2: fdlibm float kernels, polynomials as fma Horner chains",
+           "cases": cases}, open(os.path.join(HERE, "oracle_frames.json"), "w"),
           indent=1)
 print(json.dumps(cases, indent=1))
