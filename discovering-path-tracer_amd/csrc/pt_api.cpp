@@ -306,6 +306,13 @@ struct pt_context {
   int opt_kernel = 0;         // PT_OPT_KERNEL: 0 auto, 1 path-recursive, 2 lane state machine
   int opt_sm_batch = 1;       // PT_OPT_SM_BATCH
   int opt_cull = 1;           // PT_OPT_PRIMARY_CULL
+  // compact-launch item lists (live items, then culled ones), rebuilt when
+  // the frame, partition, sample lanes or cull rectangles change
+  int* d_items = nullptr;
+  size_t items_cap = 0;
+  int n_live_items = 0, n_culled_items = 0;
+  std::vector<int> h_items;
+  std::vector<float> items_key;
   float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};   // root AABB of the uploaded tree
   std::vector<pt_area_light> lights_host;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -387,6 +394,7 @@ int pt_destroy(pt_context* c) {
   dev_free(c->d_lights_dev);
   if (c->own_accum) dev_free(c->d_accum);
   dev_free(c->d_stats);
+  dev_free(c->d_items);
   for (auto& r : c->rb) {
     dev_free(r.dev);
     if (r.host) (void)hipHostFree(r.host);
@@ -573,6 +581,56 @@ int pt_read_accum(pt_context* c, float* rgba, size_t n) {
   return PT_OK;
 }
 
+// The items (owned tile x sample-lane part) the render kernel would launch,
+// split by the same float test its workgroups apply (render_kernel wg_live):
+// those whose pixel rectangle can touch a cull rectangle go to the render
+// kernel, the rest to fill_culled_kernel.  A culled workgroup still costs a
+// workgroup launch (a fully culled 1080p frame took 0.10 ms at 4 sample
+// lanes), so only live ones are launched.
+static int compact_items(pt_context* c, ptd::RenderParams* p) {
+  std::vector<float> key = {(float)p->width, (float)p->height, (float)p->nranks, (float)p->rank, (float)p->spl,
+                            (float)p->n_cull};
+  for (int r = 0; r < p->n_cull; ++r) key.insert(key.end(), p->cull[r], p->cull[r] + 4);
+  if (key.size() != c->items_key.size() || memcmp(key.data(), c->items_key.data(), key.size() * 4) != 0) {
+    const int W = p->width, H = p->height, spl = p->spl;
+    const int tiles = (p->blocks_total + p->nranks - 1 - p->rank) / p->nranks;
+    std::vector<int> live, culled;
+    for (int li = 0; li < tiles; ++li) {
+      const int b = li * p->nranks + p->rank;
+      const int gx0 = (b % p->blocks_x) * 16;
+      const float wx0 = (2.0f * (float)gx0 / (float)W) - 1.0f, wx1 = (2.0f * (float)(gx0 + 15) / (float)W) - 1.0f;
+      for (int part = 0; part < spl; ++part) {
+        const int gy0 = (b / p->blocks_x) * 16 + part * (16 / spl);
+        const float wy0 = (2.0f * (float)gy0 / (float)H) - 1.0f;
+        const float wy1 = (2.0f * (float)(gy0 + 16 / spl - 1) / (float)H) - 1.0f;
+        bool any = false;
+        for (int r = 0; r < p->n_cull && !any; ++r)
+          any = wx1 >= p->cull[r][0] && wx0 <= p->cull[r][1] && wy1 >= p->cull[r][2] && wy0 <= p->cull[r][3];
+        (any ? live : culled).push_back(li * spl + part);
+      }
+    }
+    PT_HIP(hipStreamSynchronize(c->stream));   // the previous list may still be in use
+    c->h_items = live;
+    c->h_items.insert(c->h_items.end(), culled.begin(), culled.end());
+    if (c->h_items.size() > c->items_cap) {
+      dev_free(c->d_items);
+      c->items_cap = 0;
+      PT_HIP(hipMalloc((void**)&c->d_items, c->h_items.size() * sizeof(int)));
+      c->items_cap = c->h_items.size();
+    }
+    if (!c->h_items.empty())
+      PT_HIP(hipMemcpy(c->d_items, c->h_items.data(), c->h_items.size() * sizeof(int), hipMemcpyHostToDevice));
+    c->n_live_items = (int)live.size();
+    c->n_culled_items = (int)culled.size();
+    c->items_key = key;
+  }
+  p->items = c->d_items;
+  p->n_items = c->n_live_items;
+  p->culled_items = c->d_items + c->n_live_items;
+  p->n_culled_items = c->n_culled_items;
+  return PT_OK;
+}
+
 int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   if (!c) return fail(PT_ERR_INVALID, "null context");
   if (!c->has_scene) return fail(PT_ERR_INVALID, "no scene uploaded");
@@ -640,9 +698,16 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   const bool sm = c->opt_kernel == 2;
   if (sm) p.spl = 1;
   p.n_cull = -1;
+  p.items = nullptr;
+  p.culled_items = nullptr;
+  p.n_items = p.n_culled_items = 0;
   if (c->opt_cull && !c->stats_mode && !sm)
     p.n_cull = cull_rects(c->cam, c->width, c->height, c->root_lo, c->root_hi, c->lights_host.data(),
                           c->n_lights, &p.cull[0][0], ptd::kMaxCullRects);
+  if (p.n_cull >= 0) {
+    const int rc = compact_items(c, &p);
+    if (rc) return rc;
+  }
   PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream));
   PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
   PT_HIP(hipEventRecord(c->ev1, c->stream));

@@ -56,6 +56,12 @@ struct RenderParams {
   int sm_batch;                 // state-machine kernel: lanes that must be waiting before shading runs
   // primary-ray culling (pt_primary_cull_rects): -1 = trace every pixel; else
   // a pixel traces only if its NDC origin lies in one of cull[0..n_cull)
+  // compact launch (host-built when culling applies): items (owned tile *
+  // spl + part) that may hold a live pixel, and those that cannot
+  const int* items;             // null = every item, blockIdx.x = item
+  int n_items;
+  const int* culled_items;
+  int n_culled_items;
   int n_cull;
   float cull[8][4];
 };

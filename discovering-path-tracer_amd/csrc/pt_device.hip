@@ -425,8 +425,11 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
   // A persistent variant pulling wave-sized items from per-XCD queues was
   // measured slower at every SPL, on 1 GPU and on a 1/8 tile share.
   const int spl = P.spl;
-  const int tile = ((int)blockIdx.x / spl) * P.nranks + P.rank;
-  const int part = (int)blockIdx.x % spl;
+  // item = (owned tile, part); with culling the host launches only items that
+  // can hold a live pixel, listed in P.items
+  const int item = P.items ? P.items[blockIdx.x] : (int)blockIdx.x;
+  const int tile = (item / spl) * P.nranks + P.rank;
+  const int part = item % spl;
   const int wave = tid >> 6, lane = tid & 63;
   __shared__ int cand_buf[4][kCand][64];
   __shared__ float4 col_buf[4][64];
@@ -567,6 +570,32 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
       atomicAdd(&P.stats[2], leaves);
       atomicAdd(&P.stats[3], smp);
     }
+  }
+}
+
+// Items (tile parts) whose every pixel is culled, listed by the host: each
+// thread folds the constant colour (0,0,0,1) into one pixel's running mean,
+// closed form where exact (fold_constant) — kPixPerFill pixels per thread.
+constexpr int kPixPerFill = 8;
+__global__ __launch_bounds__(256) void fill_culled_kernel(RenderParams P, const int* __restrict__ items, int n) {
+  const int spl = P.spl, per_item = 256 / spl;
+  const long long total = (long long)n * per_item;
+  for (int k = 0; k < kPixPerFill; ++k) {
+    const long long g = ((long long)blockIdx.x * kPixPerFill + k) * 256 + threadIdx.x;
+    if (g >= total) return;
+    const int item = items[g / per_item], q = (int)(g % per_item);
+    const int tile = (item / spl) * P.nranks + P.rank, part = item % spl;
+    const int px = (tile % P.blocks_x) * 16 + q % 16;
+    const int py = (tile / P.blocks_x) * 16 + part * (16 / spl) + q / 16;
+    if (px >= P.width || py >= P.height) continue;
+    float4* dst = P.accum + (size_t)py * (size_t)P.width + (size_t)px;
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (!(P.fresh && P.first_batch == 0)) {
+      const float4 a = *dst;
+      acc[0] = a.x; acc[1] = a.y; acc[2] = a.z; acc[3] = a.w;
+    }
+    fold_constant(P, acc, 1, 0);
+    *dst = make_float4(acc[0], acc[1], acc[2], acc[3]);
   }
 }
 
@@ -1138,8 +1167,9 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool
   if (p.spl != 1 && p.spl != 2 && p.spl != 4 && p.spl != 8) return hipErrorInvalidValue;
   // owned tiles b = rank + i*nranks; the recursive kernel splits each into spl workgroups
   const long long tiles = (long long)(p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;
-  const long long grid = state_machine ? tiles : tiles * p.spl;
+  long long grid = state_machine ? tiles : tiles * p.spl;
   if (grid <= 0 || p.n_batches == 0) return hipSuccess;
+  if (p.items && !state_machine) grid = p.n_items;   // compact list of live items
   if (grid > 0x7fffffffll) return hipErrorInvalidValue;
   const size_t lds = lds_scene ? scene_lds_bytes(p) : 0;
   if (lds > kMaxSceneLds) return hipErrorInvalidValue;
@@ -1150,7 +1180,14 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool
   else
     kern = lds_scene ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
                      : (stats ? render_kernel<true, false> : render_kernel<false, false>);
-  hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), lds, stream, p);
+  if (p.culled_items && p.n_culled_items > 0 && !state_machine) {
+    const long long px = (long long)p.n_culled_items * (256 / p.spl);
+    hipLaunchKernelGGL(fill_culled_kernel, dim3((unsigned)((px + 256 * kPixPerFill - 1) / (256 * kPixPerFill))),
+                       dim3(256), 0, stream, p, p.culled_items, p.n_culled_items);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (grid > 0) hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), lds, stream, p);
   return hipGetLastError();
 }
 

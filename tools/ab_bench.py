@@ -21,6 +21,9 @@ import scenes  # noqa: E402
 def load_scene(name):
     if name == "box":
         return ptamd.Scene.load_obj(scenes.BOX_OBJ).build_bvh(), scenes.DEFAULT_CAMERA
+    if name == "box_away":   # every pixel culled: the kernel's fixed per-workgroup cost
+        cam = np.array([-10, 0, 5, 0, 1, 0, 0, 0, 0, 1, 0, 0, 10, 0, 0, 0], np.float32)
+        return ptamd.Scene.load_obj(scenes.BOX_OBJ).build_bvh(), cam
     if name.startswith("sphere"):
         v, i = scenes.displaced_sphere(int(name.split(":")[1]) if ":" in name else 5)
         return ptamd.Scene.from_arrays(v, i).build_bvh(), scenes.camera((0.0, 0.5, 3.0))
