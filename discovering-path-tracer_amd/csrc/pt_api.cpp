@@ -676,12 +676,13 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   if (c->opt_sample_lanes) {
     p.spl = c->opt_sample_lanes;
   } else {
-    // auto: 4 sample lanes per pixel on a whole frame or a 1/2-1/3 share,
-    // 8 on smaller shares (each GPU's share of the frame shrinks while its
-    // heaviest workgroup does not) — measured on box.obj 1080p 8spp with
-    // primary culling: N=1 spl 1/2/4/8 = 0.524/0.469/0.455/0.544 ms,
-    // 1/8 share 0.315/0.186/0.127/0.093 ms.  Never more lanes than samples.
-    int want = c->nranks >= 4 ? 8 : 4;
+    // auto: 4 sample lanes per pixel on a whole frame, 8 on a share of it
+    // (each GPU's share shrinks while its heaviest workgroup does not) —
+    // measured on box.obj 1080p 8spp with culling and compact launch:
+    // spl 1/2/4/8 = 0.499/0.408/0.375/0.416 ms (whole frame), 0.354/0.264/
+    // 0.225/0.221 (1/2), 0.271/0.156/0.094/0.085 (1/8).  Never more lanes
+    // than samples.
+    int want = c->nranks >= 2 ? 8 : 4;
     while (want > 1 && (uint32_t)want > n_batches) want >>= 1;
     p.spl = want;
   }
