@@ -407,6 +407,34 @@ __device__ __forceinline__ void store_lane(float4* px, const float* acc, int spl
     if (ch % spl == j) a[ch] = acc[ch];
 }
 
+// Items (tile parts) whose every pixel is culled, listed by the host: each
+// thread folds the constant colour (0,0,0,1) into one pixel's running mean,
+// closed form where exact (fold_constant) — kPixPerFill pixels per thread.
+// Runs as the trailing workgroups of the render launch, so it overlaps the
+// render tail instead of costing a launch of its own.
+constexpr int kPixPerFill = 8;
+__device__ __forceinline__ void fill_culled(const RenderParams& P, const int* __restrict__ items, int n, int block) {
+  const int spl = P.spl, per_item = 256 / spl;
+  const long long total = (long long)n * per_item;
+  for (int k = 0; k < kPixPerFill; ++k) {
+    const long long g = ((long long)block * kPixPerFill + k) * 256 + threadIdx.x;
+    if (g >= total) return;
+    const int item = items[g / per_item], q = (int)(g % per_item);
+    const int tile = (item / spl) * P.nranks + P.rank, part = item % spl;
+    const int px = (tile % P.blocks_x) * 16 + q % 16;
+    const int py = (tile / P.blocks_x) * 16 + part * (16 / spl) + q / 16;
+    if (px >= P.width || py >= P.height) continue;
+    float4* dst = P.accum + (size_t)py * (size_t)P.width + (size_t)px;
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (!(P.fresh && P.first_batch == 0)) {
+      const float4 a = *dst;
+      acc[0] = a.x; acc[1] = a.y; acc[2] = a.z; acc[3] = a.w;
+    }
+    fold_constant(P, acc, 1, 0);
+    *dst = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  }
+}
+
 // LDS=true stages the whole scene (threaded nodes + triangle records) in LDS
 // once per workgroup; chosen by the host for scenes of at most a few tens of
 // KB (box.obj is 1.3 KB), where every lane re-reads the same few nodes.
@@ -424,6 +452,10 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
   // tile-split frame fast on 8 GPUs (pixels on geometry cost ~10x the others).
   // A persistent variant pulling wave-sized items from per-XCD queues was
   // measured slower at every SPL, on 1 GPU and on a 1/8 tile share.
+  if (P.items && (int)blockIdx.x >= P.n_items) {   // trailing fill workgroups (uniform)
+    fill_culled(P, P.culled_items, P.n_culled_items, (int)blockIdx.x - P.n_items);
+    return;
+  }
   const int spl = P.spl;
   // item = (owned tile, part); with culling the host launches only items that
   // can hold a live pixel, listed in P.items
@@ -570,32 +602,6 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
       atomicAdd(&P.stats[2], leaves);
       atomicAdd(&P.stats[3], smp);
     }
-  }
-}
-
-// Items (tile parts) whose every pixel is culled, listed by the host: each
-// thread folds the constant colour (0,0,0,1) into one pixel's running mean,
-// closed form where exact (fold_constant) — kPixPerFill pixels per thread.
-constexpr int kPixPerFill = 8;
-__global__ __launch_bounds__(256) void fill_culled_kernel(RenderParams P, const int* __restrict__ items, int n) {
-  const int spl = P.spl, per_item = 256 / spl;
-  const long long total = (long long)n * per_item;
-  for (int k = 0; k < kPixPerFill; ++k) {
-    const long long g = ((long long)blockIdx.x * kPixPerFill + k) * 256 + threadIdx.x;
-    if (g >= total) return;
-    const int item = items[g / per_item], q = (int)(g % per_item);
-    const int tile = (item / spl) * P.nranks + P.rank, part = item % spl;
-    const int px = (tile % P.blocks_x) * 16 + q % 16;
-    const int py = (tile / P.blocks_x) * 16 + part * (16 / spl) + q / 16;
-    if (px >= P.width || py >= P.height) continue;
-    float4* dst = P.accum + (size_t)py * (size_t)P.width + (size_t)px;
-    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    if (!(P.fresh && P.first_batch == 0)) {
-      const float4 a = *dst;
-      acc[0] = a.x; acc[1] = a.y; acc[2] = a.z; acc[3] = a.w;
-    }
-    fold_constant(P, acc, 1, 0);
-    *dst = make_float4(acc[0], acc[1], acc[2], acc[3]);
   }
 }
 
@@ -1169,7 +1175,10 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool
   const long long tiles = (long long)(p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;
   long long grid = state_machine ? tiles : tiles * p.spl;
   if (grid <= 0 || p.n_batches == 0) return hipSuccess;
-  if (p.items && !state_machine) grid = p.n_items;   // compact list of live items
+  if (p.items && !state_machine) {   // compact list of live items, then the fill workgroups
+    const long long px = (long long)p.n_culled_items * (256 / p.spl);
+    grid = p.n_items + (px + 256 * kPixPerFill - 1) / (256 * kPixPerFill);
+  }
   if (grid > 0x7fffffffll) return hipErrorInvalidValue;
   const size_t lds = lds_scene ? scene_lds_bytes(p) : 0;
   if (lds > kMaxSceneLds) return hipErrorInvalidValue;
@@ -1180,13 +1189,6 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool
   else
     kern = lds_scene ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
                      : (stats ? render_kernel<true, false> : render_kernel<false, false>);
-  if (p.culled_items && p.n_culled_items > 0 && !state_machine) {
-    const long long px = (long long)p.n_culled_items * (256 / p.spl);
-    hipLaunchKernelGGL(fill_culled_kernel, dim3((unsigned)((px + 256 * kPixPerFill - 1) / (256 * kPixPerFill))),
-                       dim3(256), 0, stream, p, p.culled_items, p.n_culled_items);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
   if (grid > 0) hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), lds, stream, p);
   return hipGetLastError();
 }
