@@ -5,8 +5,9 @@
 A step is one frame.  It renders the 8 sample batches from a fresh
 accumulator in one fused launch, bit-identical to 8 progressive 1-spp
 dispatches after a clear.  For N > 1 the frame is split into 16x16 screen
-tiles (tile b on rank b % N).  Every rank packs its tiles and the root
-assembles them with one RCCL gather.  The gather of frame k overlaps the
+tiles (tile b on rank b % N).  Every rank packs the tile parts that can
+hold a live pixel (primary culling) and the root assembles them with one
+RCCL gather, rebuilding the culled parts.  The gather of frame k overlaps the
 render of frame k+1 (double-buffered); the timed region ends only after the
 last frame is assembled.
 
@@ -209,10 +210,16 @@ def main():
                 if rank == 0:
                     frame.copy_(c)
     else:
-        max_own = int(allreduce_max(torch.tensor([r.tiles_owned()], dtype=torch.int64, device=dev)).item())
-        send = [torch.zeros((max_own, 256, 4), dtype=torch.float32, device=dev) for _ in range(2)]
-        recv = [[torch.empty((max_own, 256, 4), dtype=torch.float32, device=dev) for _ in range(world)]
-                for _ in range(2)] if rank == 0 else None
+        # Sparse gather: each rank ships only its live items (tile parts that
+        # can hold a live pixel under primary culling); the root rebuilds the
+        # culled ones.  Every rank derives every rank's item count itself.
+        r.render(0, SPP)
+        per = r.items_live(0)[1]
+        slot = max(r.items_live(k)[0] for k in range(world)) * per * 4
+        slot = max(slot, 4)
+        send = [torch.zeros(slot, dtype=torch.float32, device=dev) for _ in range(2)]
+        recv_all = [torch.empty((world, slot), dtype=torch.float32, device=dev) for _ in range(2)] if rank == 0 else None
+        recv = [[recv_all[b][k] for k in range(world)] for b in range(2)] if rank == 0 else None
         out = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
         state = {"k": 0}
 
@@ -220,14 +227,13 @@ def main():
             if work is not None:
                 work.wait()
             if rank == 0:
-                for src in range(world):
-                    r.tiles_unpack(recv[buf][src].data_ptr(), src, out.data_ptr())
+                r.items_unpack_all(recv_all[buf].data_ptr(), slot, out.data_ptr())
 
         def step():
             buf = state["k"] % 2
             state["k"] += 1
             r.render(0, SPP)
-            r.tiles_pack(send[buf].data_ptr())
+            r.items_pack(send[buf].data_ptr())
             if backend == "nccl":
                 work = dist.gather(send[buf], recv[buf] if rank == 0 else None, dst=0, async_op=True)
             else:
@@ -327,7 +333,8 @@ def main():
             "data": "synthetic (reference scene, camera and light; progressive sample batches 0-%d)" % (SPP - 1),
             "config": {"workload": wl, "width": W, "height": H, "spp": SPP, "max_depth": DEPTH,
                        "sss_bounces": SSS,
-                       "parallelism": f"tiles{world}-{args.collective}" if world > 1 else "single",
+                       "parallelism": (f"tiles{world}-" + ("sparse-gather" if args.collective == "gather" else "reduce"))
+                       if world > 1 else "single",
                        "rays_per_frame": int(rays_per_frame),
                        "primary_cull": True,
                        "msamples_per_s": round(W * H * SPP * args.steps / dt / 1e6, 3)},

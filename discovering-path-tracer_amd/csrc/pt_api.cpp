@@ -313,6 +313,17 @@ struct pt_context {
   int n_live_items = 0, n_culled_items = 0;
   std::vector<int> h_items;
   std::vector<float> items_key;
+  ptd::RenderParams last{};     // configuration of the last pt_render
+  bool last_valid = false;
+  // sparse exchange: this rank's live items, and all ranks' (root)
+  int* d_pack_items = nullptr;
+  size_t pack_cap = 0;
+  int n_pack_items = 0;
+  std::vector<float> pack_key;
+  int* d_unpack = nullptr;      // per entry: rank, item, slot (-1 = culled)
+  size_t unpack_cap = 0;
+  int n_unpack = 0;
+  std::vector<float> unpack_key;
   float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};   // root AABB of the uploaded tree
   std::vector<pt_area_light> lights_host;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -395,6 +406,8 @@ int pt_destroy(pt_context* c) {
   if (c->own_accum) dev_free(c->d_accum);
   dev_free(c->d_stats);
   dev_free(c->d_items);
+  dev_free(c->d_pack_items);
+  dev_free(c->d_unpack);
   for (auto& r : c->rb) {
     dev_free(r.dev);
     if (r.host) (void)hipHostFree(r.host);
@@ -587,28 +600,34 @@ int pt_read_accum(pt_context* c, float* rgba, size_t n) {
 // kernel, the rest to fill_culled_kernel.  A culled workgroup still costs a
 // workgroup launch (a fully culled 1080p frame took 0.10 ms at 4 sample
 // lanes), so only live ones are launched.
+static void item_lists(const ptd::RenderParams& p, int rank, std::vector<int>* live, std::vector<int>* culled) {
+  const int W = p.width, H = p.height, spl = p.spl;
+  const int tiles = (p.blocks_total + p.nranks - 1 - rank) / p.nranks;
+  live->clear();
+  culled->clear();
+  for (int li = 0; li < tiles; ++li) {
+    const int b = li * p.nranks + rank;
+    const int gx0 = (b % p.blocks_x) * 16;
+    const float wx0 = (2.0f * (float)gx0 / (float)W) - 1.0f, wx1 = (2.0f * (float)(gx0 + 15) / (float)W) - 1.0f;
+    for (int part = 0; part < spl; ++part) {
+      const int gy0 = (b / p.blocks_x) * 16 + part * (16 / spl);
+      const float wy0 = (2.0f * (float)gy0 / (float)H) - 1.0f;
+      const float wy1 = (2.0f * (float)(gy0 + 16 / spl - 1) / (float)H) - 1.0f;
+      bool any = p.n_cull < 0;   // no culling: every item is live
+      for (int r = 0; r < p.n_cull && !any; ++r)
+        any = wx1 >= p.cull[r][0] && wx0 <= p.cull[r][1] && wy1 >= p.cull[r][2] && wy0 <= p.cull[r][3];
+      (any ? live : culled)->push_back(li * spl + part);
+    }
+  }
+}
+
 static int compact_items(pt_context* c, ptd::RenderParams* p) {
   std::vector<float> key = {(float)p->width, (float)p->height, (float)p->nranks, (float)p->rank, (float)p->spl,
                             (float)p->n_cull};
   for (int r = 0; r < p->n_cull; ++r) key.insert(key.end(), p->cull[r], p->cull[r] + 4);
   if (key.size() != c->items_key.size() || memcmp(key.data(), c->items_key.data(), key.size() * 4) != 0) {
-    const int W = p->width, H = p->height, spl = p->spl;
-    const int tiles = (p->blocks_total + p->nranks - 1 - p->rank) / p->nranks;
     std::vector<int> live, culled;
-    for (int li = 0; li < tiles; ++li) {
-      const int b = li * p->nranks + p->rank;
-      const int gx0 = (b % p->blocks_x) * 16;
-      const float wx0 = (2.0f * (float)gx0 / (float)W) - 1.0f, wx1 = (2.0f * (float)(gx0 + 15) / (float)W) - 1.0f;
-      for (int part = 0; part < spl; ++part) {
-        const int gy0 = (b / p->blocks_x) * 16 + part * (16 / spl);
-        const float wy0 = (2.0f * (float)gy0 / (float)H) - 1.0f;
-        const float wy1 = (2.0f * (float)(gy0 + 16 / spl - 1) / (float)H) - 1.0f;
-        bool any = false;
-        for (int r = 0; r < p->n_cull && !any; ++r)
-          any = wx1 >= p->cull[r][0] && wx0 <= p->cull[r][1] && wy1 >= p->cull[r][2] && wy0 <= p->cull[r][3];
-        (any ? live : culled).push_back(li * spl + part);
-      }
-    }
+    item_lists(*p, p->rank, &live, &culled);
     PT_HIP(hipStreamSynchronize(c->stream));   // the previous list may still be in use
     c->h_items = live;
     c->h_items.insert(c->h_items.end(), culled.begin(), culled.end());
@@ -709,6 +728,8 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
     const int rc = compact_items(c, &p);
     if (rc) return rc;
   }
+  c->last = p;   // the item exchange (pt_items_*) follows the last rendered frame
+  c->last_valid = !sm;
   PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream));
   PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
   PT_HIP(hipEventRecord(c->ev1, c->stream));
@@ -859,6 +880,82 @@ int pt_tiles_unpack(pt_context* c, const void* src, int src_rank, void* frame) {
   if ((((uintptr_t)src) & 15) || (((uintptr_t)frame) & 15)) return fail(PT_ERR_INVALID, "buffers must be 16-B aligned");
   PT_HIP(hipSetDevice(c->device));
   PT_HIP(ptd::launch_tiles(false, (float4*)frame, (float4*)src, c->width, c->height, c->nranks, src_rank, c->stream));
+  return PT_OK;
+}
+
+// ---- sparse tile exchange (live items only) --------------------------------
+namespace {
+std::vector<float> frame_key(const ptd::RenderParams& p) {
+  std::vector<float> key = {(float)p.width, (float)p.height, (float)p.nranks, (float)p.rank, (float)p.spl,
+                            (float)p.n_cull, (float)p.blocks_x, (float)p.blocks_total};
+  for (int r = 0; r < p.n_cull; ++r) key.insert(key.end(), p.cull[r], p.cull[r] + 4);
+  return key;
+}
+int upload_ints(const std::vector<int>& h, int** d, size_t* cap) {
+  if (h.size() > *cap) {
+    dev_free(*d);
+    *cap = 0;
+    PT_HIP(hipMalloc((void**)d, h.size() * sizeof(int)));
+    *cap = h.size();
+  }
+  if (!h.empty()) PT_HIP(hipMemcpy(*d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice));
+  return PT_OK;
+}
+}  // namespace
+
+int pt_items_live(pt_context* c, int rank, int* n_items, int* item_pixels) {
+  if (!c || !n_items || !item_pixels) return fail(PT_ERR_INVALID, "null argument");
+  if (!c->last_valid) return fail(PT_ERR_INVALID, "no path-recursive pt_render yet");
+  if (rank < 0 || rank >= c->last.nranks) return fail(PT_ERR_INVALID, "rank out of range");
+  std::vector<int> live, culled;
+  item_lists(c->last, rank, &live, &culled);
+  *n_items = (int)live.size();
+  *item_pixels = 256 / c->last.spl;
+  return PT_OK;
+}
+
+int pt_items_pack(pt_context* c, void* dst) {
+  if (!c || !dst) return fail(PT_ERR_INVALID, "null argument");
+  if (!c->last_valid || !c->d_accum) return fail(PT_ERR_INVALID, "no path-recursive pt_render yet");
+  PT_HIP(hipSetDevice(c->device));
+  const std::vector<float> key = frame_key(c->last);
+  if (key != c->pack_key) {
+    std::vector<int> live, culled;
+    item_lists(c->last, c->last.rank, &live, &culled);
+    PT_HIP(hipStreamSynchronize(c->stream));
+    const int rc = upload_ints(live, &c->d_pack_items, &c->pack_cap);
+    if (rc) return rc;
+    c->n_pack_items = (int)live.size();
+    c->pack_key = key;
+  }
+  PT_HIP(ptd::launch_items_pack(c->last, c->d_accum, (float4*)dst, c->d_pack_items, c->n_pack_items, c->stream));
+  return PT_OK;
+}
+
+int pt_items_unpack_all(pt_context* c, const void* src, size_t slot_floats, void* frame) {
+  if (!c || !src || !frame) return fail(PT_ERR_INVALID, "null argument");
+  if (!c->last_valid) return fail(PT_ERR_INVALID, "no path-recursive pt_render yet");
+  if (c->last.first_batch != 0)
+    return fail(PT_ERR_INVALID, "sparse exchange needs a frame rendered from batch 0 (culled pixels are rebuilt)");
+  if ((((uintptr_t)src) & 15) || (((uintptr_t)frame) & 15) || (slot_floats & 3))
+    return fail(PT_ERR_INVALID, "buffers must be 16-B aligned, slots whole float4s");
+  PT_HIP(hipSetDevice(c->device));
+  const std::vector<float> key = frame_key(c->last);
+  if (key != c->unpack_key) {
+    std::vector<int> table, live, culled;
+    for (int r = 0; r < c->last.nranks; ++r) {
+      item_lists(c->last, r, &live, &culled);
+      for (size_t i = 0; i < live.size(); ++i) table.insert(table.end(), {r, live[i], (int)i});
+      for (int it : culled) table.insert(table.end(), {r, it, -1});
+    }
+    PT_HIP(hipStreamSynchronize(c->stream));
+    const int rc = upload_ints(table, &c->d_unpack, &c->unpack_cap);
+    if (rc) return rc;
+    c->n_unpack = (int)(table.size() / 3);
+    c->unpack_key = key;
+  }
+  PT_HIP(ptd::launch_items_unpack(c->last, (float4*)frame, (const float4*)src, slot_floats / 4, c->d_unpack,
+                                  c->n_unpack, c->stream));
   return PT_OK;
 }
 

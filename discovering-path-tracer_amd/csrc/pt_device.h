@@ -74,6 +74,13 @@ int owned_tiles(int width, int height, int nranks, int rank);
 hipError_t launch_tiles(bool pack, float4* frame, float4* packed, int width, int height, int nranks, int rank,
                         hipStream_t stream);
 hipError_t launch_clear(float4* accum, int width, int height, int nranks, int rank, hipStream_t stream);
+// live-item exchange: pack this rank's listed items (256/spl pixels each) of
+// frame densely; unpack entries {rank, item, slot} from per-rank slots of
+// slot_f4 float4s into frame, slot -1 = culled item -> (0,0,0,1)
+hipError_t launch_items_pack(const RenderParams& p, const float4* frame, float4* packed, const int* items, int n,
+                             hipStream_t stream);
+hipError_t launch_items_unpack(const RenderParams& p, float4* frame, const float4* src, size_t slot_f4,
+                               const int* table, int n, hipStream_t stream);
 // Scene bytes the LDS-staged variant needs, and the largest it accepts.
 constexpr size_t kMaxSceneLds = 48 * 1024;
 inline size_t scene_lds_bytes(const RenderParams& p) {

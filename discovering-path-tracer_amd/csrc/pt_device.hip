@@ -677,6 +677,40 @@ __global__ __launch_bounds__(256) void tiles_kernel(float4* frame, float4* packe
     frame[pi] = packed[ti];
 }
 
+// Pixel q of item `item` of rank `rank` (the render kernel's mapping).
+__device__ __forceinline__ bool item_pixel(const RenderParams& P, int rank, int item, int q, size_t* pix) {
+  const int spl = P.spl;
+  const int tile = (item / spl) * P.nranks + rank, part = item % spl;
+  const int px = (tile % P.blocks_x) * 16 + q % 16;
+  const int py = (tile / P.blocks_x) * 16 + part * (16 / spl) + q / 16;
+  *pix = (size_t)py * (size_t)P.width + (size_t)px;
+  return px < P.width && py < P.height;
+}
+
+__global__ __launch_bounds__(256) void items_pack_kernel(RenderParams P, const float4* __restrict__ frame,
+                                                         float4* __restrict__ packed, const int* __restrict__ items,
+                                                         int n) {
+  const int per = 256 / P.spl;
+  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (long long)n * per) return;
+  size_t pix;
+  const bool in = item_pixel(P, P.rank, items[g / per], (int)(g % per), &pix);
+  packed[g] = in ? frame[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+
+__global__ __launch_bounds__(256) void items_unpack_kernel(RenderParams P, float4* __restrict__ frame,
+                                                           const float4* __restrict__ src, size_t slot_f4,
+                                                           const int* __restrict__ table, int n) {
+  const int per = 256 / P.spl;
+  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (g >= (long long)n * per) return;
+  const int* e = table + 3 * (g / per);
+  const int q = (int)(g % per);
+  size_t pix;
+  if (!item_pixel(P, e[0], e[1], q, &pix)) return;
+  frame[pix] = e[2] >= 0 ? src[(size_t)e[0] * slot_f4 + (size_t)e[2] * per + q] : make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+}
+
 __global__ __launch_bounds__(256) void math_kernel(int fn, const float* __restrict__ x, float* __restrict__ y,
                                                    size_t n) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1159,6 +1193,22 @@ hipError_t launch_tiles(bool pack, float4* frame, float4* packed, int width, int
     tiles_kernel<true><<<n, 256, 0, stream>>>(frame, packed, width, height, bx, nranks, rank);
   else
     tiles_kernel<false><<<n, 256, 0, stream>>>(frame, packed, width, height, bx, nranks, rank);
+  return hipGetLastError();
+}
+
+hipError_t launch_items_pack(const RenderParams& p, const float4* frame, float4* packed, const int* items, int n,
+                             hipStream_t stream) {
+  const long long px = (long long)n * (256 / p.spl);
+  if (px == 0) return hipSuccess;
+  items_pack_kernel<<<(unsigned)((px + 255) / 256), 256, 0, stream>>>(p, frame, packed, items, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_items_unpack(const RenderParams& p, float4* frame, const float4* src, size_t slot_f4,
+                               const int* table, int n, hipStream_t stream) {
+  const long long px = (long long)n * (256 / p.spl);
+  if (px == 0) return hipSuccess;
+  items_unpack_kernel<<<(unsigned)((px + 255) / 256), 256, 0, stream>>>(p, frame, src, slot_f4, table, n);
   return hipGetLastError();
 }
 

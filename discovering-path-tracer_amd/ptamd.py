@@ -35,6 +35,7 @@ EXPORTS = [
     "pt_scene_counts", "pt_scene_copy", "pt_scene_upload", "pt_scene_free", "pt_pack_light",
     "pt_default_camera", "pt_primary_cull_rects", "pt_scene_save", "pt_scene_load_cache",
     "pt_progressive_camera", "pt_progressive_advance", "pt_readback_begin", "pt_readback_end", "pt_write_image",
+    "pt_items_live", "pt_items_pack", "pt_items_unpack_all",
 ]
 
 
@@ -96,6 +97,9 @@ def lib():
             "pt_readback_begin": ([vp, ctypes.POINTER(i32)], i32),
             "pt_readback_end": ([vp, i32, vp, sz], i32),
             "pt_write_image": ([ctypes.c_char_p, vp, i32, i32, i32], i32),
+            "pt_items_live": ([vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
+            "pt_items_pack": ([vp, vp], i32),
+            "pt_items_unpack_all": ([vp, vp, sz, vp], i32),
             "pt_scene_load_cache": ([ctypes.c_char_p, ctypes.POINTER(vp)], i32),
         }
         for name, (args, res) in sig.items():
@@ -326,6 +330,18 @@ class Renderer:
         out = np.empty(self.width * self.height * 4, np.float32)
         _check(lib().pt_readback_end(self._c, ticket, out.ctypes.data, out.size), "pt_readback_end")
         return out
+
+    def items_live(self, rank):
+        """(live items of `rank` in the last rendered frame, pixels per item)."""
+        n, per = ctypes.c_int(0), ctypes.c_int(0)
+        _check(lib().pt_items_live(self._c, rank, ctypes.byref(n), ctypes.byref(per)), "pt_items_live")
+        return n.value, per.value
+
+    def items_pack(self, dst_ptr):
+        _check(lib().pt_items_pack(self._c, dst_ptr), "pt_items_pack")
+
+    def items_unpack_all(self, src_ptr, slot_floats, frame_ptr):
+        _check(lib().pt_items_unpack_all(self._c, src_ptr, slot_floats, frame_ptr), "pt_items_unpack_all")
 
     def set_option(self, key, value):
         _check(lib().pt_set_option(self._c, key, value), "pt_set_option")

@@ -162,6 +162,18 @@ int pt_set_partition(pt_context* ctx, int nranks, int rank);
 int pt_tiles_owned(pt_context* ctx, int* n_tiles);
 int pt_tiles_pack(pt_context* ctx, void* dst_device);
 int pt_tiles_unpack(pt_context* ctx, const void* src_device, int src_rank, void* frame_device);
+/* Sparse exchange of the last rendered frame: only the tile parts ("items",
+ * 256/SPL pixels each) that can hold a live pixel under primary culling.
+ * Every rank must have rendered the same frame (camera, size, partition
+ * size, batches).  pt_items_live: rank's live item count and pixels per item
+ * (a slot must hold n_items*item_pixels float4).  pt_items_pack: this rank's
+ * live items, densely.  pt_items_unpack_all: rank r's slot at
+ * src + r*slot_floats; live items are scattered into the frame, culled ones
+ * written as (0,0,0,1) — their value for a frame rendered from batch 0, which
+ * this call requires.  With culling off every item is live. */
+int pt_items_live(pt_context* ctx, int rank, int* n_items, int* item_pixels);
+int pt_items_pack(pt_context* ctx, void* dst_device);
+int pt_items_unpack_all(pt_context* ctx, const void* src_device, size_t slot_floats, void* frame_device);
 
 /* ---- kernel options ---------------------------------------------------- */
 /* PT_OPT_SCENE_IN_LDS: stage the scene in LDS per workgroup — 0 never,

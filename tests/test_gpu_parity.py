@@ -379,3 +379,39 @@ def test_progressive_loop_camera_reset_and_async_readback():
     _assert_same(r.read_accum(), acc, "accumulator")
     with pytest.raises(ptamd.PTError):
         r.readback_end(t2)                        # already collected
+
+
+@pytest.mark.parametrize("nranks,cam", [(2, 0), (3, 1), (8, 0), (2, 5)])
+def test_sparse_item_exchange_assembles_frame(nranks, cam):
+    """pt_items_pack (live items only) on every rank + one pt_items_unpack_all
+    on the root = the single-GPU frame; culled items are rebuilt as
+    (0,0,0,1).  Camera 5 sits inside the box (no culling: every item live)."""
+    import torch
+    v, i, n = _box()
+    W, H = 150, 70
+    camera = CULL_CAMS[cam]
+    rs, counts = [], []
+    for rank in range(nranks):
+        r = _setup(v, i, n, cam=camera)
+        r.set_partition(nranks, rank)
+        r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+        r.resize_and_clear(W, H)
+        r.render(0, 8)
+        rs.append(r)
+    per = rs[0].items_live(0)[1]
+    counts = [rs[0].items_live(k)[0] for k in range(nranks)]
+    assert all(rs[k].items_live(k) == (counts[k], per) for k in range(nranks))
+    slot = max(counts) * per * 4
+    src = torch.full((nranks, max(slot, 4)), float("nan"), dtype=torch.float32, device="cuda")
+    for k, r in enumerate(rs):
+        r.items_pack(src[k].data_ptr())
+        r.synchronize()
+    frame = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+    rs[0].items_unpack_all(src.data_ptr(), src.shape[1], frame.data_ptr())
+    rs[0].synchronize()
+    ref, _ = _oracle(v, i, n, W, H, nb=8, cam=camera)
+    _assert_same(frame.cpu().numpy().reshape(-1), ref, f"sparse exchange over {nranks}")
+    if cam == 5:
+        assert sum(counts) * per >= W * H
+    else:
+        assert sum(counts) * per < W * H          # culled items are not shipped
