@@ -356,6 +356,81 @@ struct pt_scene {
   uint32_t flags = 0;
 };
 
+// The items (owned tile x sample-lane part) the render kernel would launch,
+// split by the same float test its workgroups apply (render_kernel wg_live):
+// those whose pixel rectangle can touch a cull rectangle go to the render
+// kernel, the rest to fill_culled_kernel.  A culled workgroup still costs a
+// workgroup launch (a fully culled 1080p frame took 0.10 ms at 4 sample
+// lanes), so only live ones are launched.
+static void item_lists(const ptd::RenderParams& p, int rank, std::vector<int>* live, std::vector<int>* culled) {
+  const int W = p.width, H = p.height, spl = p.spl;
+  const int tiles = (p.blocks_total + p.nranks - 1 - rank) / p.nranks;
+  live->clear();
+  culled->clear();
+  for (int li = 0; li < tiles; ++li) {
+    const int b = li * p.nranks + rank;
+    const int gx0 = (b % p.blocks_x) * 16;
+    const float wx0 = (2.0f * (float)gx0 / (float)W) - 1.0f, wx1 = (2.0f * (float)(gx0 + 15) / (float)W) - 1.0f;
+    for (int part = 0; part < spl; ++part) {
+      const int gy0 = (b / p.blocks_x) * 16 + part * (16 / spl);
+      const float wy0 = (2.0f * (float)gy0 / (float)H) - 1.0f;
+      const float wy1 = (2.0f * (float)(gy0 + 16 / spl - 1) / (float)H) - 1.0f;
+      bool any = p.n_cull < 0;   // no culling: every item is live
+      for (int r = 0; r < p.n_cull && !any; ++r)
+        any = wx1 >= p.cull[r][0] && wx0 <= p.cull[r][1] && wy1 >= p.cull[r][2] && wy0 <= p.cull[r][3];
+      (any ? live : culled)->push_back(li * spl + part);
+    }
+  }
+}
+
+static int compact_items(pt_context* c, ptd::RenderParams* p) {
+  std::vector<float> key = {(float)p->width, (float)p->height, (float)p->nranks, (float)p->rank, (float)p->spl,
+                            (float)p->n_cull};
+  for (int r = 0; r < p->n_cull; ++r) key.insert(key.end(), p->cull[r], p->cull[r] + 4);
+  if (key.size() != c->items_key.size() || memcmp(key.data(), c->items_key.data(), key.size() * 4) != 0) {
+    std::vector<int> live, culled;
+    item_lists(*p, p->rank, &live, &culled);
+    PT_HIP(hipStreamSynchronize(c->stream));   // the previous list may still be in use
+    c->h_items = live;
+    c->h_items.insert(c->h_items.end(), culled.begin(), culled.end());
+    if (c->h_items.size() > c->items_cap) {
+      dev_free(c->d_items);
+      c->items_cap = 0;
+      PT_HIP(hipMalloc((void**)&c->d_items, c->h_items.size() * sizeof(int)));
+      c->items_cap = c->h_items.size();
+    }
+    if (!c->h_items.empty())
+      PT_HIP(hipMemcpy(c->d_items, c->h_items.data(), c->h_items.size() * sizeof(int), hipMemcpyHostToDevice));
+    c->n_live_items = (int)live.size();
+    c->n_culled_items = (int)culled.size();
+    c->items_key = key;
+  }
+  p->items = c->d_items;
+  p->n_items = c->n_live_items;
+  p->culled_items = c->d_items + c->n_live_items;
+  p->n_culled_items = c->n_culled_items;
+  return PT_OK;
+}
+
+namespace {
+std::vector<float> frame_key(const ptd::RenderParams& p) {
+  std::vector<float> key = {(float)p.width, (float)p.height, (float)p.nranks, (float)p.rank, (float)p.spl,
+                            (float)p.n_cull, (float)p.blocks_x, (float)p.blocks_total};
+  for (int r = 0; r < p.n_cull; ++r) key.insert(key.end(), p.cull[r], p.cull[r] + 4);
+  return key;
+}
+int upload_ints(const std::vector<int>& h, int** d, size_t* cap) {
+  if (h.size() > *cap) {
+    dev_free(*d);
+    *cap = 0;
+    PT_HIP(hipMalloc((void**)d, h.size() * sizeof(int)));
+    *cap = h.size();
+  }
+  if (!h.empty()) PT_HIP(hipMemcpy(*d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice));
+  return PT_OK;
+}
+}  // namespace
+
 extern "C" {
 
 int pt_abi_version(void) { return PT_ABI_VERSION; }
@@ -594,62 +669,6 @@ int pt_read_accum(pt_context* c, float* rgba, size_t n) {
   return PT_OK;
 }
 
-// The items (owned tile x sample-lane part) the render kernel would launch,
-// split by the same float test its workgroups apply (render_kernel wg_live):
-// those whose pixel rectangle can touch a cull rectangle go to the render
-// kernel, the rest to fill_culled_kernel.  A culled workgroup still costs a
-// workgroup launch (a fully culled 1080p frame took 0.10 ms at 4 sample
-// lanes), so only live ones are launched.
-static void item_lists(const ptd::RenderParams& p, int rank, std::vector<int>* live, std::vector<int>* culled) {
-  const int W = p.width, H = p.height, spl = p.spl;
-  const int tiles = (p.blocks_total + p.nranks - 1 - rank) / p.nranks;
-  live->clear();
-  culled->clear();
-  for (int li = 0; li < tiles; ++li) {
-    const int b = li * p.nranks + rank;
-    const int gx0 = (b % p.blocks_x) * 16;
-    const float wx0 = (2.0f * (float)gx0 / (float)W) - 1.0f, wx1 = (2.0f * (float)(gx0 + 15) / (float)W) - 1.0f;
-    for (int part = 0; part < spl; ++part) {
-      const int gy0 = (b / p.blocks_x) * 16 + part * (16 / spl);
-      const float wy0 = (2.0f * (float)gy0 / (float)H) - 1.0f;
-      const float wy1 = (2.0f * (float)(gy0 + 16 / spl - 1) / (float)H) - 1.0f;
-      bool any = p.n_cull < 0;   // no culling: every item is live
-      for (int r = 0; r < p.n_cull && !any; ++r)
-        any = wx1 >= p.cull[r][0] && wx0 <= p.cull[r][1] && wy1 >= p.cull[r][2] && wy0 <= p.cull[r][3];
-      (any ? live : culled)->push_back(li * spl + part);
-    }
-  }
-}
-
-static int compact_items(pt_context* c, ptd::RenderParams* p) {
-  std::vector<float> key = {(float)p->width, (float)p->height, (float)p->nranks, (float)p->rank, (float)p->spl,
-                            (float)p->n_cull};
-  for (int r = 0; r < p->n_cull; ++r) key.insert(key.end(), p->cull[r], p->cull[r] + 4);
-  if (key.size() != c->items_key.size() || memcmp(key.data(), c->items_key.data(), key.size() * 4) != 0) {
-    std::vector<int> live, culled;
-    item_lists(*p, p->rank, &live, &culled);
-    PT_HIP(hipStreamSynchronize(c->stream));   // the previous list may still be in use
-    c->h_items = live;
-    c->h_items.insert(c->h_items.end(), culled.begin(), culled.end());
-    if (c->h_items.size() > c->items_cap) {
-      dev_free(c->d_items);
-      c->items_cap = 0;
-      PT_HIP(hipMalloc((void**)&c->d_items, c->h_items.size() * sizeof(int)));
-      c->items_cap = c->h_items.size();
-    }
-    if (!c->h_items.empty())
-      PT_HIP(hipMemcpy(c->d_items, c->h_items.data(), c->h_items.size() * sizeof(int), hipMemcpyHostToDevice));
-    c->n_live_items = (int)live.size();
-    c->n_culled_items = (int)culled.size();
-    c->items_key = key;
-  }
-  p->items = c->d_items;
-  p->n_items = c->n_live_items;
-  p->culled_items = c->d_items + c->n_live_items;
-  p->n_culled_items = c->n_culled_items;
-  return PT_OK;
-}
-
 int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   if (!c) return fail(PT_ERR_INVALID, "null context");
   if (!c->has_scene) return fail(PT_ERR_INVALID, "no scene uploaded");
@@ -884,24 +903,6 @@ int pt_tiles_unpack(pt_context* c, const void* src, int src_rank, void* frame) {
 }
 
 // ---- sparse tile exchange (live items only) --------------------------------
-namespace {
-std::vector<float> frame_key(const ptd::RenderParams& p) {
-  std::vector<float> key = {(float)p.width, (float)p.height, (float)p.nranks, (float)p.rank, (float)p.spl,
-                            (float)p.n_cull, (float)p.blocks_x, (float)p.blocks_total};
-  for (int r = 0; r < p.n_cull; ++r) key.insert(key.end(), p.cull[r], p.cull[r] + 4);
-  return key;
-}
-int upload_ints(const std::vector<int>& h, int** d, size_t* cap) {
-  if (h.size() > *cap) {
-    dev_free(*d);
-    *cap = 0;
-    PT_HIP(hipMalloc((void**)d, h.size() * sizeof(int)));
-    *cap = h.size();
-  }
-  if (!h.empty()) PT_HIP(hipMemcpy(*d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice));
-  return PT_OK;
-}
-}  // namespace
 
 int pt_items_live(pt_context* c, int rank, int* n_items, int* item_pixels) {
   if (!c || !n_items || !item_pixels) return fail(PT_ERR_INVALID, "null argument");
