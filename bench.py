@@ -138,7 +138,9 @@ def main():
     dist = None
     dev = torch.device("cuda", device)
     torch.cuda.set_device(dev)
-    if world > 1:
+    # PT_BENCH_FORCE_DIST=1 runs the N>1 step (pack, RCCL gather, unpack) at
+    # N=1 too: measures the exchange's own overhead on a 1-GPU box
+    if world > 1 or os.environ.get("PT_BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
         kw = {"device_id": dev} if backend == "nccl" else {}
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
