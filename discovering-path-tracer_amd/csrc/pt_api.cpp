@@ -714,13 +714,16 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   if (c->opt_sample_lanes) {
     p.spl = c->opt_sample_lanes;
   } else {
-    // auto: 4 sample lanes per pixel on a whole frame, 8 on a share of it
-    // (each GPU's share shrinks while its heaviest workgroup does not) —
-    // measured on box.obj 1080p 8spp with culling and compact launch:
-    // spl 1/2/4/8 = 0.499/0.408/0.375/0.416 ms (whole frame), 0.354/0.264/
-    // 0.225/0.221 (1/2), 0.271/0.156/0.094/0.085 (1/8).  Never more lanes
-    // than samples.
-    int want = c->nranks >= 2 ? 8 : 4;
+    // auto: 4 sample lanes per pixel for an LDS-resident scene on a whole
+    // frame, else 8 — on a share of the frame each GPU's share shrinks while
+    // its heaviest workgroup does not, and on big scenes the samples of one
+    // pixel walk nearly the same nodes, so their loads coalesce.  Measured
+    // at 1080p 8spp with culling and compact launch: box spl 1/2/4/8 =
+    // 0.499/0.408/0.375/0.416 ms (whole frame), 0.354/0.264/0.225/0.221
+    // (1/2), 0.271/0.156/0.094/0.085 (1/8); displaced sphere 828/645/582/563;
+    // 1M cloud 968/930/927/923.  Never more lanes than samples.
+    const bool small = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
+    int want = (c->nranks >= 2 || !small) ? 8 : 4;
     while (want > 1 && (uint32_t)want > n_batches) want >>= 1;
     p.spl = want;
   }

@@ -1,4 +1,3 @@
 set -e
-timeout -k 10 300 python3 bench.py --no-cpu-baseline --steps 50 > gpurun_out/b1.log 2>&1; grep '^{' gpurun_out/b1.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('plain', d['ms_per_step'], d['roofline']['kernel_ms'])"
-PT_BENCH_FORCE_DIST=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29511 bench.py --no-cpu-baseline --steps 50 > gpurun_out/b2.log 2>&1; grep '^{' gpurun_out/b2.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('dist1', d['ms_per_step'], d['roofline']['kernel_ms'], d['config']['parallelism'])"
-PT_BENCH_FORCE_DIST=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29512 bench.py --no-cpu-baseline --steps 50 --collective reduce > gpurun_out/b3.log 2>&1; grep '^{' gpurun_out/b3.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('dist1-reduce', d['ms_per_step'], d['roofline']['kernel_ms'])"
+timeout -k 10 300 python3 tools/ab_bench.py --scene sphere:6 --spp 8 --reps 2 --no-parity s1:opt2=1 s2:opt2=2 s4:opt2=4 s8:opt2=8 | tail -n 1
+timeout -k 10 300 python3 tools/ab_bench.py --scene random:1000000 --spp 8 --reps 2 --no-parity s1:opt2=1 s2:opt2=2 s4:opt2=4 s8:opt2=8 | tail -n 1
