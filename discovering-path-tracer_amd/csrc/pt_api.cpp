@@ -303,9 +303,10 @@ struct pt_context {
   int opt_scene_lds = 1;   // PT_OPT_SCENE_IN_LDS: 0 never, 1 auto, 2 always
   int opt_sample_lanes = 0;   // PT_OPT_SAMPLE_LANES: 0 auto, else 1/2/4/8
   int opt_fresh = 0;          // PT_OPT_FRESH_BATCH0
-  int opt_kernel = 0;         // PT_OPT_KERNEL: 0 auto, 1 path-recursive, 2 lane state machine
+  int opt_kernel = 0;         // PT_OPT_KERNEL: 0 auto, 1 path-recursive, 2 lane state machine, 3 wavefront
   int opt_sm_batch = 1;       // PT_OPT_SM_BATCH
   int opt_cull = 1;           // PT_OPT_PRIMARY_CULL
+  int opt_wf_paths = 0;       // PT_OPT_WF_PATHS (0 = 2^24)
   // compact-launch item lists (live items, then culled ones), rebuilt when
   // the frame, partition, sample lanes or cull rectangles change
   int* d_items = nullptr;
@@ -327,6 +328,9 @@ struct pt_context {
   float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};   // root AABB of the uploaded tree
   std::vector<pt_area_light> lights_host;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // wavefront pipeline buffers (PT_OPT_KERNEL 3), grown on demand
+  ptd::WfBuffers wf{};
+  void* wf_block = nullptr;
   // progressive loop (VulkanRayTracer::mainLoop, :717-865)
   float prog_cam[16] = {0};
   bool prog_has_cam = false;
@@ -429,6 +433,35 @@ int upload_ints(const std::vector<int>& h, int** d, size_t* cap) {
   if (!h.empty()) PT_HIP(hipMemcpy(*d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice));
   return PT_OK;
 }
+// Wavefront buffers for `paths` paths in one allocation.  Up to 2^24 paths
+// (4.3 GB) are kept per launch; more batches run in chunks of that size.
+constexpr long long kWfMaxPaths = 1ll << 24;
+int wf_reserve(pt_context* c, long long pixels, uint32_t batches, long long* chunk_paths) {
+  const long long limit = c->opt_wf_paths > 0 ? c->opt_wf_paths : kWfMaxPaths;
+  const long long want = std::max(pixels, std::min(pixels * (long long)batches, limit));
+  if (want > 0x7fffffffll) return fail(PT_ERR_UNSUPPORTED, "frame too large for the wavefront kernel");
+  *chunk_paths = want;
+  if (want <= c->wf.cap) return PT_OK;
+  PT_HIP(hipStreamSynchronize(c->stream));
+  dev_free(c->wf_block);
+  c->wf = ptd::WfBuffers{};
+  const size_t n = (size_t)want;
+  const size_t b_state = n * ptd::kWfStateF4 * 16, b_col = n * 16, b_rays = n * 32, b_ids = n * 4, b_hits = n * 8;
+  char* base = nullptr;
+  PT_HIP(hipMalloc((void**)&base, b_state + b_col + 2 * (b_rays + b_ids) + b_hits + 64));
+  c->wf_block = base;
+  char* q = base;
+  c->wf.state = (float4*)q;    q += b_state;
+  c->wf.colors = (float4*)q;   q += b_col;
+  c->wf.rays[0] = (float4*)q;  q += b_rays;
+  c->wf.rays[1] = (float4*)q;  q += b_rays;
+  c->wf.hits = (float2*)q;     q += b_hits;
+  c->wf.ids[0] = (int*)q;      q += b_ids;
+  c->wf.ids[1] = (int*)q;      q += b_ids;
+  c->wf.counters = (int*)q;
+  c->wf.cap = want;
+  return PT_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -483,6 +516,7 @@ int pt_destroy(pt_context* c) {
   dev_free(c->d_items);
   dev_free(c->d_pack_items);
   dev_free(c->d_unpack);
+  dev_free(c->wf_block);
   for (auto& r : c->rb) {
     dev_free(r.dev);
     if (r.host) (void)hipHostFree(r.host);
@@ -738,6 +772,8 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   // option; it was measured slower on every scene (1080p: displaced sphere
   // 8 spp 1022 vs 596 ms, 1M-triangle cloud 1 spp 191 vs 127 ms).
   const bool sm = c->opt_kernel == 2;
+  const bool wf = c->opt_kernel == 3;
+  if (wf && c->stats_mode) return fail(PT_ERR_UNSUPPORTED, "stats mode runs the path-recursive kernel only");
   if (sm) p.spl = 1;
   p.n_cull = -1;
   p.items = nullptr;
@@ -752,7 +788,18 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   }
   c->last = p;   // the item exchange (pt_items_*) follows the last rendered frame
   c->last_valid = !sm;
-  PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream));
+  if (wf) {
+    const long long tiles = (p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;
+    const long long items = p.items ? p.n_items : tiles * p.spl;
+    long long chunk_paths = 0;
+    const int rc = wf_reserve(c, items * (256 / p.spl), n_batches, &chunk_paths);
+    if (rc) return rc;
+    ptd::WfBuffers b = c->wf;
+    b.cap = chunk_paths;   // paths per chunk (the allocation may be larger)
+    PT_HIP(ptd::launch_wavefront(p, b, lds, c->stream));
+  } else {
+    PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream));
+  }
   PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
   PT_HIP(hipEventRecord(c->ev1, c->stream));
   c->ring_n++;
@@ -851,12 +898,16 @@ int pt_set_option(pt_context* c, int key, int value) {
   if (!c) return fail(PT_ERR_INVALID, "null context");
   switch (key) {
     case PT_OPT_KERNEL:
-      if (value < 0 || value > 2) return fail(PT_ERR_INVALID, "PT_OPT_KERNEL takes 0, 1 or 2");
+      if (value < 0 || value > 3) return fail(PT_ERR_INVALID, "PT_OPT_KERNEL takes 0, 1, 2 or 3");
       c->opt_kernel = value;
       return PT_OK;
     case PT_OPT_PRIMARY_CULL:
       if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_PRIMARY_CULL takes 0 or 1");
       c->opt_cull = value;
+      return PT_OK;
+    case PT_OPT_WF_PATHS:
+      if (value < 0) return fail(PT_ERR_INVALID, "PT_OPT_WF_PATHS takes 0 or a path count");
+      c->opt_wf_paths = value;
       return PT_OK;
     case PT_OPT_SM_BATCH:
       if (value < 1 || value > 64) return fail(PT_ERR_INVALID, "PT_OPT_SM_BATCH takes 1..64");

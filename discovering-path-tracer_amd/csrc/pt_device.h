@@ -87,6 +87,29 @@ inline size_t scene_lds_bytes(const RenderParams& p) {
   return ((size_t)2 * p.n_nodes + (size_t)3 * p.n_tris) * 16;
 }
 hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool state_machine, hipStream_t stream);
+// Wavefront pipeline (PT_OPT_KERNEL 3): one path per (pixel, sample) held in
+// HBM; generate, then alternate a persistent traversal kernel over the list of
+// paths waiting for a ray and a shading kernel that consumes the hits and
+// emits the next rays; finally fold each pixel's sample colours in batch
+// order.  Buffers hold `cap` paths; larger launches run in batch chunks.
+struct WfBuffers {
+  float4* state;     // kWfStateF4 float4 per path (PathSt)
+  float4* colors;    // per path radiance
+  int* ids[2];       // work lists: path id per slot
+  float4* rays[2];   // ... and its ray, 2 float4 per slot: {o.xyz, limit} {d.xyz, shadow}
+  float2* hits;      // per slot of the list being traced: {t, tri bits / occluded}
+  int* counters;     // [0],[1] list sizes, [2] trace fetch cursor
+  long long cap;     // paths the buffers hold
+};
+constexpr int kWfStateF4 = 10;
+constexpr size_t kWfBytesPerPath = (size_t)kWfStateF4 * 16 + 16 + 2 * (4 + 32) + 8;
+// rays a path may trace in one sample: the primary ray, then per bounce the
+// light shadow rays, sss_bounces x (walk ray + light shadow rays) and the
+// next bounce ray
+inline int wf_max_rays(const RenderParams& p) {
+  return 1 + p.max_depth * (p.n_lights + p.sss_bounces * (1 + p.n_lights) + 1);
+}
+hipError_t launch_wavefront(const RenderParams& p, const WfBuffers& b, bool lds_scene, hipStream_t stream);
 hipError_t launch_math(int fn, const float* x, float* y, size_t n, hipStream_t stream);
 hipError_t launch_exhaustive(int fn, unsigned long long* bad, uint32_t* first_bad, hipStream_t stream);
 

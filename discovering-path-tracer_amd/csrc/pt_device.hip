@@ -22,6 +22,8 @@
 //
 // Numerics: every float op is the reference's, in its order, via pt_math.h;
 // the file is compiled with -ffp-contract=off and correctly rounded div/sqrt.
+#include <algorithm>
+
 #include "pt_device.h"
 #include "pt_math.h"
 
@@ -885,10 +887,13 @@ __device__ __forceinline__ void camera_ray(const CamFrame& F, uint32_t seed, v3*
   *dir = normalize(sub(focal, *origin));
 }
 
-// Runs lane-local shading from the current phase until the lane needs a ray
-// traced (returns true, T set up) or has finished all its samples (false).
+// pathTrace (:300-418) as a state machine over one sample: runs shading from
+// the current phase until a ray must be traced (returns true, T set up; the
+// caller traces it and calls again with T.lim/T.res holding the result) or
+// the sample is complete (returns false, *out = its radiance).  Shared by the
+// lane state-machine kernel and the wavefront pipeline.
 template <bool STATS>
-__device__ bool sm_run(const RenderParams& P, const CamFrame& F, PathSt& S, Trav& T, Ctr& c, float* acc) {
+__device__ bool path_step(const RenderParams& P, const CamFrame& F, PathSt& S, Trav& T, Ctr& c, v3* out) {
   const float OFFSET = 0.001f;
   const v3 albedo = mk(0.8f, 0.8f, 0.8f);
   const v3 sss_albedo = mk(1.0f, 0.2f, 0.1f);
@@ -1058,16 +1063,28 @@ __device__ bool sm_run(const RenderParams& P, const CamFrame& F, PathSt& S, Trav
       finished = true;
     }
     if (finished) {
-      const uint32_t batch = P.first_batch + S.s;
-      const float fb = (float)batch, fb1 = (float)(batch + 1u);          // :468
-      acc[0] = (acc[0] * fb + color.x) / fb1;
-      acc[1] = (acc[1] * fb + color.y) / fb1;
-      acc[2] = (acc[2] * fb + color.z) / fb1;
-      acc[3] = (acc[3] * fb + 1.0f) / fb1;
-      S.s++;
-      if (S.s >= P.n_batches) return false;
-      S.phase = PH_BEGIN;
+      *out = color;
+      return false;
     }
+  }
+}
+
+// Runs a lane's samples in order: path_step until a ray is needed (true) or
+// the lane's last sample is folded into acc (false).
+template <bool STATS>
+__device__ bool sm_run(const RenderParams& P, const CamFrame& F, PathSt& S, Trav& T, Ctr& c, float* acc) {
+  for (;;) {
+    v3 color;
+    if (path_step<STATS>(P, F, S, T, c, &color)) return true;
+    const uint32_t batch = P.first_batch + S.s;
+    const float fb = (float)batch, fb1 = (float)(batch + 1u);          // :468
+    acc[0] = (acc[0] * fb + color.x) / fb1;
+    acc[1] = (acc[1] * fb + color.y) / fb1;
+    acc[2] = (acc[2] * fb + color.z) / fb1;
+    acc[3] = (acc[3] * fb + 1.0f) / fb1;
+    S.s++;
+    if (S.s >= P.n_batches) return false;
+    S.phase = PH_BEGIN;
   }
 }
 
@@ -1151,6 +1168,324 @@ __global__ __launch_bounds__(256, PT_SM_MIN_BLOCKS) void render_sm_kernel(Render
       atomicAdd(&P.stats[3], smp);
     }
   }
+}
+
+
+// ===========================================================================
+// Wavefront pipeline, for scenes too large for LDS.
+//
+// Measured on the 1080p displaced sphere (16.6M paths): the path-recursive
+// kernel keeps 11 % of its lanes busy (VALUUtilization) with L2 hit rate 92 %
+// and no memory stall — the wave waits for its longest walk.  Here every
+// (pixel, sample) path lives in HBM (PathSt, 160 B) and the work is split by
+// kind: a persistent traversal kernel whose lanes pull waiting paths from a
+// list and refill as soon as their walk ends (uniform code, ~20 live VGPRs),
+// and a shading kernel that consumes the hits with path_step() and appends
+// the paths that need another ray to the next list.  Each path's arithmetic,
+// RNG draws and traversal order are those of path_trace(); the colours are
+// folded per pixel in batch order at the end, so the image is bit-identical.
+// ===========================================================================
+static_assert(sizeof(PathSt) == kWfStateF4 * 16, "PathSt is stored as kWfStateF4 float4");
+
+__device__ __forceinline__ void wf_load_state(const float4* __restrict__ src, PathSt* S) {
+  float4 v[kWfStateF4];
+#pragma unroll
+  for (int i = 0; i < kWfStateF4; ++i) v[i] = src[i];
+  __builtin_memcpy(S, v, sizeof(PathSt));
+}
+
+__device__ __forceinline__ void wf_store_state(float4* __restrict__ dst, const PathSt& S) {
+  float4 v[kWfStateF4];
+  __builtin_memcpy(v, &S, sizeof(PathSt));
+#pragma unroll
+  for (int i = 0; i < kWfStateF4; ++i) dst[i] = v[i];
+}
+
+__device__ __forceinline__ void wf_store_ray(float4* __restrict__ dst, const Trav& T) {
+  dst[0] = make_float4(T.o.x, T.o.y, T.o.z, T.lim);
+  dst[1] = make_float4(T.d.x, T.d.y, T.d.z, __int_as_float(T.shadow));
+}
+
+// A list slot for every lane with pred set (-1 for the others): one atomic
+// per wave, consecutive slots in lane order.
+__device__ __forceinline__ int wave_slot(int* counter, bool pred) {
+  const unsigned long long m = __ballot(pred);
+  if (m == 0ull) return -1;
+  const int lane = (int)__lane_id();
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, (int)__popcll(m));
+  base = __shfl(base, leader);
+  return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+
+__device__ __forceinline__ void wf_push(const WfBuffers& B, int list, int slot, int p, const Trav& T) {
+  B.ids[list][slot] = p;
+  wf_store_ray(B.rays[list] + 2 * (size_t)slot, T);
+}
+
+// Path g of a launch: pixel (item, q) = g / n_batches, sample g % n_batches
+// (samples of a pixel adjacent, so the fold reads them contiguously).
+__device__ __forceinline__ bool wf_pixel(const RenderParams& P, long long pp, int* px, int* py) {
+  const int spl = P.spl, per = 256 / spl;
+  const int idx = (int)(pp / per), q = (int)(pp % per);
+  const int item = P.items ? P.items[idx] : idx;
+  const int tile = (item / spl) * P.nranks + P.rank, part = item % spl;
+  *px = (tile % P.blocks_x) * 16 + q % 16;
+  *py = (tile / P.blocks_x) * 16 + part * (16 / spl) + q / 16;
+  return tile < P.blocks_total && *px < P.width && *py < P.height;
+}
+
+// render_kernel's per-pixel culling test, same float ops.
+__device__ __forceinline__ bool pixel_live(const RenderParams& P, float ndcX0, float ndcY0) {
+  if (P.n_cull < 0) return true;
+  bool live = false;
+#pragma unroll
+  for (int r = 0; r < kMaxCullRects; ++r)
+    live = live || (r < P.n_cull && ndcX0 >= P.cull[r][0] && ndcX0 <= P.cull[r][1] && ndcY0 >= P.cull[r][2] &&
+                    ndcY0 <= P.cull[r][3]);
+  return live;
+}
+
+// Ray generation + shading up to the primary trace (path_step from PH_BEGIN).
+__global__ __launch_bounds__(256) void wf_gen_kernel(RenderParams P, WfBuffers B, long long n) {
+  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+  bool need = false;
+  Trav T;
+  if (g < n) {
+    const long long pp = g / (long long)P.n_batches;
+    CamFrame F;
+    if (wf_pixel(P, pp, &F.px, &F.py)) {
+      F.W = P.width;
+      F.H = P.height;
+      F.cpos = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
+      F.cdir = mk(P.cam_dir[0], P.cam_dir[1], P.cam_dir[2]);
+      F.ndcX0 = (2.0f * (float)F.px / (float)F.W) - 1.0f;
+      F.ndcY0 = (2.0f * (float)F.py / (float)F.H) - 1.0f;
+      F.aspect = (float)F.W / (float)F.H;
+      F.right = mk(P.cam_right[0], P.cam_right[1], P.cam_right[2]);
+      F.up = mk(P.cam_upv[0], P.cam_upv[1], P.cam_upv[2]);
+      F.tanFov = P.tan_fov;
+      v3 col = mk(0.0f, 0.0f, 0.0f);
+      if (pixel_live(P, F.ndcX0, F.ndcY0)) {
+        PathSt S;
+        S.s = (uint32_t)(g - pp * (long long)P.n_batches);
+        S.phase = PH_BEGIN;
+        Ctr c = {0u, 0u, 0u};
+        need = path_step<false>(P, F, S, T, c, &col);
+        if (need) wf_store_state(B.state + (size_t)g * kWfStateF4, S);
+      }
+      if (!need) B.colors[g] = make_float4(col.x, col.y, col.z, 1.0f);
+    }
+  }
+  const int slot = wave_slot(&B.counters[0], need);
+  if (need) wf_push(B, 0, slot, (int)g, T);
+}
+
+// Traversal state of one lane of the persistent traversal kernel: the ray,
+// the walk position and the node at it (loaded one step ahead, as in
+// trace_closest).
+struct WfLane {
+  v3 o, d, inv;
+  float4 a, b;   // node k
+  int k, nc, res, shadow;
+  float lim;
+};
+
+__device__ __forceinline__ void wf_lane_start(const float4* __restrict__ ray, float4 root_a, float4 root_b,
+                                              WfLane& L) {
+  const float4 r0 = ray[0], r1 = ray[1];
+  L.o = mk(r0.x, r0.y, r0.z);
+  L.d = mk(r1.x, r1.y, r1.z);
+  L.inv = mk(rcp_(L.d.x), rcp_(L.d.y), rcp_(L.d.z));
+  L.shadow = __float_as_int(r1.w);
+  L.lim = L.shadow ? r0.w : 1e30f;
+  L.res = L.shadow ? 0 : -1;
+  L.k = 0;
+  L.nc = 0;
+  L.a = root_a;
+  L.b = root_b;
+}
+
+// One node of trace_closest / occluded (same visit order and tests); true
+// when the ray is finished (L.lim / L.res hold the result).
+template <bool PF>
+__device__ __forceinline__ bool wf_lane_step(const RenderParams& P, WfLane& L, int* cand) {
+  if (L.k >= P.n_nodes) {
+    if (!L.shadow) test_candidates(P, L.o, L.d, cand, L.nc, &L.lim, &L.res);
+    return true;
+  }
+  float4 na, nb;
+  if (PF) {
+    na = P.nodes[2 * L.k + 2];
+    nb = P.nodes[2 * L.k + 3];
+  }
+  const int raw = __float_as_int(L.a.w);
+  const bool h = (raw < 0) | slab(L.o, L.inv, L.a, L.b);
+  const int tri = __float_as_int(L.b.w);
+  const bool leaf_hit = h && tri >= 0;
+  if (L.shadow) {
+    if (leaf_hit) {
+      const float4* T = P.tris + 3 * tri;
+      float t;
+      if (tri_test(L.o, L.d, T[0], T[1], T[2], &t) && t < 1e30f && !(t >= L.lim)) {
+        L.res = 1;
+        return true;
+      }
+    }
+  } else {
+    cand[L.nc * 64] = tri;
+    L.nc += leaf_hit ? 1 : 0;
+    if (L.nc == kCand) {
+      test_candidates(P, L.o, L.d, cand, L.nc, &L.lim, &L.res);
+      L.nc = 0;
+    }
+  }
+  const int next = (h && tri < 0) ? L.k + 1 : (raw & 0x7fffffff);
+  if (PF && next == L.k + 1) {
+    L.a = na;
+    L.b = nb;
+  } else {
+    L.a = P.nodes[2 * next];
+    L.b = P.nodes[2 * next + 1];
+  }
+  L.k = next;
+  return false;
+}
+
+// Persistent traversal over list `cur`: lanes pull path ids (one atomic per
+// wave) and refill once at least PT_WF_REFILL lanes are idle.
+#ifndef PT_WF_STEPS
+#define PT_WF_STEPS 8
+#endif
+#ifndef PT_WF_REFILL
+#define PT_WF_REFILL 1
+#endif
+#ifndef PT_WF_MIN_BLOCKS
+#define PT_WF_MIN_BLOCKS 6
+#endif
+template <bool LDS>
+__global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderParams P, WfBuffers B, int cur) {
+  const int tid = (int)threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0) B.counters[cur ^ 1] = 0;   // filled by the shading that follows
+  const int count = B.counters[cur];
+  if (count == 0) return;
+  if (LDS) {
+    extern __shared__ float4 lds_scene[];
+    const int nn = 2 * P.n_nodes, nt = 3 * P.n_tris;
+    for (int i = tid; i < nn; i += 256) lds_scene[i] = P.nodes[i];
+    for (int i = tid; i < nt; i += 256) lds_scene[nn + i] = P.tris[i];
+    __syncthreads();
+    P.nodes = lds_scene;
+    P.tris = lds_scene + nn;
+  }
+  const int wave = tid >> 6, lane = tid & 63;
+  __shared__ int cand_buf[4][kCand][64];
+  int* cand = &cand_buf[wave][0][lane];
+  const float4* __restrict__ rays = B.rays[cur];
+  // every walk starts at node 0: held in scalar registers
+  float4 root_a = P.nodes[0], root_b = P.nodes[1];
+  root_a.x = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(root_a.x)));
+  root_a.y = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(root_a.y)));
+  root_a.z = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(root_a.z)));
+  root_a.w = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(root_a.w)));
+  root_b.x = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(root_b.x)));
+  root_b.y = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(root_b.y)));
+  root_b.z = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(root_b.z)));
+  root_b.w = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(root_b.w)));
+  int p = -1;   // list slot this lane traces
+  bool more = true;
+  WfLane L;
+  for (;;) {
+    const unsigned long long idle = __ballot(p < 0);
+    if (more && (int)__popcll(idle) >= PT_WF_REFILL) {
+      const int n = (int)__popcll(idle);
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&B.counters[2], n);
+      base = __shfl(base, 0);
+      if (base + n >= count) more = false;
+      if (p < 0) {
+        const int slot = base + (int)__popcll(idle & ((1ull << lane) - 1ull));
+        if (slot < count) {
+          p = slot;
+          wf_lane_start(rays + 2 * (size_t)slot, root_a, root_b, L);
+        }
+      }
+    }
+    if (!more && __ballot(p >= 0) == 0ull) break;
+    for (int it = 0; it < PT_WF_STEPS; ++it) {
+      if (p >= 0 && wf_lane_step<!LDS>(P, L, cand)) {
+        B.hits[p] = make_float2(L.lim, __int_as_float(L.res));
+        p = -1;
+      }
+    }
+  }
+}
+
+// Shading of every path in list `cur` (path_step on the returned hit);
+// paths that need another ray go to list cur^1, finished ones store colour.
+__global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers B, int cur) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) B.counters[2] = 0;   // the next traversal's cursor
+  const int count = B.counters[cur];
+  CamFrame F = {};   // camera frame: used by PH_BEGIN only
+  for (int base = (int)blockIdx.x * 256; base < count; base += (int)gridDim.x * 256) {
+    const int i = base + (int)threadIdx.x;
+    bool need = false;
+    int p = -1;
+    Trav T;
+    if (i < count) {
+      p = B.ids[cur][i];
+      PathSt S;
+      wf_load_state(B.state + (size_t)p * kWfStateF4, &S);
+      const float4 r0 = B.rays[cur][2 * (size_t)i], r1 = B.rays[cur][2 * (size_t)i + 1];
+      const float2 h = B.hits[i];
+      T.o = mk(r0.x, r0.y, r0.z);
+      T.d = mk(r1.x, r1.y, r1.z);
+      T.shadow = __float_as_int(r1.w);
+      T.lim = h.x;
+      T.res = __float_as_int(h.y);
+      T.nc = 0;
+      T.cn = T.cl = 0u;
+      Ctr c = {0u, 0u, 0u};
+      v3 col;
+      need = path_step<false>(P, F, S, T, c, &col);
+      if (need)
+        wf_store_state(B.state + (size_t)p * kWfStateF4, S);
+      else
+        B.colors[p] = make_float4(col.x, col.y, col.z, 1.0f);
+    }
+    const int slot = wave_slot(&B.counters[cur ^ 1], need);
+    if (need) wf_push(B, cur ^ 1, slot, p, T);
+  }
+}
+
+// Running mean (:467-469) of each pixel's samples, in batch order.
+__global__ __launch_bounds__(256) void wf_fold_kernel(RenderParams P, WfBuffers B, long long n_pix) {
+  const long long pp = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (pp >= n_pix) return;
+  int px, py;
+  if (!wf_pixel(P, pp, &px, &py)) return;
+  float4* dst = P.accum + (size_t)py * (size_t)P.width + (size_t)px;
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (!(P.fresh && P.first_batch == 0)) {
+    const float4 a = *dst;
+    acc[0] = a.x; acc[1] = a.y; acc[2] = a.z; acc[3] = a.w;
+  }
+  const float4* col = B.colors + (size_t)pp * P.n_batches;
+  for (uint32_t s = 0; s < P.n_batches; ++s) {
+    const float4 c = col[s];
+    const uint32_t batch = P.first_batch + s;
+    const float fb = (float)batch, fb1 = (float)(batch + 1u);
+    acc[0] = (acc[0] * fb + c.x) / fb1;
+    acc[1] = (acc[1] * fb + c.y) / fb1;
+    acc[2] = (acc[2] * fb + c.z) / fb1;
+    acc[3] = (acc[3] * fb + 1.0f) / fb1;
+  }
+  *dst = make_float4(acc[0], acc[1], acc[2], acc[3]);
+}
+
+__global__ __launch_bounds__(256) void fill_culled_kernel(RenderParams P) {
+  fill_culled(P, P.culled_items, P.n_culled_items, (int)blockIdx.x);
 }
 
 }  // namespace
@@ -1240,6 +1575,51 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool
     kern = lds_scene ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
                      : (stats ? render_kernel<true, false> : render_kernel<false, false>);
   if (grid > 0) hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), lds, stream, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds_scene, hipStream_t stream) {
+  if (p0.spl != 1 && p0.spl != 2 && p0.spl != 4 && p0.spl != 8) return hipErrorInvalidValue;
+  if (p0.n_batches == 0) return hipSuccess;
+  const int per = 256 / p0.spl;
+  const long long tiles = (long long)(p0.blocks_total + p0.nranks - 1 - p0.rank) / p0.nranks;
+  const long long items = p0.items ? p0.n_items : tiles * p0.spl;
+  if (p0.items && p0.n_culled_items > 0) {
+    const long long px = (long long)p0.n_culled_items * per;
+    fill_culled_kernel<<<(unsigned)((px + 256 * kPixPerFill - 1) / (256 * kPixPerFill)), 256, 0, stream>>>(p0);
+  }
+  if (items <= 0) return hipGetLastError();
+  const long long px = items * per;
+  if (px > b.cap || b.cap > 0x7fffffffll) return hipErrorInvalidValue;
+  const size_t lds = lds_scene ? scene_lds_bytes(p0) : 0;
+  if (lds > kMaxSceneLds) return hipErrorInvalidValue;
+  int dev = 0, cus = 0, per_cu_t = 0, per_cu_s = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  void (*trace)(RenderParams, WfBuffers, int) = lds_scene ? wf_trace_kernel<true> : wf_trace_kernel<false>;
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, trace, 256, lds);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, wf_shade_kernel, 256, 0);
+  if (e != hipSuccess) return e;
+  const unsigned grid_t = (unsigned)(cus * (per_cu_t > 0 ? per_cu_t : 1));
+  const unsigned grid_s = (unsigned)(cus * (per_cu_s > 0 ? per_cu_s : 1));
+  const uint32_t chunk = (uint32_t)std::min<long long>((long long)p0.n_batches, b.cap / px);
+  const int iters = wf_max_rays(p0);
+  for (uint32_t b0 = 0; b0 < p0.n_batches; b0 += chunk) {
+    RenderParams p = p0;
+    p.first_batch = p0.first_batch + b0;
+    p.n_batches = std::min(chunk, p0.n_batches - b0);
+    const long long n = px * p.n_batches;
+    e = hipMemsetAsync(b.counters, 0, 3 * sizeof(int), stream);
+    if (e != hipSuccess) return e;
+    wf_gen_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(p, b, n);
+    int cur = 0;
+    for (int it = 0; it < iters; ++it) {
+      hipLaunchKernelGGL(trace, dim3(grid_t), dim3(256), lds, stream, p, b, cur);
+      wf_shade_kernel<<<grid_s, 256, 0, stream>>>(p, b, cur);
+      cur ^= 1;
+    }
+    wf_fold_kernel<<<(unsigned)((px + 255) / 256), 256, 0, stream>>>(p, b, px);
+  }
   return hipGetLastError();
 }
 

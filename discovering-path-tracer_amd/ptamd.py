@@ -23,6 +23,8 @@ PT_OPT_FRESH_BATCH0 = 3
 PT_OPT_KERNEL = 4
 PT_OPT_SM_BATCH = 5
 PT_OPT_PRIMARY_CULL = 6
+PT_OPT_WF_PATHS = 7
+KERNEL_AUTO, KERNEL_RECURSIVE, KERNEL_STATE_MACHINE, KERNEL_WAVEFRONT = 0, 1, 2, 3
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).
 EXPORTS = [

@@ -190,7 +190,10 @@ int pt_items_unpack_all(pt_context* ctx, const void* src_device, size_t slot_flo
  * 0 (default) = read the accumulator, as the reference does (prev * 0). */
 #define PT_OPT_FRESH_BATCH0 3
 /* PT_OPT_KERNEL: 0 auto (path-recursive), 1 path-recursive, 2 lane state
- * machine (slower on every scene measured; kept for comparison).
+ * machine (slower on every scene measured; kept for comparison), 3 wavefront
+ * pipeline (paths held in device memory, traversal and shading in separate
+ * kernels; ~224 bytes of device memory per pixel x sample, at most 2^24 paths
+ * per chunk; not with stats mode).  Output is identical for every value.
  * PT_OPT_SM_BATCH: state machine only — finished rays wait until this many
  * lanes of the wave need shading (1..64, default 1).  Output is identical. */
 #define PT_OPT_KERNEL 4
@@ -200,8 +203,13 @@ int pt_items_unpack_all(pt_context* ctx, const void* src_device, size_t slot_flo
  * pt_primary_cull_rects' rectangles) is not ray-generated: each of its samples
  * is (0,0,0) exactly as the reference computes it (pre-pass misses, depth-0
  * traceRay misses, background 0).  0 = generate and trace every sample.
- * Path-recursive kernel only; output is identical either way. */
+ * Path-recursive and wavefront kernels; output is identical either way. */
 #define PT_OPT_PRIMARY_CULL 6
+/* PT_OPT_WF_PATHS: wavefront kernel only — paths (pixel x sample) held in
+ * device memory per chunk; 0 = 2^24 (3.8 GB).  A launch with more runs in
+ * chunks of whole batches (at least one batch of the frame per chunk).
+ * Output is identical for every value. */
+#define PT_OPT_WF_PATHS 7
 int pt_set_option(pt_context* ctx, int key, int value);
 
 /* Screen regions that primary rays can reach the scene or a light from.

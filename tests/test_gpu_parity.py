@@ -415,3 +415,81 @@ def test_sparse_item_exchange_assembles_frame(nranks, cam):
         assert sum(counts) * per >= W * H
     else:
         assert sum(counts) * per < W * H          # culled items are not shipped
+
+
+# ---- wavefront pipeline (PT_OPT_KERNEL 3) ----------------------------------
+
+@pytest.mark.parametrize("lds,spl", [(0, 1), (2, 4), (0, 8)])
+def test_wavefront_kernel_box(lds, spl):
+    v, i, n = _box()
+    r = _setup(v, i, n, lds=lds)
+    r.set_option(ptamd.PT_OPT_KERNEL, ptamd.KERNEL_WAVEFRONT)
+    r.set_option(ptamd.PT_OPT_SAMPLE_LANES, spl)
+    r.resize_and_clear(70, 45)
+    r.render(1, 5)
+    ref, _ = _oracle(v, i, n, 70, 45, first=1, nb=5)
+    _assert_same(r.read_accum(), ref, f"wavefront box lds={lds} spl={spl}")
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_wavefront_kernel_scenes(case):
+    name, sv, si, cam, lights, depth, sss = _sm_cases()[case]
+    s = ptamd.Scene.from_arrays(sv, si).build_bvh()
+    v, i, n, _, _ = s.arrays()
+    r = _setup(v, i, n, cam=cam, lights=lights, depth=depth, sss=sss, lds=0)
+    r.set_option(ptamd.PT_OPT_KERNEL, ptamd.KERNEL_WAVEFRONT)
+    r.resize_and_clear(56, 40)
+    r.render(0, 3)
+    ref, _ = _oracle(v, i, n, 56, 40, nb=3, depth=depth, sss=sss, cam=cam, lights=lights)
+    _assert_same(r.read_accum(), ref, f"wavefront {name}")
+
+
+@pytest.mark.parametrize("paths", [1, 3000, 7000])
+def test_wavefront_batch_chunks(paths):
+    """Launches larger than PT_OPT_WF_PATHS run in chunks of whole batches
+    (1 = one batch per chunk): same frame, over a stale accumulator too."""
+    v, i, n = _box()
+    W, H = 50, 41
+    camA, camB = CULL_CAMS[1], CULL_CAMS[0]
+    ref, _ = _oracle(v, i, n, W, H, first=0, nb=3, cam=camA)
+    ref, _ = _oracle(v, i, n, W, H, first=3, nb=7, cam=camB, accum=ref)
+    r = _setup(v, i, n, cam=camA)
+    r.set_option(ptamd.PT_OPT_KERNEL, ptamd.KERNEL_WAVEFRONT)
+    r.set_option(ptamd.PT_OPT_WF_PATHS, paths)
+    r.resize_and_clear(W, H)
+    r.render(0, 3)
+    r.set_camera(camB)
+    r.render(3, 7)
+    _assert_same(r.read_accum(), ref, f"wavefront chunks of {paths} paths")
+
+
+@pytest.mark.parametrize("cam", range(len(CULL_CAMS)))
+def test_wavefront_culling_and_partition(cam):
+    """Culling (compact items + fill) and a tile partition under the wavefront
+    kernel: every rank's owned pixels equal the oracle's."""
+    v, i, n = _box()
+    W, H = 96, 54
+    ref, _ = _oracle(v, i, n, W, H, nb=4, cam=CULL_CAMS[cam])
+    ref = ref.reshape(H, W, 4)
+    bx = (W + 15) // 16
+    yy, xx = np.mgrid[0:H, 0:W]
+    tile = (yy // 16) * bx + xx // 16
+    for nranks, rank in [(1, 0), (3, 2)]:
+        r = _setup(v, i, n, cam=CULL_CAMS[cam])
+        r.set_option(ptamd.PT_OPT_KERNEL, ptamd.KERNEL_WAVEFRONT)
+        r.set_partition(nranks, rank)
+        r.resize_and_clear(W, H)
+        r.render(0, 4)
+        got = r.read_accum().reshape(H, W, 4)
+        own = tile % nranks == rank
+        _assert_same(got[own].reshape(-1), ref[own].reshape(-1), f"wavefront cam {cam} rank {rank}/{nranks}")
+
+
+def test_wavefront_rejects_stats_mode():
+    v, i, n = _box()
+    r = _setup(v, i, n)
+    r.set_option(ptamd.PT_OPT_KERNEL, ptamd.KERNEL_WAVEFRONT)
+    r.set_stats_mode(True)
+    r.resize_and_clear(16, 16)
+    with pytest.raises(ptamd.PTError):
+        r.render(0, 1)
