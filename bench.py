@@ -102,6 +102,10 @@ def cpu_baseline(v, i, n, cam, light, W, H, spp, DEPTH, SSS):
                       f"{int(st[0])} rays, {dt:.2f} s, {threads} std::threads, oracle/pt_oracle.cpp)"}
 
 
+KERNEL_NAMES = {1: "render_kernel<false,*>", 2: "render_sm_kernel<false,*>",
+                3: "wavefront pipeline (wf_gen + wf_trace/wf_shade x rays + wf_fold), per frame"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -344,7 +348,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": None if prof is None else int(prof[1]),
                          "traffic_source": None if prof is None else prof[0],
-                         "kernel": "render_kernel<false,*>", "kernel_ms": round(kernel_ms, 4),
+                         "kernel": KERNEL_NAMES.get(r.last_kernel(), "?"), "kernel_ms": round(kernel_ms, 4),
                          "algorithmic_bytes_per_launch": int(own_bytes)},
         }
         if prof is not None and prof[2]:

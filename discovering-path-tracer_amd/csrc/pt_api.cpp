@@ -307,6 +307,7 @@ struct pt_context {
   int opt_sm_batch = 1;       // PT_OPT_SM_BATCH
   int opt_cull = 1;           // PT_OPT_PRIMARY_CULL
   int opt_wf_paths = 0;       // PT_OPT_WF_PATHS (0 = 2^24)
+  int last_kernel = 0;        // kernel of the last render (1 recursive, 2 state machine, 3 wavefront)
   // compact-launch item lists (live items, then culled ones), rebuilt when
   // the frame, partition, sample lanes or cull rectangles change
   int* d_items = nullptr;
@@ -436,6 +437,7 @@ int upload_ints(const std::vector<int>& h, int** d, size_t* cap) {
 // Wavefront buffers for `paths` paths in one allocation.  Up to 2^24 paths
 // (4.3 GB) are kept per launch; more batches run in chunks of that size.
 constexpr long long kWfMaxPaths = 1ll << 24;
+constexpr int kWfAutoTris = 32768;
 int wf_reserve(pt_context* c, long long pixels, uint32_t batches, long long* chunk_paths) {
   const long long limit = c->opt_wf_paths > 0 ? c->opt_wf_paths : kWfMaxPaths;
   const long long want = std::max(pixels, std::min(pixels * (long long)batches, limit));
@@ -772,7 +774,12 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
   // option; it was measured slower on every scene (1080p: displaced sphere
   // 8 spp 1022 vs 596 ms, 1M-triangle cloud 1 spp 191 vs 127 ms).
   const bool sm = c->opt_kernel == 2;
-  const bool wf = c->opt_kernel == 3;
+  // auto: the wavefront pipeline for scenes of at least kWfAutoTris triangles
+  // (not LDS-resident), the path-recursive kernel otherwise.  Measured at
+  // 1080p 8 spp (ms, recursive -> wavefront): displaced sphere 5K tris
+  // 39.5 -> 58.4, 20K 67 -> 72, 82K 560 -> 465; random cloud 100K 130 -> 76,
+  // 1M 923 -> 833; 10M (1 spp) 719 -> 667; box 0.38 -> 8.4.
+  const bool wf = c->opt_kernel == 3 || (c->opt_kernel == 0 && !lds && !c->stats_mode && c->n_tris >= kWfAutoTris);
   if (wf && c->stats_mode) return fail(PT_ERR_UNSUPPORTED, "stats mode runs the path-recursive kernel only");
   if (sm) p.spl = 1;
   p.n_cull = -1;
@@ -787,6 +794,7 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
     if (rc) return rc;
   }
   c->last = p;   // the item exchange (pt_items_*) follows the last rendered frame
+  c->last_kernel = wf ? 3 : sm ? 2 : 1;
   c->last_valid = !sm;
   if (wf) {
     const long long tiles = (p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;
@@ -892,6 +900,12 @@ int pt_readback_end(pt_context* c, int ticket, float* rgba, size_t n) {
     return PT_OK;
   }
   return fail(PT_ERR_INVALID, "unknown or already collected readback ticket " + std::to_string(ticket));
+}
+
+int pt_last_kernel(pt_context* c, int* kernel) {
+  if (!c || !kernel) return fail(PT_ERR_INVALID, "null argument");
+  *kernel = c->last_kernel;
+  return PT_OK;
 }
 
 int pt_set_option(pt_context* c, int key, int value) {

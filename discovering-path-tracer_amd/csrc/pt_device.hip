@@ -1353,14 +1353,25 @@ __device__ __forceinline__ bool wf_lane_step(const RenderParams& P, WfLane& L, i
   return false;
 }
 
-// Persistent traversal over list `cur`: lanes pull path ids (one atomic per
+// Persistent traversal over list `cur`: lanes pull list slots (one atomic per
 // wave) and refill once at least PT_WF_REFILL lanes are idle.
 #ifndef PT_WF_STEPS
 #define PT_WF_STEPS 8
 #endif
 #ifndef PT_WF_REFILL
-#define PT_WF_REFILL 1
+#define PT_WF_REFILL 16
 #endif
+#ifndef PT_WF_GROUP
+#define PT_WF_GROUP 4
+#endif
+static_assert(PT_WF_GROUP == 1 || PT_WF_GROUP == 2 || PT_WF_GROUP == 4 || PT_WF_GROUP == 8 || PT_WF_GROUP == 16,
+              "refill group: power of two");
+constexpr unsigned long long kGroupLead =
+    PT_WF_GROUP == 1   ? ~0ull
+    : PT_WF_GROUP == 2 ? 0x5555555555555555ull
+    : PT_WF_GROUP == 4 ? 0x1111111111111111ull
+    : PT_WF_GROUP == 8 ? 0x0101010101010101ull
+                       : 0x0001000100010001ull;
 #ifndef PT_WF_MIN_BLOCKS
 #define PT_WF_MIN_BLOCKS 6
 #endif
@@ -1398,14 +1409,22 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
   WfLane L;
   for (;;) {
     const unsigned long long idle = __ballot(p < 0);
-    if (more && (int)__popcll(idle) >= PT_WF_REFILL) {
-      const int n = (int)__popcll(idle);
+    // groups of PT_WF_GROUP lanes refill together with consecutive list
+    // slots (neighbouring paths: the same pixel's samples), so their walks
+    // stay as coherent as the path-recursive kernel's sample lanes
+    unsigned long long gm = idle;
+#pragma unroll
+    for (int sh = 1; sh < PT_WF_GROUP; sh <<= 1) gm &= gm >> sh;
+    gm &= kGroupLead;
+    const int ng = (int)__popcll(gm);
+    if (more && ng * PT_WF_GROUP >= PT_WF_REFILL) {
       int base = 0;
-      if (lane == 0) base = atomicAdd(&B.counters[2], n);
+      if (lane == 0) base = atomicAdd(&B.counters[2], ng * PT_WF_GROUP);
       base = __shfl(base, 0);
-      if (base + n >= count) more = false;
-      if (p < 0) {
-        const int slot = base + (int)__popcll(idle & ((1ull << lane) - 1ull));
+      if (base + ng * PT_WF_GROUP >= count) more = false;
+      const int lead = lane & ~(PT_WF_GROUP - 1);
+      if ((gm >> lead) & 1ull) {
+        const int slot = base + (int)__popcll(gm & ((1ull << lead) - 1ull)) * PT_WF_GROUP + (lane - lead);
         if (slot < count) {
           p = slot;
           wf_lane_start(rays + 2 * (size_t)slot, root_a, root_b, L);

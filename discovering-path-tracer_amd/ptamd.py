@@ -31,7 +31,7 @@ EXPORTS = [
     "pt_abi_version", "pt_last_error", "pt_create", "pt_destroy", "pt_set_stream", "pt_synchronize",
     "pt_upload_scene", "pt_upload_lights", "pt_set_camera", "pt_set_params", "pt_resize_and_clear",
     "pt_bind_accum", "pt_clear_accum", "pt_accum_device_ptr", "pt_read_accum", "pt_dispatch", "pt_render",
-    "pt_set_partition", "pt_tiles_owned", "pt_tiles_pack", "pt_tiles_unpack", "pt_set_option", "pt_set_stats_mode", "pt_get_stats", "pt_reset_stats", "pt_last_launch_ms",
+    "pt_set_partition", "pt_tiles_owned", "pt_tiles_pack", "pt_tiles_unpack", "pt_set_option", "pt_last_kernel", "pt_set_stats_mode", "pt_get_stats", "pt_reset_stats", "pt_last_launch_ms",
     "pt_launch_times_ms", "pt_reset_launch_times", "pt_selftest_math", "pt_selftest_exhaustive",
     "pt_scene_load_obj", "pt_scene_parse_obj", "pt_scene_from_arrays", "pt_scene_build_bvh",
     "pt_scene_counts", "pt_scene_copy", "pt_scene_upload", "pt_scene_free", "pt_pack_light",
@@ -77,7 +77,7 @@ def lib():
             "pt_clear_accum": ([vp], i32), "pt_accum_device_ptr": ([vp], vp),
             "pt_read_accum": ([vp, vp, sz], i32), "pt_dispatch": ([vp, u32], i32),
             "pt_render": ([vp, u32, u32], i32), "pt_set_partition": ([vp, i32, i32], i32),
-            "pt_set_stats_mode": ([vp, i32], i32), "pt_set_option": ([vp, i32, i32], i32),
+            "pt_set_stats_mode": ([vp, i32], i32), "pt_set_option": ([vp, i32, i32], i32), "pt_last_kernel": ([vp, ctypes.POINTER(ctypes.c_int)], i32),
             "pt_tiles_owned": ([vp, ctypes.POINTER(i32)], i32), "pt_tiles_pack": ([vp, vp], i32),
             "pt_tiles_unpack": ([vp, vp, i32, vp], i32), "pt_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
             "pt_reset_stats": ([vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
@@ -347,6 +347,12 @@ class Renderer:
 
     def set_option(self, key, value):
         _check(lib().pt_set_option(self._c, key, value), "pt_set_option")
+
+    def last_kernel(self):
+        """Kernel of the last render: KERNEL_RECURSIVE, KERNEL_STATE_MACHINE or KERNEL_WAVEFRONT."""
+        k = ctypes.c_int(0)
+        _check(lib().pt_last_kernel(self._c, ctypes.byref(k)), "pt_last_kernel")
+        return k.value
 
     def set_stream(self, stream_handle):
         _check(lib().pt_set_stream(self._c, stream_handle), "pt_set_stream")

@@ -189,7 +189,8 @@ int pt_items_unpack_all(pt_context* ctx, const void* src_device, size_t slot_flo
  * pt_clear_accum + pt_render give, minus a clear and a read of the image.
  * 0 (default) = read the accumulator, as the reference does (prev * 0). */
 #define PT_OPT_FRESH_BATCH0 3
-/* PT_OPT_KERNEL: 0 auto (path-recursive), 1 path-recursive, 2 lane state
+/* PT_OPT_KERNEL: 0 auto (wavefront for scenes of >= 32768 triangles that
+ * are not LDS-resident, else path-recursive), 1 path-recursive, 2 lane state
  * machine (slower on every scene measured; kept for comparison), 3 wavefront
  * pipeline (paths held in device memory, traversal and shading in separate
  * kernels; ~224 bytes of device memory per pixel x sample, at most 2^24 paths
@@ -211,6 +212,9 @@ int pt_items_unpack_all(pt_context* ctx, const void* src_device, size_t slot_flo
  * Output is identical for every value. */
 #define PT_OPT_WF_PATHS 7
 int pt_set_option(pt_context* ctx, int key, int value);
+/* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
+ * after auto selection); 0 before the first render. */
+int pt_last_kernel(pt_context* ctx, int* kernel);
 
 /* Screen regions that primary rays can reach the scene or a light from.
  * Writes up to max_rects NDC rectangles {x0, x1, y0, y1} (one per object:

@@ -233,7 +233,7 @@ def test_tile_gather_assembles_frame(nranks):
     _assert_same(frame.cpu().numpy().reshape(-1), ref, f"gather over {nranks}")
 
 
-@pytest.mark.parametrize("ntri,int_bits", [(1, False), (2, False), (1000, False), (20000, True)])
+@pytest.mark.parametrize("ntri,int_bits", [(1, False), (2, False), (1000, False), (20000, True), (40000, False)])
 def test_random_triangles(ntri, int_bits):
     tv, ti = scenes.random_triangles(ntri, seed=ntri)
     s = ptamd.Scene.from_arrays(tv, ti).build_bvh(int_bits=int_bits)
