@@ -106,6 +106,21 @@ KERNEL_NAMES = {1: "render_kernel<false,*>", 2: "render_sm_kernel<false,*>",
                 3: "wavefront pipeline (wf_gen + wf_trace/wf_shade x rays + wf_fold), per frame"}
 
 
+class _StreamWork:
+    """Stand-in for an async collective's Work in the rank emulation: wait()
+    orders the caller's current stream after what `stream` had queued when
+    the work was issued (as ProcessGroupNCCL's Work.wait does)."""
+
+    def __init__(self, stream):
+        import torch
+        self.ev = torch.cuda.Event()
+        self.ev.record(stream)
+
+    def wait(self):
+        import torch
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,6 +135,11 @@ def main():
     ap.add_argument("--collective", choices=["gather", "reduce"], default="gather")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", action="store_true", help="N>1: compare the assembled frame with a 1-GPU render")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VAL",
+                    help="pt_set_option before timing (A/B of output-invariant kernel options)")
+    ap.add_argument("--assemble", type=int, choices=[0, 1, 2], default=2,
+                    help="N>1 gather: 2 = render_packed assembling frame k-2 in frame k's launch, "
+                         "1 = render_packed + assembly launch, 0 = render + pack + assembly launches")
     ap.add_argument("--compare-no-cull", action="store_true",
                     help="N=1: also time the same steps with primary-ray culling off (reported as primary_cull_off)")
     args = ap.parse_args()
@@ -131,6 +151,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # PT_BENCH_EMULATE_RANKS=N (1-GPU box only): rank 0's step of an N-GPU
+    # gather run -- its tile share, pack, the root's unpack of N slots -- with
+    # the collective replaced by a device copy of its own slot.  A rehearsal of
+    # the root's critical path, never a multi-GPU result (the line says so).
+    emu = int(os.environ.get("PT_BENCH_EMULATE_RANKS", "1"))
+    if emu > 1 and world != 1:
+        raise SystemExit("PT_BENCH_EMULATE_RANKS needs a 1-process run")
+    if emu > 1 and (args.collective != "gather" or args.verify):
+        raise SystemExit("PT_BENCH_EMULATE_RANKS rehearses the gather path without --verify")
     # Rehearsal knobs for a 1-GPU box: every rank on one device, gloo staged on the host.
     device = int(os.environ.get("PT_BENCH_DEVICE", local))
     backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
@@ -165,7 +194,10 @@ def main():
     r.upload_lights(light)
     r.set_camera(cam)
     r.set_params(DEPTH, SSS)
-    r.set_partition(world, rank)
+    r.set_partition(max(world, emu), rank)
+    for kv in args.opt:
+        k, _, val = kv.partition("=")
+        r.set_option(int(k), int(val))
     # One explicit stream for the renderer and every torch op/collective: the
     # legacy default stream has handle 0, which pt_set_stream reads as "the
     # context's own stream", so it cannot be shared by handle.
@@ -197,7 +229,8 @@ def main():
     r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
     pending = []
     finish = None
-    if dist is None:
+    nparts = max(world, emu)
+    if dist is None and emu == 1:
         def step():
             r.render(0, SPP)
     elif args.collective == "reduce":
@@ -219,39 +252,62 @@ def main():
         # Sparse gather: each rank ships only its live items (tile parts that
         # can hold a live pixel under primary culling); the root rebuilds the
         # culled ones.  Every rank derives every rank's item count itself.
+        # --assemble 2 (default): frame k's render launch (pt_render_packed)
+        # also assembles frame k-2 on the root, whose gather ran during frame
+        # k-1's render -- one launch per step; 1: render_packed, then a
+        # separate assembly launch; 0: render + pack + assembly launches.
         r.render(0, SPP)
         per = r.items_live(0)[1]
-        slot = max(r.items_live(k)[0] for k in range(world)) * per * 4
+        slot = max(r.items_live(k)[0] for k in range(nparts)) * per * 4
         slot = max(slot, 4)
+        root = rank == 0
         send = [torch.zeros(slot, dtype=torch.float32, device=dev) for _ in range(2)]
-        recv_all = [torch.empty((world, slot), dtype=torch.float32, device=dev) for _ in range(2)] if rank == 0 else None
-        recv = [[recv_all[b][k] for k in range(world)] for b in range(2)] if rank == 0 else None
-        out = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if rank == 0 else None
+        recv_all = [torch.zeros((nparts, slot), dtype=torch.float32, device=dev) for _ in range(2)] if root else None
+        recv = [[recv_all[b][k] for k in range(nparts)] for b in range(2)] if root else None
+        out = torch.empty((H, W, 4), dtype=torch.float32, device=dev) if root else None
         state = {"k": 0}
+        depth = 2 if args.assemble == 2 else 1   # frames in flight before assembly
 
-        def finish(work, buf):
+        def finish(work, buf):   # separate assembly launch of one gathered frame
             if work is not None:
                 work.wait()
-            if rank == 0:
+            if root:
                 r.items_unpack_all(recv_all[buf].data_ptr(), slot, out.data_ptr())
 
         def step():
             buf = state["k"] % 2
             state["k"] += 1
-            r.render(0, SPP)
-            r.items_pack(send[buf].data_ptr())
-            if backend == "nccl":
-                work = dist.gather(send[buf], recv[buf] if rank == 0 else None, dst=0, async_op=True)
+            fused = None
+            if len(pending) >= depth:
+                work, pbuf = pending.pop(0)
+                if args.assemble == 2:
+                    if work is not None:
+                        work.wait()   # gather of frame k-2: finished during frame k-1
+                    if root:
+                        fused = (recv_all[pbuf].data_ptr(), slot, out.data_ptr())
+                else:
+                    finish(work, pbuf)
+            # emulation: the root's own slot is written in place, no transfer
+            dst = recv[buf][0] if dist is None else send[buf]
+            if args.assemble == 0:
+                r.render(0, SPP)
+                r.items_pack(dst.data_ptr())
+            elif fused is not None:
+                r.render_packed(SPP, dst.data_ptr(), *fused)
             else:
-                host = [torch.empty_like(x, device="cpu") for x in recv[buf]] if rank == 0 else None
+                r.render_packed(SPP, dst.data_ptr())
+            if dist is None:
+                work = _StreamWork(stream)
+            elif backend == "nccl":
+                work = dist.gather(send[buf], recv[buf] if root else None, dst=0, async_op=True)
+            else:
+                host = [torch.empty_like(x, device="cpu") for x in recv[buf]] if root else None
                 dist.gather(send[buf].cpu(), host, dst=0)
-                if rank == 0:
+                if root:
                     for x, h in zip(recv[buf], host):
                         x.copy_(h)
                 work = None
             pending.append((work, buf))
-            if len(pending) > 1:          # frame k-1 is assembled while frame k renders
-                finish(*pending.pop(0))
 
     def drain():
         while pending:
@@ -268,6 +324,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    t_enq = time.perf_counter() - t0   # host time to issue the steps (no sync inside)
     drain()
     r.synchronize()
     torch.cuda.synchronize(dev)
@@ -322,7 +379,7 @@ def main():
         own_bytes = algorithmic_bytes({"nodes": mine[1], "leaf_tests": mine[2], "samples": mine[3]})
         achieved = own_bytes / (kernel_ms * 1e-3) / 1e9
         default_cfg = args.scene == "box" and (W, H, SPP, DEPTH, SSS) == (1920, 1080, 8, 4, 3)
-        prof = profiled_traffic() if (world == 1 and default_cfg) else None
+        prof = profiled_traffic() if (world == 1 and emu == 1 and default_cfg) else None
         wl = f"{scene_desc} {W}x{H} {SPP}spp {DEPTH} bounces {SSS} sss"
         out_line = {
             "metric": "Mrays/s at 1920x1080x8spp, box.obj BVH" if default_cfg else f"Mrays/s, {wl}",
@@ -332,6 +389,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
+            "host_issue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -359,11 +417,15 @@ def main():
             out_line["roofline_valu"] = {"bound": "valu_issue", "achieved": round(gi, 2), "peak": VALU_PEAK_GINST,
                                          "unit": "G wave-instr/s", "frac": round(gi / VALU_PEAK_GINST, 4),
                                          "valu_wave_instr_per_launch": int(prof[2]), "source": prof[0]}
+        if emu > 1:
+            out_line["metric"] = f"EMULATED (1 GPU, not a multi-GPU result): rank 0 of {emu}, " + out_line["metric"]
+            out_line["emulated_ranks"] = emu
+            out_line["config"]["parallelism"] = f"emulated-tiles{emu}-sparse-gather"
         if no_cull is not None:
             out_line["primary_cull_off"] = no_cull
         if verified is not None:
             out_line["verified_bitwise_vs_single_gpu"] = verified
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and emu == 1 and not args.no_cpu_baseline:
             out_line["cpu_baseline"] = cpu_baseline(v, i, n, cam, light, W, H, SPP, DEPTH, SSS)
         print(json.dumps(out_line), flush=True)
     if dist is not None:

@@ -303,6 +303,7 @@ struct pt_context {
   int opt_scene_lds = 1;   // PT_OPT_SCENE_IN_LDS: 0 never, 1 auto, 2 always
   int opt_sample_lanes = 0;   // PT_OPT_SAMPLE_LANES: 0 auto, else 1/2/4/8
   int opt_fresh = 0;          // PT_OPT_FRESH_BATCH0
+  int opt_item_order = 1;     // PT_OPT_ITEM_ORDER
   int opt_kernel = 0;         // PT_OPT_KERNEL: 0 auto, 1 path-recursive, 2 lane state machine, 3 wavefront
   int opt_sm_batch = 1;       // PT_OPT_SM_BATCH
   int opt_cull = 1;           // PT_OPT_PRIMARY_CULL
@@ -326,9 +327,9 @@ struct pt_context {
   size_t unpack_cap = 0;
   int n_unpack = 0;
   std::vector<float> unpack_key;
+  std::vector<float> packed_key;   // frame parameters of the last pt_render_packed
   float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};   // root AABB of the uploaded tree
   std::vector<pt_area_light> lights_host;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // wavefront pipeline buffers (PT_OPT_KERNEL 3), grown on demand
   ptd::WfBuffers wf{};
   void* wf_block = nullptr;
@@ -352,6 +353,7 @@ struct pt_context {
   static constexpr int kRing = 512;
   hipEvent_t ring[kRing][2] = {};
   int ring_n = 0;
+  int last_slot = 0;          // ring slot of the newest launch (pt_last_launch_ms)
 };
 
 struct pt_scene {
@@ -367,30 +369,62 @@ struct pt_scene {
 // kernel, the rest to fill_culled_kernel.  A culled workgroup still costs a
 // workgroup launch (a fully culled 1080p frame took 0.10 ms at 4 sample
 // lanes), so only live ones are launched.
+// Pixels of columns [g0, g0+n) (or rows) whose NDC origin (the kernel's
+// ndc = 2*p/res - 1) lies in [lo, hi].
+static int pixels_in(int g0, int n, int res, float lo, float hi) {
+  int k = 0;
+  for (int i = 0; i < n; ++i) {
+    const float v = (2.0f * (float)(g0 + i) / (float)res) - 1.0f;
+    k += (v >= lo && v <= hi) ? 1 : 0;
+  }
+  return k;
+}
+
+// Live items are listed heaviest first (longest-processing-time order: the
+// hardware dispatches workgroups in list order, so the long ones start early
+// and the short ones fill the tail).  Weight = pixels inside the root box's
+// rectangle (cull[0]: full paths, ~9 rays per sample on box.obj) x 8 + pixels
+// inside a light rectangle (pre-pass only).  Output does not depend on the
+// order; every consumer (launch, pack, unpack table) uses this one list.
 static void item_lists(const ptd::RenderParams& p, int rank, std::vector<int>* live, std::vector<int>* culled) {
-  const int W = p.width, H = p.height, spl = p.spl;
+  const int W = p.width, H = p.height, spl = p.spl, rows = 16 / spl;
   const int tiles = (p.blocks_total + p.nranks - 1 - rank) / p.nranks;
   live->clear();
   culled->clear();
+  std::vector<std::pair<int, int>> weighted;   // (-weight, item)
   for (int li = 0; li < tiles; ++li) {
     const int b = li * p.nranks + rank;
     const int gx0 = (b % p.blocks_x) * 16;
     const float wx0 = (2.0f * (float)gx0 / (float)W) - 1.0f, wx1 = (2.0f * (float)(gx0 + 15) / (float)W) - 1.0f;
+    int cols[ptd::kMaxCullRects] = {};
+    for (int r = 0; r < p.n_cull; ++r) cols[r] = pixels_in(gx0, 16, W, p.cull[r][0], p.cull[r][1]);
     for (int part = 0; part < spl; ++part) {
-      const int gy0 = (b / p.blocks_x) * 16 + part * (16 / spl);
+      const int gy0 = (b / p.blocks_x) * 16 + part * rows;
       const float wy0 = (2.0f * (float)gy0 / (float)H) - 1.0f;
-      const float wy1 = (2.0f * (float)(gy0 + 16 / spl - 1) / (float)H) - 1.0f;
+      const float wy1 = (2.0f * (float)(gy0 + rows - 1) / (float)H) - 1.0f;
       bool any = p.n_cull < 0;   // no culling: every item is live
       for (int r = 0; r < p.n_cull && !any; ++r)
         any = wx1 >= p.cull[r][0] && wx0 <= p.cull[r][1] && wy1 >= p.cull[r][2] && wy0 <= p.cull[r][3];
-      (any ? live : culled)->push_back(li * spl + part);
+      if (!any) {
+        culled->push_back(li * spl + part);
+        continue;
+      }
+      int w = 0;
+      for (int r = 0; r < p.n_cull; ++r)
+        if (cols[r]) w += (r == 0 ? 8 : 1) * cols[r] * pixels_in(gy0, rows, H, p.cull[r][2], p.cull[r][3]);
+      weighted.push_back({-w, li * spl + part});
     }
   }
+  if (p.item_order)
+    std::stable_sort(weighted.begin(), weighted.end(),
+                   [](const std::pair<int, int>& a, const std::pair<int, int>& b) { return a.first < b.first; });
+  live->reserve(weighted.size());
+  for (const auto& e : weighted) live->push_back(e.second);
 }
 
 static int compact_items(pt_context* c, ptd::RenderParams* p) {
   std::vector<float> key = {(float)p->width, (float)p->height, (float)p->nranks, (float)p->rank, (float)p->spl,
-                            (float)p->n_cull};
+                            (float)p->n_cull, (float)p->item_order};
   for (int r = 0; r < p->n_cull; ++r) key.insert(key.end(), p->cull[r], p->cull[r] + 4);
   if (key.size() != c->items_key.size() || memcmp(key.data(), c->items_key.data(), key.size() * 4) != 0) {
     std::vector<int> live, culled;
@@ -420,7 +454,7 @@ static int compact_items(pt_context* c, ptd::RenderParams* p) {
 namespace {
 std::vector<float> frame_key(const ptd::RenderParams& p) {
   std::vector<float> key = {(float)p.width, (float)p.height, (float)p.nranks, (float)p.rank, (float)p.spl,
-                            (float)p.n_cull, (float)p.blocks_x, (float)p.blocks_total};
+                            (float)p.n_cull, (float)p.blocks_x, (float)p.blocks_total, (float)p.item_order};
   for (int r = 0; r < p.n_cull; ++r) key.insert(key.end(), p.cull[r], p.cull[r] + 4);
   return key;
 }
@@ -438,6 +472,24 @@ int upload_ints(const std::vector<int>& h, int** d, size_t* cap) {
 // (4.3 GB) are kept per launch; more batches run in chunks of that size.
 constexpr long long kWfMaxPaths = 1ll << 24;
 constexpr int kWfAutoTris = 32768;
+// The root's assembly table for frames rendered with params p: per rank its
+// live items {rank, item, slot} and its culled items {rank, item, -1}.
+int unpack_table(pt_context* c, const ptd::RenderParams& p) {
+  const std::vector<float> key = frame_key(p);
+  if (key == c->unpack_key) return PT_OK;
+  std::vector<int> table, live, culled;
+  for (int r = 0; r < p.nranks; ++r) {
+    item_lists(p, r, &live, &culled);
+    for (size_t i = 0; i < live.size(); ++i) table.insert(table.end(), {r, live[i], (int)i});
+    for (int it : culled) table.insert(table.end(), {r, it, -1});
+  }
+  PT_HIP(hipStreamSynchronize(c->stream));
+  const int rc = upload_ints(table, &c->d_unpack, &c->unpack_cap);
+  if (rc) return rc;
+  c->n_unpack = (int)(table.size() / 3);
+  c->unpack_key = key;
+  return PT_OK;
+}
 int wf_reserve(pt_context* c, long long pixels, uint32_t batches, long long* chunk_paths) {
   const long long limit = c->opt_wf_paths > 0 ? c->opt_wf_paths : kWfMaxPaths;
   const long long want = std::max(pixels, std::min(pixels * (long long)batches, limit));
@@ -466,6 +518,168 @@ int wf_reserve(pt_context* c, long long pixels, uint32_t batches, long long* chu
 }
 }  // namespace
 
+extern "C" int pt_items_pack(pt_context* c, void* dst);
+extern "C" int pt_items_unpack_all(pt_context* c, const void* src, size_t slot_floats, void* frame);
+
+namespace {
+// pt_render / pt_render_packed (pack_out != null: fresh frame, live items
+// written to pack_out in the pt_items_pack layout).
+struct Assembly {   // pt_render_packed's optional gathered frame to assemble
+  const void* src = nullptr;
+  size_t slot_floats = 0;
+  void* frame = nullptr;
+};
+int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4* pack_out,
+                const Assembly& as = Assembly()) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  if (!c->has_scene) return fail(PT_ERR_INVALID, "no scene uploaded");
+  if (!c->has_camera) return fail(PT_ERR_INVALID, "no camera set");
+  if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
+  ptd::RenderParams p;
+  p.nodes = c->stats_mode ? c->d_nodes_full : c->d_nodes;
+  p.tris = c->d_tris;
+  p.lights = c->d_lights_dev;
+  p.accum = c->d_accum;
+  p.stats = c->d_stats;
+  p.n_nodes = c->stats_mode ? c->n_nodes_full : c->n_nodes;
+  p.n_tris = c->n_tris;
+  p.n_lights = c->n_lights;
+  p.width = c->width;
+  p.height = c->height;
+  p.first_batch = first_batch;
+  p.n_batches = n_batches;
+  p.max_depth = c->params.max_depth;
+  p.sss_bounces = c->params.sss_bounces;
+  for (int i = 0; i < 3; ++i) {
+    p.cam_pos[i] = c->cam[i];
+    p.cam_dir[i] = c->cam[4 + i];
+    p.cam_up[i] = c->cam[8 + i];
+  }
+  p.fov = c->cam[12];
+  {
+    using namespace ptm;
+    const v3 cdir = mk(p.cam_dir[0], p.cam_dir[1], p.cam_dir[2]);
+    const v3 cup = mk(p.cam_up[0], p.cam_up[1], p.cam_up[2]);
+    const v3 right = normalize(cross(cdir, neg(cup)));
+    const v3 up = normalize(cross(right, cdir));
+    p.cam_right[0] = right.x; p.cam_right[1] = right.y; p.cam_right[2] = right.z;
+    p.cam_upv[0] = up.x; p.cam_upv[1] = up.y; p.cam_upv[2] = up.z;
+    p.tan_fov = tan_(radians_(p.fov * 0.5f));
+  }
+  p.blocks_x = (c->width + 15) / 16;
+  p.blocks_total = p.blocks_x * ((c->height + 15) / 16);
+  p.nranks = c->nranks;
+  p.rank = c->rank;
+  p.fresh = pack_out ? 1 : c->opt_fresh;
+  p.item_order = c->opt_item_order;
+  p.pack_out = nullptr;
+  p.sm_batch = c->opt_sm_batch;
+  if (c->opt_sample_lanes) {
+    p.spl = c->opt_sample_lanes;
+  } else {
+    // auto: 4 sample lanes per pixel for an LDS-resident scene on a whole
+    // frame, else 8 — on a share of the frame each GPU's share shrinks while
+    // its heaviest workgroup does not, and on big scenes the samples of one
+    // pixel walk nearly the same nodes, so their loads coalesce.  Measured
+    // at 1080p 8spp with culling and compact launch: box spl 1/2/4/8 =
+    // 0.499/0.408/0.375/0.416 ms (whole frame), 0.354/0.264/0.225/0.221
+    // (1/2), 0.271/0.156/0.094/0.085 (1/8); displaced sphere 828/645/582/563;
+    // 1M cloud 968/930/927/923.  Never more lanes than samples.
+    const bool small = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
+    int want = (c->nranks >= 2 || !small) ? 8 : 4;
+    while (want > 1 && (uint32_t)want > n_batches) want >>= 1;
+    p.spl = want;
+  }
+  PT_HIP(hipSetDevice(c->device));
+  const int slot = c->ring_n % pt_context::kRing;
+  PT_HIP(hipEventRecord(c->ring[slot][0], c->stream));
+  const bool fits = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
+  if (c->opt_scene_lds == 2 && !fits) return fail(PT_ERR_UNSUPPORTED, "scene too large for the LDS variant");
+  const bool lds = c->opt_scene_lds == 2 || (c->opt_scene_lds == 1 && fits);
+  // auto: the path-recursive kernel.  The lane state machine is kept as an
+  // option; it was measured slower on every scene (1080p: displaced sphere
+  // 8 spp 1022 vs 596 ms, 1M-triangle cloud 1 spp 191 vs 127 ms).
+  const bool sm = c->opt_kernel == 2;
+  // auto: the wavefront pipeline for scenes of at least kWfAutoTris triangles
+  // (not LDS-resident), the path-recursive kernel otherwise.  Measured at
+  // 1080p 8 spp (ms, recursive -> wavefront): displaced sphere 5K tris
+  // 39.5 -> 58.4, 20K 67 -> 72, 82K 560 -> 465; random cloud 100K 130 -> 76,
+  // 1M 923 -> 833; 10M (1 spp) 719 -> 667; box 0.38 -> 8.4.
+  const bool wf = c->opt_kernel == 3 || (c->opt_kernel == 0 && !lds && !c->stats_mode && c->n_tris >= kWfAutoTris);
+  if (wf && c->stats_mode) return fail(PT_ERR_UNSUPPORTED, "stats mode runs the path-recursive kernel only");
+  if (sm) p.spl = 1;
+  p.n_cull = -1;
+  p.items = nullptr;
+  p.culled_items = nullptr;
+  p.n_items = p.n_culled_items = 0;
+  if (c->opt_cull && !c->stats_mode && !sm)
+    p.n_cull = cull_rects(c->cam, c->width, c->height, c->root_lo, c->root_hi, c->lights_host.data(),
+                          c->n_lights, &p.cull[0][0], ptd::kMaxCullRects);
+  if (p.n_cull >= 0) {
+    const int rc = compact_items(c, &p);
+    if (rc) return rc;
+  }
+  c->last = p;   // the item exchange (pt_items_*) follows the last rendered frame
+  c->last_kernel = wf ? 3 : sm ? 2 : 1;
+  c->last_valid = !sm;
+  p.unpack_src = nullptr;
+  p.unpack_frame = nullptr;
+  p.unpack_table = nullptr;
+  p.n_unpack = 0;
+  p.unpack_slot_f4 = 0;
+  if (pack_out) {
+    const std::vector<float> key = frame_key(p);
+    if (as.src && key != c->packed_key)
+      return fail(PT_ERR_INVALID, "pt_render_packed: the frame to assemble has another item layout (size, partition, lanes, culling)");
+    if (wf || sm) {
+      // these kernels render into the accumulation buffer: render, pack,
+      // then assemble the previous frame in a launch of its own
+      if (as.src) {
+        const int rc = pt_items_unpack_all(c, as.src, as.slot_floats, as.frame);
+        if (rc) return rc;
+      }
+      const int fresh = c->opt_fresh;
+      c->opt_fresh = 1;
+      const int rc = render_impl(c, 0, n_batches, nullptr);
+      c->opt_fresh = fresh;
+      if (rc) return rc;
+      c->packed_key = key;
+      return pt_items_pack(c, pack_out);
+    }
+    if (as.src) {
+      const int rc = unpack_table(c, p);
+      if (rc) return rc;
+      p.unpack_src = (const float4*)as.src;
+      p.unpack_frame = (float4*)as.frame;
+      p.unpack_table = c->d_unpack;
+      p.n_unpack = c->n_unpack;
+      p.unpack_slot_f4 = (long long)(as.slot_floats / 4);
+    }
+    if (!p.items) p.n_items = (int)(((p.blocks_total + p.nranks - 1 - p.rank) / p.nranks) * p.spl);
+    c->packed_key = key;
+  }
+  p.pack_out = pack_out;
+  if (wf) {
+    const long long tiles = (p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;
+    const long long items = p.items ? p.n_items : tiles * p.spl;
+    long long chunk_paths = 0;
+    const int rc = wf_reserve(c, items * (256 / p.spl), n_batches, &chunk_paths);
+    if (rc) return rc;
+    ptd::WfBuffers b = c->wf;
+    b.cap = chunk_paths;   // paths per chunk (the allocation may be larger)
+    PT_HIP(ptd::launch_wavefront(p, b, lds, c->stream));
+  } else {
+    PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream));
+  }
+  PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
+  c->last_slot = slot;
+  c->ring_n++;
+  c->timed = true;
+  return PT_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int pt_abi_version(void) { return PT_ABI_VERSION; }
@@ -489,8 +703,6 @@ int pt_create(int device_ordinal, pt_context** out) {
   hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, 4 * sizeof(unsigned long long));
   if (e == hipSuccess) e = hipMemset(c->d_stats, 0, 4 * sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipEventCreate(&c->ev0);
-  if (e == hipSuccess) e = hipEventCreate(&c->ev1);
   for (int i = 0; i < pt_context::kRing && e == hipSuccess; ++i) {
     e = hipEventCreate(&c->ring[i][0]);
     if (e == hipSuccess) e = hipEventCreate(&c->ring[i][1]);
@@ -526,8 +738,6 @@ int pt_destroy(pt_context* c) {
     if (r.done) (void)hipEventDestroy(r.done);
   }
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
-  if (c->ev0) (void)hipEventDestroy(c->ev0);
-  if (c->ev1) (void)hipEventDestroy(c->ev1);
   for (int i = 0; i < pt_context::kRing; ++i)
     for (int j = 0; j < 2; ++j)
       if (c->ring[i][j]) (void)hipEventDestroy(c->ring[i][j]);
@@ -706,113 +916,28 @@ int pt_read_accum(pt_context* c, float* rgba, size_t n) {
 }
 
 int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
-  if (!c) return fail(PT_ERR_INVALID, "null context");
-  if (!c->has_scene) return fail(PT_ERR_INVALID, "no scene uploaded");
-  if (!c->has_camera) return fail(PT_ERR_INVALID, "no camera set");
-  if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
-  ptd::RenderParams p;
-  p.nodes = c->stats_mode ? c->d_nodes_full : c->d_nodes;
-  p.tris = c->d_tris;
-  p.lights = c->d_lights_dev;
-  p.accum = c->d_accum;
-  p.stats = c->d_stats;
-  p.n_nodes = c->stats_mode ? c->n_nodes_full : c->n_nodes;
-  p.n_tris = c->n_tris;
-  p.n_lights = c->n_lights;
-  p.width = c->width;
-  p.height = c->height;
-  p.first_batch = first_batch;
-  p.n_batches = n_batches;
-  p.max_depth = c->params.max_depth;
-  p.sss_bounces = c->params.sss_bounces;
-  for (int i = 0; i < 3; ++i) {
-    p.cam_pos[i] = c->cam[i];
-    p.cam_dir[i] = c->cam[4 + i];
-    p.cam_up[i] = c->cam[8 + i];
+  return render_impl(c, first_batch, n_batches, nullptr);
+}
+
+// The gather step of a tile split (bench.py N>1): a fresh frame rendered from
+// batch 0 whose live items go straight into the pt_items_pack layout -- one
+// launch instead of render + culled fill + pack, and no accumulation-buffer
+// traffic.  The accumulation buffer is neither read nor written.
+int pt_render_packed(pt_context* c, uint32_t n_batches, void* packed, const void* gathered, size_t slot_floats,
+                     void* frame) {
+  if (!c || !packed) return fail(PT_ERR_INVALID, "null argument");
+  if (((uintptr_t)packed) & 15) return fail(PT_ERR_INVALID, "packed buffer must be 16-B aligned");
+  if (c->stats_mode) return fail(PT_ERR_UNSUPPORTED, "stats mode renders into the accumulation buffer");
+  Assembly as;
+  if (gathered) {
+    if (!frame) return fail(PT_ERR_INVALID, "gathered slots without a frame");
+    if ((((uintptr_t)gathered) & 15) || (((uintptr_t)frame) & 15) || (slot_floats & 3))
+      return fail(PT_ERR_INVALID, "buffers must be 16-B aligned, slots whole float4s");
+    as.src = gathered;
+    as.slot_floats = slot_floats;
+    as.frame = frame;
   }
-  p.fov = c->cam[12];
-  {
-    using namespace ptm;
-    const v3 cdir = mk(p.cam_dir[0], p.cam_dir[1], p.cam_dir[2]);
-    const v3 cup = mk(p.cam_up[0], p.cam_up[1], p.cam_up[2]);
-    const v3 right = normalize(cross(cdir, neg(cup)));
-    const v3 up = normalize(cross(right, cdir));
-    p.cam_right[0] = right.x; p.cam_right[1] = right.y; p.cam_right[2] = right.z;
-    p.cam_upv[0] = up.x; p.cam_upv[1] = up.y; p.cam_upv[2] = up.z;
-    p.tan_fov = tan_(radians_(p.fov * 0.5f));
-  }
-  p.blocks_x = (c->width + 15) / 16;
-  p.blocks_total = p.blocks_x * ((c->height + 15) / 16);
-  p.nranks = c->nranks;
-  p.rank = c->rank;
-  p.fresh = c->opt_fresh;
-  p.sm_batch = c->opt_sm_batch;
-  if (c->opt_sample_lanes) {
-    p.spl = c->opt_sample_lanes;
-  } else {
-    // auto: 4 sample lanes per pixel for an LDS-resident scene on a whole
-    // frame, else 8 — on a share of the frame each GPU's share shrinks while
-    // its heaviest workgroup does not, and on big scenes the samples of one
-    // pixel walk nearly the same nodes, so their loads coalesce.  Measured
-    // at 1080p 8spp with culling and compact launch: box spl 1/2/4/8 =
-    // 0.499/0.408/0.375/0.416 ms (whole frame), 0.354/0.264/0.225/0.221
-    // (1/2), 0.271/0.156/0.094/0.085 (1/8); displaced sphere 828/645/582/563;
-    // 1M cloud 968/930/927/923.  Never more lanes than samples.
-    const bool small = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
-    int want = (c->nranks >= 2 || !small) ? 8 : 4;
-    while (want > 1 && (uint32_t)want > n_batches) want >>= 1;
-    p.spl = want;
-  }
-  PT_HIP(hipSetDevice(c->device));
-  const int slot = c->ring_n % pt_context::kRing;
-  PT_HIP(hipEventRecord(c->ev0, c->stream));
-  PT_HIP(hipEventRecord(c->ring[slot][0], c->stream));
-  const bool fits = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
-  if (c->opt_scene_lds == 2 && !fits) return fail(PT_ERR_UNSUPPORTED, "scene too large for the LDS variant");
-  const bool lds = c->opt_scene_lds == 2 || (c->opt_scene_lds == 1 && fits);
-  // auto: the path-recursive kernel.  The lane state machine is kept as an
-  // option; it was measured slower on every scene (1080p: displaced sphere
-  // 8 spp 1022 vs 596 ms, 1M-triangle cloud 1 spp 191 vs 127 ms).
-  const bool sm = c->opt_kernel == 2;
-  // auto: the wavefront pipeline for scenes of at least kWfAutoTris triangles
-  // (not LDS-resident), the path-recursive kernel otherwise.  Measured at
-  // 1080p 8 spp (ms, recursive -> wavefront): displaced sphere 5K tris
-  // 39.5 -> 58.4, 20K 67 -> 72, 82K 560 -> 465; random cloud 100K 130 -> 76,
-  // 1M 923 -> 833; 10M (1 spp) 719 -> 667; box 0.38 -> 8.4.
-  const bool wf = c->opt_kernel == 3 || (c->opt_kernel == 0 && !lds && !c->stats_mode && c->n_tris >= kWfAutoTris);
-  if (wf && c->stats_mode) return fail(PT_ERR_UNSUPPORTED, "stats mode runs the path-recursive kernel only");
-  if (sm) p.spl = 1;
-  p.n_cull = -1;
-  p.items = nullptr;
-  p.culled_items = nullptr;
-  p.n_items = p.n_culled_items = 0;
-  if (c->opt_cull && !c->stats_mode && !sm)
-    p.n_cull = cull_rects(c->cam, c->width, c->height, c->root_lo, c->root_hi, c->lights_host.data(),
-                          c->n_lights, &p.cull[0][0], ptd::kMaxCullRects);
-  if (p.n_cull >= 0) {
-    const int rc = compact_items(c, &p);
-    if (rc) return rc;
-  }
-  c->last = p;   // the item exchange (pt_items_*) follows the last rendered frame
-  c->last_kernel = wf ? 3 : sm ? 2 : 1;
-  c->last_valid = !sm;
-  if (wf) {
-    const long long tiles = (p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;
-    const long long items = p.items ? p.n_items : tiles * p.spl;
-    long long chunk_paths = 0;
-    const int rc = wf_reserve(c, items * (256 / p.spl), n_batches, &chunk_paths);
-    if (rc) return rc;
-    ptd::WfBuffers b = c->wf;
-    b.cap = chunk_paths;   // paths per chunk (the allocation may be larger)
-    PT_HIP(ptd::launch_wavefront(p, b, lds, c->stream));
-  } else {
-    PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream));
-  }
-  PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
-  PT_HIP(hipEventRecord(c->ev1, c->stream));
-  c->ring_n++;
-  c->timed = true;
-  return PT_OK;
+  return render_impl(c, 0, n_batches, (float4*)packed, as);
 }
 
 int pt_dispatch(pt_context* c, uint32_t sample_batch) { return pt_render(c, sample_batch, 1); }
@@ -927,6 +1052,10 @@ int pt_set_option(pt_context* c, int key, int value) {
       if (value < 1 || value > 64) return fail(PT_ERR_INVALID, "PT_OPT_SM_BATCH takes 1..64");
       c->opt_sm_batch = value;
       return PT_OK;
+    case PT_OPT_ITEM_ORDER:
+      if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_ITEM_ORDER takes 0 or 1");
+      c->opt_item_order = value;
+      return PT_OK;
     case PT_OPT_FRESH_BATCH0:
       if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_FRESH_BATCH0 takes 0 or 1");
       c->opt_fresh = value;
@@ -1009,20 +1138,8 @@ int pt_items_unpack_all(pt_context* c, const void* src, size_t slot_floats, void
   if ((((uintptr_t)src) & 15) || (((uintptr_t)frame) & 15) || (slot_floats & 3))
     return fail(PT_ERR_INVALID, "buffers must be 16-B aligned, slots whole float4s");
   PT_HIP(hipSetDevice(c->device));
-  const std::vector<float> key = frame_key(c->last);
-  if (key != c->unpack_key) {
-    std::vector<int> table, live, culled;
-    for (int r = 0; r < c->last.nranks; ++r) {
-      item_lists(c->last, r, &live, &culled);
-      for (size_t i = 0; i < live.size(); ++i) table.insert(table.end(), {r, live[i], (int)i});
-      for (int it : culled) table.insert(table.end(), {r, it, -1});
-    }
-    PT_HIP(hipStreamSynchronize(c->stream));
-    const int rc = upload_ints(table, &c->d_unpack, &c->unpack_cap);
-    if (rc) return rc;
-    c->n_unpack = (int)(table.size() / 3);
-    c->unpack_key = key;
-  }
+  const int rc = unpack_table(c, c->last);
+  if (rc) return rc;
   PT_HIP(ptd::launch_items_unpack(c->last, (float4*)frame, (const float4*)src, slot_floats / 4, c->d_unpack,
                                   c->n_unpack, c->stream));
   return PT_OK;
@@ -1057,8 +1174,9 @@ int pt_reset_stats(pt_context* c) {
 int pt_last_launch_ms(pt_context* c, float* ms) {
   if (!c || !ms) return fail(PT_ERR_INVALID, "null argument");
   if (!c->timed) return fail(PT_ERR_INVALID, "no launch recorded");
-  PT_HIP(hipEventSynchronize(c->ev1));
-  PT_HIP(hipEventElapsedTime(ms, c->ev0, c->ev1));
+  PT_HIP(hipSetDevice(c->device));
+  PT_HIP(hipEventSynchronize(c->ring[c->last_slot][1]));
+  PT_HIP(hipEventElapsedTime(ms, c->ring[c->last_slot][0], c->ring[c->last_slot][1]));
   return PT_OK;
 }
 

@@ -64,6 +64,19 @@ struct RenderParams {
   int n_culled_items;
   int n_cull;
   float cull[8][4];
+  // pt_render_packed: live workgroup i stores its pixels to pack_out[i*256/spl
+  // + q] (the pt_items_pack layout) instead of the accumulation buffer, and no
+  // culled-item fill runs; null = normal rendering
+  float4* pack_out;
+  // ... and, optionally, trailing workgroups that assemble a gathered frame
+  // (the pt_items_unpack_all work: table entries {rank, item, slot} over
+  // per-rank slots of unpack_slot_f4 float4s) in the same launch
+  const float4* unpack_src;
+  float4* unpack_frame;
+  const int* unpack_table;
+  int n_unpack;
+  long long unpack_slot_f4;
+  int item_order;   // host only: PT_OPT_ITEM_ORDER for the item lists
 };
 constexpr int kMaxCullRects = 8;
 

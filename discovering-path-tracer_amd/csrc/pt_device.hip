@@ -409,6 +409,17 @@ __device__ __forceinline__ void store_lane(float4* px, const float* acc, int spl
     if (ch % spl == j) a[ch] = acc[ch];
 }
 
+// The pixel's result: into the accumulation buffer, or (pt_render_packed)
+// into this workgroup's slot of the packed live-item layout, where pixels
+// outside the image are zeros (acc of an inactive lane is never loaded).
+__device__ __forceinline__ void emit_lane(const RenderParams& P, bool active, size_t pix, int q, const float* acc,
+                                          int spl, int j) {
+  if (P.pack_out)
+    store_lane(P.pack_out + (size_t)blockIdx.x * (size_t)(256 / spl) + (size_t)q, acc, spl, j);
+  else if (active)
+    store_lane(P.accum + pix, acc, spl, j);
+}
+
 // Items (tile parts) whose every pixel is culled, listed by the host: each
 // thread folds the constant colour (0,0,0,1) into one pixel's running mean,
 // closed form where exact (fold_constant) — kPixPerFill pixels per thread.
@@ -437,6 +448,39 @@ __device__ __forceinline__ void fill_culled(const RenderParams& P, const int* __
   }
 }
 
+// Pixel q of item `item` of rank `rank` (the render kernel's mapping).
+__device__ __forceinline__ bool item_pixel(const RenderParams& P, int rank, int item, int q, size_t* pix) {
+  const int spl = P.spl;
+  const int tile = (item / spl) * P.nranks + rank, part = item % spl;
+  const int px = (tile % P.blocks_x) * 16 + q % 16;
+  const int py = (tile / P.blocks_x) * 16 + part * (16 / spl) + q / 16;
+  *pix = (size_t)py * (size_t)P.width + (size_t)px;
+  return px < P.width && py < P.height;
+}
+
+// One pixel-slot g of the gathered-frame assembly (items_unpack_kernel, and
+// the trailing workgroups of a pt_render_packed launch): a live item's pixel
+// from its rank's slot, a culled item's pixel as (0,0,0,1).
+__device__ __forceinline__ void unpack_pixel(const RenderParams& P, float4* __restrict__ frame,
+                                             const float4* __restrict__ src, size_t slot_f4,
+                                             const int* __restrict__ table, long long g) {
+  const int per = 256 / P.spl;
+  const int* e = table + 3 * (g / per);
+  const int q = (int)(g % per);
+  size_t pix;
+  if (!item_pixel(P, e[0], e[1], q, &pix)) return;
+  frame[pix] = e[2] >= 0 ? src[(size_t)e[0] * slot_f4 + (size_t)e[2] * per + q] : make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+}
+
+__device__ __forceinline__ void unpack_block(const RenderParams& P, int block) {
+  const long long total = (long long)P.n_unpack * (256 / P.spl);
+  for (int k = 0; k < kPixPerFill; ++k) {
+    const long long g = ((long long)block * kPixPerFill + k) * 256 + threadIdx.x;
+    if (g >= total) return;
+    unpack_pixel(P, P.unpack_frame, P.unpack_src, (size_t)P.unpack_slot_f4, P.unpack_table, g);
+  }
+}
+
 // LDS=true stages the whole scene (threaded nodes + triangle records) in LDS
 // once per workgroup; chosen by the host for scenes of at most a few tens of
 // KB (box.obj is 1.3 KB), where every lane re-reads the same few nodes.
@@ -454,8 +498,11 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
   // tile-split frame fast on 8 GPUs (pixels on geometry cost ~10x the others).
   // A persistent variant pulling wave-sized items from per-XCD queues was
   // measured slower at every SPL, on 1 GPU and on a 1/8 tile share.
-  if (P.items && (int)blockIdx.x >= P.n_items) {   // trailing fill workgroups (uniform)
-    fill_culled(P, P.culled_items, P.n_culled_items, (int)blockIdx.x - P.n_items);
+  if ((P.items || P.pack_out) && (int)blockIdx.x >= P.n_items) {   // trailing workgroups (uniform)
+    if (P.pack_out)
+      unpack_block(P, (int)blockIdx.x - P.n_items);   // assemble the previous gathered frame
+    else
+      fill_culled(P, P.culled_items, P.n_culled_items, (int)blockIdx.x - P.n_items);
     return;
   }
   const int spl = P.spl;
@@ -521,7 +568,7 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
   // the colour hand-off (fold_constant), the live pixels' lanes below.
   if (!live && active) fold_constant(P, acc, spl, j);
   if (!wg_live) {   // uniform per workgroup; stats mode never culls
-    if (active) store_lane(P.accum + pix, acc, spl, j);
+    emit_lane(P, active, pix, q, acc, spl, j);
     return;
   }
   if (LDS) {
@@ -569,6 +616,9 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
       const v3 bdir = normalize(sub(add(cdir, muls(neg(right), (ndcX * tanFov) * aspect)), muls(up, ndcY * tanFov)));
       const v3 focal = add(cpos, muls(bdir, 3.0f));                       // :459
       const v3 dir = normalize(sub(focal, origin));                       // :460
+      // PF (prefetch node k+1) for walks from device memory; on an LDS-staged
+      // scene it measured slower at every tile share (1080p box: +7 % on a
+      // whole frame, +12 % on a 1/8 share: registers)
       const v3 col = path_trace<STATS, !LDS>(P, origin, dir, seed, c, cand);
       col4 = make_float4(col.x, col.y, col.z, 1.0f);                      // vec4(color, 1.0)
      }
@@ -594,7 +644,7 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
   }
-  if (active) store_lane(P.accum + pix, acc, spl, j);
+  emit_lane(P, active, pix, q, acc, spl, j);
   if (STATS) {
     const unsigned long long rays = wave_sum(c.rays), nodes = wave_sum(c.nodes), leaves = wave_sum(c.leaves);
     const unsigned long long smp = wave_sum((unsigned long long)nsamp);
@@ -679,16 +729,6 @@ __global__ __launch_bounds__(256) void tiles_kernel(float4* frame, float4* packe
     frame[pi] = packed[ti];
 }
 
-// Pixel q of item `item` of rank `rank` (the render kernel's mapping).
-__device__ __forceinline__ bool item_pixel(const RenderParams& P, int rank, int item, int q, size_t* pix) {
-  const int spl = P.spl;
-  const int tile = (item / spl) * P.nranks + rank, part = item % spl;
-  const int px = (tile % P.blocks_x) * 16 + q % 16;
-  const int py = (tile / P.blocks_x) * 16 + part * (16 / spl) + q / 16;
-  *pix = (size_t)py * (size_t)P.width + (size_t)px;
-  return px < P.width && py < P.height;
-}
-
 __global__ __launch_bounds__(256) void items_pack_kernel(RenderParams P, const float4* __restrict__ frame,
                                                          float4* __restrict__ packed, const int* __restrict__ items,
                                                          int n) {
@@ -703,14 +743,9 @@ __global__ __launch_bounds__(256) void items_pack_kernel(RenderParams P, const f
 __global__ __launch_bounds__(256) void items_unpack_kernel(RenderParams P, float4* __restrict__ frame,
                                                            const float4* __restrict__ src, size_t slot_f4,
                                                            const int* __restrict__ table, int n) {
-  const int per = 256 / P.spl;
   const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (g >= (long long)n * per) return;
-  const int* e = table + 3 * (g / per);
-  const int q = (int)(g % per);
-  size_t pix;
-  if (!item_pixel(P, e[0], e[1], q, &pix)) return;
-  frame[pix] = e[2] >= 0 ? src[(size_t)e[0] * slot_f4 + (size_t)e[2] * per + q] : make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+  if (g >= (long long)n * (256 / P.spl)) return;
+  unpack_pixel(P, frame, src, slot_f4, table, g);
 }
 
 __global__ __launch_bounds__(256) void math_kernel(int fn, const float* __restrict__ x, float* __restrict__ y,
@@ -1579,7 +1614,11 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool
   const long long tiles = (long long)(p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;
   long long grid = state_machine ? tiles : tiles * p.spl;
   if (grid <= 0 || p.n_batches == 0) return hipSuccess;
-  if (p.items && !state_machine) {   // compact list of live items, then the fill workgroups
+  if (p.pack_out && (state_machine || stats)) return hipErrorInvalidValue;
+  if (p.pack_out) {   // live items (p.n_items), then the assembly workgroups
+    const long long px = (long long)p.n_unpack * (256 / p.spl);
+    grid = p.n_items + (px + 256 * kPixPerFill - 1) / (256 * kPixPerFill);
+  } else if (p.items && !state_machine) {   // compact list of live items, then the fill workgroups
     const long long px = (long long)p.n_culled_items * (256 / p.spl);
     grid = p.n_items + (px + 256 * kPixPerFill - 1) / (256 * kPixPerFill);
   }

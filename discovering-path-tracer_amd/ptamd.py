@@ -24,6 +24,7 @@ PT_OPT_KERNEL = 4
 PT_OPT_SM_BATCH = 5
 PT_OPT_PRIMARY_CULL = 6
 PT_OPT_WF_PATHS = 7
+PT_OPT_ITEM_ORDER = 8
 KERNEL_AUTO, KERNEL_RECURSIVE, KERNEL_STATE_MACHINE, KERNEL_WAVEFRONT = 0, 1, 2, 3
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).
@@ -37,7 +38,7 @@ EXPORTS = [
     "pt_scene_counts", "pt_scene_copy", "pt_scene_upload", "pt_scene_free", "pt_pack_light",
     "pt_default_camera", "pt_primary_cull_rects", "pt_scene_save", "pt_scene_load_cache",
     "pt_progressive_camera", "pt_progressive_advance", "pt_readback_begin", "pt_readback_end", "pt_write_image",
-    "pt_items_live", "pt_items_pack", "pt_items_unpack_all",
+    "pt_items_live", "pt_items_pack", "pt_items_unpack_all", "pt_render_packed",
 ]
 
 
@@ -102,6 +103,7 @@ def lib():
             "pt_items_live": ([vp, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
             "pt_items_pack": ([vp, vp], i32),
             "pt_items_unpack_all": ([vp, vp, sz, vp], i32),
+            "pt_render_packed": ([vp, u32, vp, vp, sz, vp], i32),
             "pt_scene_load_cache": ([ctypes.c_char_p, ctypes.POINTER(vp)], i32),
         }
         for name, (args, res) in sig.items():
@@ -341,6 +343,12 @@ class Renderer:
 
     def items_pack(self, dst_ptr):
         _check(lib().pt_items_pack(self._c, dst_ptr), "pt_items_pack")
+
+    def render_packed(self, n_batches, dst_ptr, gathered_ptr=None, slot_floats=0, frame_ptr=None):
+        """Fresh frame's live items into dst; optionally assemble the previous
+        frame's gathered slots into frame in the same launch."""
+        _check(lib().pt_render_packed(self._c, n_batches, dst_ptr, gathered_ptr, slot_floats, frame_ptr),
+               "pt_render_packed")
 
     def items_unpack_all(self, src_ptr, slot_floats, frame_ptr):
         _check(lib().pt_items_unpack_all(self._c, src_ptr, slot_floats, frame_ptr), "pt_items_unpack_all")

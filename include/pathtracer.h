@@ -174,6 +174,20 @@ int pt_tiles_unpack(pt_context* ctx, const void* src_device, int src_rank, void*
 int pt_items_live(pt_context* ctx, int rank, int* n_items, int* item_pixels);
 int pt_items_pack(pt_context* ctx, void* dst_device);
 int pt_items_unpack_all(pt_context* ctx, const void* src_device, size_t slot_floats, void* frame_device);
+/* pt_render_packed: render a fresh frame (batches 0..n_batches-1, as
+ * pt_clear_accum + pt_render) and write this rank's live items straight into
+ * dst_device in the pt_items_pack layout — what pt_render + pt_items_pack
+ * give, in one launch, without the culled-item fill.  The accumulation buffer
+ * is neither read nor written.  gathered_device (optional, else null): the
+ * per-rank slots of the PREVIOUS frame, which the same launch assembles into
+ * frame_device exactly as pt_items_unpack_all would — the root's step of a
+ * pipelined tile split is then one launch; that frame must have been
+ * rendered by pt_render_packed with the same item layout — frame size,
+ * partition, sample lanes, culling rectangles, item order (error otherwise).
+ * Replaces, for the tile split, the reference's one dispatch per frame plus
+ * image readback (VulkanRayTracer.cpp:803-865). */
+int pt_render_packed(pt_context* ctx, uint32_t n_batches, void* dst_device, const void* gathered_device,
+                     size_t slot_floats, void* frame_device);
 
 /* ---- kernel options ---------------------------------------------------- */
 /* PT_OPT_SCENE_IN_LDS: stage the scene in LDS per workgroup — 0 never,
@@ -211,6 +225,11 @@ int pt_items_unpack_all(pt_context* ctx, const void* src_device, size_t slot_flo
  * chunks of whole batches (at least one batch of the frame per chunk).
  * Output is identical for every value. */
 #define PT_OPT_WF_PATHS 7
+/* PT_OPT_ITEM_ORDER: 1 (default) = live items (tile parts) launched heaviest
+ * first by a host estimate (pixels inside the root box's rectangle), so long
+ * workgroups start early and short ones fill the tail; 0 = scan order.  The
+ * packed exchange layout follows the same order.  Output is identical. */
+#define PT_OPT_ITEM_ORDER 8
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */

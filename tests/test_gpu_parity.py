@@ -381,11 +381,17 @@ def test_progressive_loop_camera_reset_and_async_readback():
         r.readback_end(t2)                        # already collected
 
 
-@pytest.mark.parametrize("nranks,cam", [(2, 0), (3, 1), (8, 0), (2, 5)])
-def test_sparse_item_exchange_assembles_frame(nranks, cam):
+@pytest.mark.parametrize("nranks,cam,mode", [(2, 0, "pack"), (3, 1, "pack"), (8, 0, "pack"), (2, 5, "pack"),
+                                           (3, 1, "direct"), (8, 0, "direct"), (2, 5, "direct"),
+                                           (3, 0, "direct-scan-order"), (2, 1, "direct-wavefront")])
+def test_sparse_item_exchange_assembles_frame(nranks, cam, mode):
     """pt_items_pack (live items only) on every rank + one pt_items_unpack_all
     on the root = the single-GPU frame; culled items are rebuilt as
-    (0,0,0,1).  Camera 5 sits inside the box (no culling: every item live)."""
+    (0,0,0,1).  Camera 5 sits inside the box (no culling: every item live).
+    "direct": pt_render_packed writes the live items into the slot in the
+    render launch itself (the accumulator, pre-filled with NaN, stays
+    untouched); "scan-order": PT_OPT_ITEM_ORDER 0; "wavefront": the wavefront
+    kernel, which renders then packs."""
     import torch
     v, i, n = _box()
     W, H = 150, 70
@@ -395,6 +401,10 @@ def test_sparse_item_exchange_assembles_frame(nranks, cam):
         r = _setup(v, i, n, cam=camera)
         r.set_partition(nranks, rank)
         r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+        if mode.endswith("scan-order"):
+            r.set_option(ptamd.PT_OPT_ITEM_ORDER, 0)
+        if mode.endswith("wavefront"):
+            r.set_option(ptamd.PT_OPT_KERNEL, 3)
         r.resize_and_clear(W, H)
         r.render(0, 8)
         rs.append(r)
@@ -403,9 +413,20 @@ def test_sparse_item_exchange_assembles_frame(nranks, cam):
     assert all(rs[k].items_live(k) == (counts[k], per) for k in range(nranks))
     slot = max(counts) * per * 4
     src = torch.full((nranks, max(slot, 4)), float("nan"), dtype=torch.float32, device="cuda")
+    rs_keep = []
     for k, r in enumerate(rs):
-        r.items_pack(src[k].data_ptr())
-        r.synchronize()
+        if mode.startswith("direct"):
+            if not mode.endswith("wavefront"):
+                nan = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+                r.bind_accum(nan.data_ptr(), W, H)
+                rs_keep.append(nan)
+            r.render_packed(8, src[k].data_ptr())
+            r.synchronize()
+            if not mode.endswith("wavefront"):
+                assert torch.isnan(nan).all(), "pt_render_packed wrote the accumulation buffer"
+        else:
+            r.items_pack(src[k].data_ptr())
+            r.synchronize()
     frame = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
     rs[0].items_unpack_all(src.data_ptr(), src.shape[1], frame.data_ptr())
     rs[0].synchronize()
@@ -415,6 +436,50 @@ def test_sparse_item_exchange_assembles_frame(nranks, cam):
         assert sum(counts) * per >= W * H
     else:
         assert sum(counts) * per < W * H          # culled items are not shipped
+
+
+@pytest.mark.parametrize("nranks,cam,kernel", [(2, 0, 0), (3, 1, 0), (8, 0, 0), (2, 5, 0), (3, 0, 3)])
+def test_render_packed_assembles_previous_frame(nranks, cam, kernel):
+    """The pipelined tile-split step: every rank's pt_render_packed writes its
+    live items to its slot, and the root's next pt_render_packed assembles
+    those slots into the frame in the same launch (kernel 3: the wavefront
+    fallback, separate launches).  Both gathered frames equal the oracle; a
+    change of item layout in between (frame size) is refused."""
+    import torch
+    v, i, n = _box()
+    W, H = 150, 70
+    camera = CULL_CAMS[cam]
+    rs = []
+    for rank in range(nranks):
+        r = _setup(v, i, n, cam=camera)
+        r.set_partition(nranks, rank)
+        if kernel:
+            r.set_option(ptamd.PT_OPT_KERNEL, kernel)
+        r.resize_and_clear(W, H)
+        r.render(0, 8)
+        rs.append(r)
+    per = rs[0].items_live(0)[1]
+    slot = max(4, max(rs[0].items_live(k)[0] for k in range(nranks)) * per * 4)
+    src = [torch.full((nranks, slot), float("nan"), dtype=torch.float32, device="cuda") for _ in range(2)]
+    for k, r in enumerate(rs):
+        r.render_packed(8, src[0][k].data_ptr())
+        r.synchronize()
+    frame = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+    for k in range(nranks - 1, -1, -1):   # the root (0) last: it assembles frame 1
+        if k == 0:
+            rs[0].render_packed(8, src[1][0].data_ptr(), src[0].data_ptr(), slot, frame.data_ptr())
+        else:
+            rs[k].render_packed(8, src[1][k].data_ptr())
+        rs[k].synchronize()
+    ref, _ = _oracle(v, i, n, W, H, nb=8, cam=camera)
+    _assert_same(frame.cpu().numpy().reshape(-1), ref, f"frame 1 assembled in frame 2's launch, {nranks} ranks")
+    frame2 = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+    rs[0].items_unpack_all(src[1].data_ptr(), slot, frame2.data_ptr())
+    rs[0].synchronize()
+    _assert_same(frame2.cpu().numpy().reshape(-1), ref, "frame 2")
+    rs[0].resize_and_clear(W + 16, H)   # another item layout
+    with pytest.raises(ptamd.PTError):
+        rs[0].render_packed(8, src[0][0].data_ptr(), src[1].data_ptr(), slot, frame.data_ptr())
 
 
 # ---- wavefront pipeline (PT_OPT_KERNEL 3) ----------------------------------
