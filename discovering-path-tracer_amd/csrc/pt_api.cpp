@@ -577,16 +577,19 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   if (c->opt_sample_lanes) {
     p.spl = c->opt_sample_lanes;
   } else {
-    // auto: 4 sample lanes per pixel for an LDS-resident scene on a whole
-    // frame, else 8 — on a share of the frame each GPU's share shrinks while
+    // auto: 4 sample lanes per pixel for an LDS-resident scene on up to 7
+    // ranks, else 8 — on a share of the frame each GPU's share shrinks while
     // its heaviest workgroup does not, and on big scenes the samples of one
     // pixel walk nearly the same nodes, so their loads coalesce.  Measured
     // at 1080p 8spp with culling and compact launch: box spl 1/2/4/8 =
     // 0.499/0.408/0.375/0.416 ms (whole frame), 0.354/0.264/0.225/0.221
     // (1/2), 0.271/0.156/0.094/0.085 (1/8); displaced sphere 828/645/582/563;
     // 1M cloud 968/930/927/923.  Never more lanes than samples.
+    // With frames alternating between two streams (bench.py N > 1), the
+    // 1/2 and 1/4 shares favour 4 lanes (0.187 vs 0.210, 0.101 vs 0.110 ms
+    // per step) and the 1/8 share 8 (0.062 vs 0.069).
     const bool small = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
-    int want = (c->nranks >= 2 || !small) ? 8 : 4;
+    int want = (c->nranks >= 8 || !small) ? 8 : 4;
     while (want > 1 && (uint32_t)want > n_batches) want >>= 1;
     p.spl = want;
   }
@@ -1193,6 +1196,26 @@ int pt_launch_times_ms(pt_context* c, float* out, size_t max_n, size_t* n_out) {
     ++n;
   }
   *n_out = n;
+  return PT_OK;
+}
+
+// Launches may overlap (frames alternating between streams): the device time
+// from the first launch's start to the last end, i.e. the busy span a
+// throughput figure divides by.
+int pt_launch_span_ms(pt_context* c, float* ms, size_t* n_out) {
+  if (!c || !ms || !n_out) return fail(PT_ERR_INVALID, "null argument");
+  if (c->ring_n == 0) return fail(PT_ERR_INVALID, "no launch recorded since pt_reset_launch_times");
+  if (c->ring_n > pt_context::kRing) return fail(PT_ERR_UNSUPPORTED, "more launches than the event ring holds");
+  PT_HIP(hipSetDevice(c->device));
+  float span = 0.0f;
+  for (int k = 0; k < c->ring_n; ++k) {
+    float t = 0.0f;
+    PT_HIP(hipEventSynchronize(c->ring[k][1]));
+    PT_HIP(hipEventElapsedTime(&t, c->ring[0][0], c->ring[k][1]));
+    span = t > span ? t : span;
+  }
+  *ms = span;
+  *n_out = (size_t)c->ring_n;
   return PT_OK;
 }
 

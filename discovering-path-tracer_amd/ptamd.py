@@ -38,7 +38,7 @@ EXPORTS = [
     "pt_scene_counts", "pt_scene_copy", "pt_scene_upload", "pt_scene_free", "pt_pack_light",
     "pt_default_camera", "pt_primary_cull_rects", "pt_scene_save", "pt_scene_load_cache",
     "pt_progressive_camera", "pt_progressive_advance", "pt_readback_begin", "pt_readback_end", "pt_write_image",
-    "pt_items_live", "pt_items_pack", "pt_items_unpack_all", "pt_render_packed",
+    "pt_items_live", "pt_items_pack", "pt_items_unpack_all", "pt_render_packed", "pt_launch_span_ms",
 ]
 
 
@@ -83,6 +83,7 @@ def lib():
             "pt_tiles_unpack": ([vp, vp, i32, vp], i32), "pt_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
             "pt_reset_stats": ([vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
             "pt_launch_times_ms": ([vp, vp, sz, psz], i32), "pt_reset_launch_times": ([vp], i32),
+            "pt_launch_span_ms": ([vp, ctypes.POINTER(ctypes.c_float), psz], i32),
             "pt_selftest_math": ([i32, i32, vp, vp, sz], i32),
             "pt_selftest_exhaustive": ([i32, i32, ctypes.POINTER(ctypes.c_ulonglong), ctypes.POINTER(u32)], i32),
             "pt_scene_load_obj": ([ctypes.c_char_p, ctypes.POINTER(vp)], i32),
@@ -414,6 +415,13 @@ class Renderer:
         out = np.zeros(512, np.float32)
         _check(lib().pt_launch_times_ms(self._c, out.ctypes.data, out.size, ctypes.byref(n)), "pt_launch_times_ms")
         return out[: n.value].copy()
+
+    def launch_span_ms(self):
+        """(device ms from the first launch's start to the last end, launches)
+        since reset_launch_times -- the busy span of overlapping launches."""
+        ms, n = ctypes.c_float(), ctypes.c_size_t()
+        _check(lib().pt_launch_span_ms(self._c, ctypes.byref(ms), ctypes.byref(n)), "pt_launch_span_ms")
+        return ms.value, n.value
 
     def reset_launch_times(self):
         _check(lib().pt_reset_launch_times(self._c), "pt_reset_launch_times")

@@ -260,6 +260,11 @@ int pt_last_launch_ms(pt_context* ctx, float* ms);
 /* Device times of every render launch since pt_reset_launch_times (the last
  * 512 at most), oldest first; waits for them to finish. */
 int pt_launch_times_ms(pt_context* ctx, float* out, size_t max_n, size_t* n_out);
+/* Device time from the start of the first render launch since
+ * pt_reset_launch_times to the end of the last one (launches on several
+ * streams overlap, so their durations do not add up); *n_out = launches.
+ * Waits for them to finish; PT_ERR_UNSUPPORTED past 512 launches. */
+int pt_launch_span_ms(pt_context* ctx, float* ms, size_t* n_out);
 int pt_reset_launch_times(pt_context* ctx);
 /* Evaluates the kernel's fp32 math on the device for bitwise checks against
  * the oracle: fn 0 log, 1 exp, 2 sin, 3 cos, 4 tan, 5 acos, 6 sqrt,
