@@ -394,12 +394,14 @@ static void item_lists(const ptd::RenderParams& p, int rank, std::vector<int>* l
   std::vector<std::pair<int, int>> weighted;   // (-weight, item)
   for (int li = 0; li < tiles; ++li) {
     const int b = li * p.nranks + rank;
-    const int gx0 = (b % p.blocks_x) * 16;
+    int bx, by;
+    ptd::tile_block(b, p.blocks_x, &bx, &by);
+    const int gx0 = bx * 16;
     const float wx0 = (2.0f * (float)gx0 / (float)W) - 1.0f, wx1 = (2.0f * (float)(gx0 + 15) / (float)W) - 1.0f;
     int cols[ptd::kMaxCullRects] = {};
     for (int r = 0; r < p.n_cull; ++r) cols[r] = pixels_in(gx0, 16, W, p.cull[r][0], p.cull[r][1]);
     for (int part = 0; part < spl; ++part) {
-      const int gy0 = (b / p.blocks_x) * 16 + part * rows;
+      const int gy0 = by * 16 + part * rows;
       const float wy0 = (2.0f * (float)gy0 / (float)H) - 1.0f;
       const float wy1 = (2.0f * (float)(gy0 + rows - 1) / (float)H) - 1.0f;
       bool any = p.n_cull < 0;   // no culling: every item is live

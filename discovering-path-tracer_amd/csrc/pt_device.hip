@@ -434,8 +434,10 @@ __device__ __forceinline__ void fill_culled(const RenderParams& P, const int* __
     if (g >= total) return;
     const int item = items[g / per_item], q = (int)(g % per_item);
     const int tile = (item / spl) * P.nranks + P.rank, part = item % spl;
-    const int px = (tile % P.blocks_x) * 16 + q % 16;
-    const int py = (tile / P.blocks_x) * 16 + part * (16 / spl) + q / 16;
+    int bx, by;
+    tile_block(tile, P.blocks_x, &bx, &by);
+    const int px = bx * 16 + q % 16;
+    const int py = by * 16 + part * (16 / spl) + q / 16;
     if (px >= P.width || py >= P.height) continue;
     float4* dst = P.accum + (size_t)py * (size_t)P.width + (size_t)px;
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -452,8 +454,10 @@ __device__ __forceinline__ void fill_culled(const RenderParams& P, const int* __
 __device__ __forceinline__ bool item_pixel(const RenderParams& P, int rank, int item, int q, size_t* pix) {
   const int spl = P.spl;
   const int tile = (item / spl) * P.nranks + rank, part = item % spl;
-  const int px = (tile % P.blocks_x) * 16 + q % 16;
-  const int py = (tile / P.blocks_x) * 16 + part * (16 / spl) + q / 16;
+  int bx, by;
+  tile_block(tile, P.blocks_x, &bx, &by);
+  const int px = bx * 16 + q % 16;
+  const int py = by * 16 + part * (16 / spl) + q / 16;
   *pix = (size_t)py * (size_t)P.width + (size_t)px;
   return px < P.width && py < P.height;
 }
@@ -517,7 +521,8 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
   int* cand = &cand_buf[wave][0][lane];
   const int q = wave * (64 / spl) + lane / spl;       // pixel within the workgroup
   const int j = lane % spl;                           // sample slot
-  const int bx = tile % P.blocks_x, by = tile / P.blocks_x;
+  int bx, by;
+  tile_block(tile, P.blocks_x, &bx, &by);
   const int px = bx * 16 + q % 16;
   const int py = by * 16 + part * (16 / spl) + q / 16;
   const bool active = tile < P.blocks_total && px < P.width && py < P.height;   // :425-428
@@ -705,12 +710,12 @@ __global__ __launch_bounds__(256) void clear_kernel(float4* accum, int W, int H,
   if (i >= (size_t)W * (size_t)H) return;
   const int x = (int)(i % (size_t)W), y = (int)(i / (size_t)W);
   const int blocks_x = (W + 15) / 16;
-  const int b = (y / 16) * blocks_x + x / 16;
+  const int b = block_tile(x / 16, y / 16, blocks_x);
   const float z = (b % nranks == rank) ? 0.0f : -0.0f;
   accum[i] = make_float4(z, z, z, z);
 }
 
-// Owned 16x16 tiles <-> a dense buffer (tile o = owned block rank + o*nranks,
+// Owned 16x16 tiles <-> a dense buffer (tile o = owned tile rank + o*nranks,
 // 256 float4 row-major inside the tile, zeros outside the image): what a rank
 // ships to the root so the frame can be assembled by a gather.
 template <bool PACK>
@@ -719,7 +724,9 @@ __global__ __launch_bounds__(256) void tiles_kernel(float4* frame, float4* packe
   const int o = (int)blockIdx.x;
   const int b = o * nranks + rank;
   const int t = (int)threadIdx.x;
-  const int x = (b % blocks_x) * 16 + (t & 15), y = (b / blocks_x) * 16 + (t >> 4);
+  int bx, by;
+  tile_block(b, blocks_x, &bx, &by);
+  const int x = bx * 16 + (t & 15), y = by * 16 + (t >> 4);
   const bool in = x < W && y < H;
   const size_t pi = (size_t)y * (size_t)W + (size_t)x;
   const size_t ti = (size_t)o * 256 + (size_t)t;
@@ -1147,7 +1154,8 @@ __global__ __launch_bounds__(256, PT_SM_MIN_BLOCKS) void render_sm_kernel(Render
   CamFrame F;
   F.W = P.width;
   F.H = P.height;
-  const int bx = tile % P.blocks_x, by = tile / P.blocks_x;
+  int bx, by;
+  tile_block(tile, P.blocks_x, &bx, &by);
   F.px = bx * 16 + (wave & 1) * 8 + (lane & 7);
   F.py = by * 16 + (wave >> 1) * 8 + (lane >> 3);
   const bool active = tile < P.blocks_total && F.px < F.W && F.py < F.H;
@@ -1266,8 +1274,10 @@ __device__ __forceinline__ bool wf_pixel(const RenderParams& P, long long pp, in
   const int idx = (int)(pp / per), q = (int)(pp % per);
   const int item = P.items ? P.items[idx] : idx;
   const int tile = (item / spl) * P.nranks + P.rank, part = item % spl;
-  *px = (tile % P.blocks_x) * 16 + q % 16;
-  *py = (tile / P.blocks_x) * 16 + part * (16 / spl) + q / 16;
+  int bx, by;
+  tile_block(tile, P.blocks_x, &bx, &by);
+  *px = bx * 16 + q % 16;
+  *py = by * 16 + part * (16 / spl) + q / 16;
   return tile < P.blocks_total && *px < P.width && *py < P.height;
 }
 

@@ -229,11 +229,13 @@ def device_math_exhaustive(fn, device=0):
 
 
 def partition_owned(width, height, nranks, rank):
-    """Pixels a rank renders under pt_set_partition: 16x16 blocks, row-major
-    block id b, owned iff b % nranks == rank.  Returns a (H, W) bool mask."""
-    bx = (width + 15) // 16
+    """Pixels a rank renders under pt_set_partition: 16x16 blocks, block
+    (bx, by) is tile b = by*blocks_x + (bx - by) mod blocks_x (rows rotated),
+    owned iff b % nranks == rank.  Returns a (H, W) bool mask."""
+    nbx = (width + 15) // 16
     ys, xs = np.mgrid[0:height, 0:width]
-    return ((ys // 16) * bx + xs // 16) % nranks == rank
+    by, bx = ys // 16, xs // 16
+    return (by * nbx + (bx - by) % nbx) % nranks == rank
 
 
 def primary_cull_rects(camera_ubo, width, height, root_min, root_max, lights16, max_rects=8):

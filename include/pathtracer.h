@@ -149,8 +149,10 @@ int pt_readback_begin(pt_context* ctx, int* ticket);
 int pt_readback_end(pt_context* ctx, int ticket, float* rgba, size_t n_floats);
 
 /* ---- multi-GPU screen-space partition ------------------ */
-/* Pixels are grouped into 16x16 blocks, numbered row-major; this context
- * renders block b iff b % nranks == rank.  pt_clear_accum then writes +0 to
+/* Pixels are grouped into 16x16 blocks.  Block (bx, by) is tile
+ * b = by*blocks_x + (bx - by) mod blocks_x (rows rotated by their index, so
+ * ranks get anti-diagonal stripes, not column stripes); this context renders
+ * tile b iff b % nranks == rank.  pt_clear_accum then writes +0 to
  * owned pixels and -0 (the IEEE additive identity) to the others, so a sum
  * reduction of all ranks' buffers is bit-identical to a single-GPU frame. */
 int pt_set_partition(pt_context* ctx, int nranks, int rank);

@@ -649,7 +649,9 @@ int oracle_bvh_build(const float* verts, const uint32_t* idx_in, size_t n_idx,
 // One or more sequential sample batches (= that many 1-spp dispatches of the
 // reference) over the pixels selected by (row_stride,row_phase) and the tile
 // ownership (tile, nranks, rank): pixel (x,y) is rendered iff
-// y % row_stride == row_phase and ((y/tile)*ceil(W/tile) + x/tile) % nranks == rank.
+// y % row_stride == row_phase and tile (x/tile, y/tile) is owned: with
+// tx = ceil(W/tile), block (bx, by) is tile by*tx + (bx - by) mod tx, owned iff
+// that % nranks == rank.
 // accum is W*H*4 floats (RGBA32F, row-major, y*W+x), read-modify-written.
 // stats[0..2] += traceRay calls, nodes visited, leaf triangle tests.
 int oracle_render(const float* verts, const uint32_t* idx, const float* nodes, size_t n_nodes,
@@ -687,7 +689,9 @@ int oracle_render(const float* verts, const uint32_t* idx, const float* nodes, s
       if (y >= H) break;
       if (y % row_stride != row_phase) continue;
       for (int x = 0; x < W; ++x) {
-        int tid2 = (y / tile) * tiles_x + x / tile;
+        // partition order of the product (pt_device.h tile_block): rows rotated by their index
+        const int by = y / tile, bx = x / tile;
+        const int tid2 = by * tiles_x + (bx - by % tiles_x + tiles_x) % tiles_x;
         if (tid2 % nranks != rank) continue;
         float* a = accum + ((size_t)y * W + x) * 4;
         for (uint32_t b = 0; b < n_batches; ++b) shade_pixel(S, (uint32_t)x, (uint32_t)y, first_batch + b, a, &st);

@@ -536,9 +536,6 @@ def test_wavefront_culling_and_partition(cam):
     W, H = 96, 54
     ref, _ = _oracle(v, i, n, W, H, nb=4, cam=CULL_CAMS[cam])
     ref = ref.reshape(H, W, 4)
-    bx = (W + 15) // 16
-    yy, xx = np.mgrid[0:H, 0:W]
-    tile = (yy // 16) * bx + xx // 16
     for nranks, rank in [(1, 0), (3, 2)]:
         r = _setup(v, i, n, cam=CULL_CAMS[cam])
         r.set_option(ptamd.PT_OPT_KERNEL, ptamd.KERNEL_WAVEFRONT)
@@ -546,7 +543,7 @@ def test_wavefront_culling_and_partition(cam):
         r.resize_and_clear(W, H)
         r.render(0, 4)
         got = r.read_accum().reshape(H, W, 4)
-        own = tile % nranks == rank
+        own = ptamd.partition_owned(W, H, nranks, rank)
         _assert_same(got[own].reshape(-1), ref[own].reshape(-1), f"wavefront cam {cam} rank {rank}/{nranks}")
 
 

@@ -82,10 +82,10 @@ rep("""    for (uint32_t base = 0; base < P.n_batches; base += (uint32_t)spl) {
      const uint32_t s = base + (uint32_t)j;""", """    ph_add(10, ph_t() - tk0_);
     for (uint32_t base = 0; base < P.n_batches; base += (uint32_t)spl) {
      const uint32_t s = base + (uint32_t)j;""")
-rep("""  if (active) {
-    float* a = (float*)&P.accum[pix];""", """  const unsigned long long te0_ = ph_t();
-  if (active) {
-    float* a = (float*)&P.accum[pix];""")
+rep("""  emit_lane(P, active, pix, q, acc, spl, j);
+  ph_add(8, ph_t() - tk0_);""", """  const unsigned long long te0_ = ph_t();
+  emit_lane(P, active, pix, q, acc, spl, j);
+  ph_add(8, ph_t() - tk0_);""")
 rep("""  ph_add(8, ph_t() - tk0_);""", """  ph_add(11, ph_t() - te0_);
   ph_add(8, ph_t() - tk0_);""")
 src += """
