@@ -143,6 +143,9 @@ def main():
     ap.add_argument("--streams", type=int, choices=[1, 2, 3, 4], default=None,
                     help="gather path: frames alternate between this many streams, so one frame's tail "
                          "overlaps the next frame's head (default 2 for N > 1, 1 at N = 1)")
+    ap.add_argument("--timing-every", type=int, default=None,
+                    help="HIP event pair around every k-th launch (default 4 on one stream, where a pair "
+                         "costs ~7 us of device time per launch, 1 on two streams, where it is hidden)")
     ap.add_argument("--packed", action="store_true", help="N=1: run the gather path (render_packed + assembly)")
     ap.add_argument("--compare-no-cull", action="store_true",
                     help="N=1: also time the same steps with primary-ray culling off (reported as primary_cull_off)")
@@ -153,6 +156,8 @@ def main():
                              or int(os.environ.get("PT_BENCH_EMULATE_RANKS", "1")) > 1) else 1
     if args.collective == "reduce":
         args.streams = 1   # the reduce path runs on one stream
+    if args.timing_every is None:
+        args.timing_every = 4 if args.streams == 1 else 1
     DEPTH, SSS = args.depth, args.sss
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -204,6 +209,7 @@ def main():
     r.set_camera(cam)
     r.set_params(DEPTH, SSS)
     r.set_partition(max(world, emu), rank)
+    r.set_option(ptamd.PT_OPT_LAUNCH_TIMING, args.timing_every)
     for kv in args.opt:
         k, _, val = kv.partition("=")
         r.set_option(int(k), int(val))
@@ -270,14 +276,21 @@ def main():
         slot = max(r.items_live(k)[0] for k in range(nparts)) * per * 4
         slot = max(slot, 4)
         root = rank == 0
-        send = [torch.zeros(slot, dtype=torch.float32, device=dev) for _ in range(2)]
-        recv_all = [torch.zeros((nparts, slot), dtype=torch.float32, device=dev) for _ in range(2)] if root else None
-        recv = [[recv_all[b][k] for k in range(nparts)] for b in range(2)] if root else None
+        # Frame k uses buffer set k % nbuf and, under --assemble 2, assembles
+        # frame k - depth from that same set in its own launch; depth = streams,
+        # so frame k waits only for frame k - depth's gather (which follows
+        # frame k - depth's launch on frame k's stream) and `streams` frames
+        # are in flight.  The gather of frame k then overwrites the receive
+        # set after the launch that read it, on the same stream.
+        depth = max(2, args.streams) if args.assemble == 2 else 1   # frames in flight before assembly
+        nbuf = max(2, depth)
+        send = [torch.zeros(slot, dtype=torch.float32, device=dev) for _ in range(nbuf)]
+        recv_all = [torch.zeros((nparts, slot), dtype=torch.float32, device=dev) for _ in range(nbuf)] if root else None
+        recv = [[recv_all[b][k] for k in range(nparts)] for b in range(nbuf)] if root else None
         outs = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) for _ in range(args.streams)] if root else None
         out = outs[0] if root else None
         streams = [stream] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
         state = {"k": 0}
-        depth = 2 if args.assemble == 2 else 1   # frames in flight before assembly
 
         def finish(work, buf):   # separate assembly launch of one gathered frame
             if work is not None:
@@ -286,7 +299,7 @@ def main():
                 r.items_unpack_all(recv_all[buf].data_ptr(), slot, out.data_ptr())
 
         def step():
-            buf = state["k"] % 2
+            buf = state["k"] % nbuf
             sid = state["k"] % len(streams)
             state["k"] += 1
             if len(streams) > 1:
@@ -297,7 +310,7 @@ def main():
                 work, pbuf = pending.pop(0)
                 if args.assemble == 2:
                     if work is not None:
-                        work.wait()   # gather of frame k-2: finished during frame k-1
+                        work.wait()   # gather of frame k-depth: ran during the frames since
                     if root:
                         fused = (recv_all[pbuf].data_ptr(), slot, outs[sid].data_ptr())
                 else:
@@ -351,7 +364,10 @@ def main():
     # Launches on two streams overlap, so each one's event-measured duration
     # includes time shared with its neighbour: the per-launch figure the
     # roofline divides by is then the busy span over the launches.
-    span_ms, n_launch = r.launch_span_ms()
+    try:
+        span_ms, n_launch = r.launch_span_ms()
+    except ptamd.PTError:   # launch timing off (--opt 9=0)
+        span_ms, n_launch = float("nan"), 1
     interval_ms = span_ms / max(n_launch, 1)
     if dist is not None:
         t = allreduce_max(torch.tensor([dt, kernel_ms, interval_ms], dtype=torch.float64, device=dev))
@@ -434,6 +450,7 @@ def main():
                          "traffic_source": None if prof is None else prof[0],
                          "kernel": KERNEL_NAMES.get(r.last_kernel(), "?"), "kernel_ms": round(kernel_ms, 4),
                          "launch_interval_ms": round(interval_ms, 4),
+                         "timed_launches": int(kt.size),
                          "time_basis": "launch_interval_ms (busy span / launches; launches overlap on "
                                        f"{args.streams} streams)" if args.streams > 1 else "kernel_ms",
                          "algorithmic_bytes_per_launch": int(own_bytes)},

@@ -354,6 +354,9 @@ struct pt_context {
   hipEvent_t ring[kRing][2] = {};
   int ring_n = 0;
   int last_slot = 0;          // ring slot of the newest launch (pt_last_launch_ms)
+  int opt_timing = 1;         // PT_OPT_LAUNCH_TIMING: event pair on every k-th launch, 0 = none
+  long long launch_n = 0;     // render launches since pt_reset_launch_times
+  long long ring_launch[kRing] = {};   // launch number of each recorded pair
 };
 
 struct pt_scene {
@@ -597,7 +600,8 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   }
   PT_HIP(hipSetDevice(c->device));
   const int slot = c->ring_n % pt_context::kRing;
-  PT_HIP(hipEventRecord(c->ring[slot][0], c->stream));
+  const bool timed = c->opt_timing > 0 && c->launch_n % c->opt_timing == 0;
+  if (timed) PT_HIP(hipEventRecord(c->ring[slot][0], c->stream));
   const bool fits = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
   if (c->opt_scene_lds == 2 && !fits) return fail(PT_ERR_UNSUPPORTED, "scene too large for the LDS variant");
   const bool lds = c->opt_scene_lds == 2 || (c->opt_scene_lds == 1 && fits);
@@ -676,10 +680,14 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   } else {
     PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream));
   }
-  PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
-  c->last_slot = slot;
-  c->ring_n++;
-  c->timed = true;
+  if (timed) {
+    PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
+    c->ring_launch[slot] = c->launch_n;
+    c->last_slot = slot;
+    c->ring_n++;
+    c->timed = true;
+  }
+  c->launch_n++;
   return PT_OK;
 }
 
@@ -1057,6 +1065,10 @@ int pt_set_option(pt_context* c, int key, int value) {
       if (value < 1 || value > 64) return fail(PT_ERR_INVALID, "PT_OPT_SM_BATCH takes 1..64");
       c->opt_sm_batch = value;
       return PT_OK;
+    case PT_OPT_LAUNCH_TIMING:
+      if (value < 0) return fail(PT_ERR_INVALID, "PT_OPT_LAUNCH_TIMING takes 0 (off) or k >= 1 (every k-th launch)");
+      c->opt_timing = value;
+      return PT_OK;
     case PT_OPT_ITEM_ORDER:
       if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_ITEM_ORDER takes 0 or 1");
       c->opt_item_order = value;
@@ -1217,13 +1229,14 @@ int pt_launch_span_ms(pt_context* c, float* ms, size_t* n_out) {
     span = t > span ? t : span;
   }
   *ms = span;
-  *n_out = (size_t)c->ring_n;
+  *n_out = (size_t)(c->ring_launch[c->ring_n - 1] - c->ring_launch[0] + 1);   // launches the span covers
   return PT_OK;
 }
 
 int pt_reset_launch_times(pt_context* c) {
   if (!c) return fail(PT_ERR_INVALID, "null context");
   c->ring_n = 0;
+  c->launch_n = 0;
   return PT_OK;
 }
 

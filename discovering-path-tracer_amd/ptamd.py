@@ -25,6 +25,7 @@ PT_OPT_SM_BATCH = 5
 PT_OPT_PRIMARY_CULL = 6
 PT_OPT_WF_PATHS = 7
 PT_OPT_ITEM_ORDER = 8
+PT_OPT_LAUNCH_TIMING = 9
 KERNEL_AUTO, KERNEL_RECURSIVE, KERNEL_STATE_MACHINE, KERNEL_WAVEFRONT = 0, 1, 2, 3
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).

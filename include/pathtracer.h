@@ -232,6 +232,10 @@ int pt_render_packed(pt_context* ctx, uint32_t n_batches, void* dst_device, cons
  * workgroups start early and short ones fill the tail; 0 = scan order.  The
  * packed exchange layout follows the same order.  Output is identical. */
 #define PT_OPT_ITEM_ORDER 8
+/* PT_OPT_LAUNCH_TIMING: record a HIP event pair around every k-th render
+ * launch (default 1; 0 = none) for pt_last_launch_ms / pt_launch_times_ms /
+ * pt_launch_span_ms.  Output-invariant. */
+#define PT_OPT_LAUNCH_TIMING 9
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */

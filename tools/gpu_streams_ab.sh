@@ -17,6 +17,6 @@ run() {   # name, env, args
 for n in ${RANKS:-1 2 4 8}; do
   for v in ${VARIANTS:-s1:--streams,1 s2:--streams,2}; do
     name=${v%%:*}; args=${v#*:}; args=${args//,/ }
-    if [ $n = 1 ]; then run n1_$name X=1 --packed $args; else run emu${n}_$name PT_BENCH_EMULATE_RANKS=$n $args; fi
+    if [ $n = 1 ]; then run n1_$name X=1 $args; else run emu${n}_$name PT_BENCH_EMULATE_RANKS=$n $args; fi
   done
 done
