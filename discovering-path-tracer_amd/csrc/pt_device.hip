@@ -118,7 +118,7 @@ __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* can
     if (STATS) c.nodes++;
     const int raw = __float_as_int(a.w);
     // bit 31: bounds identical to the parent's, which this ray hit -> hit
-    const bool h = (raw < 0) | slab(o, inv, a, b);   // branch-free: one LDS round trip per node
+    const bool h = slab(o, inv, a, b) || (raw < 0);   // branch-free: one LDS round trip per node
     const int tri = __float_as_int(b.w);
     // slot nc is free: write it unconditionally, keep it only for a hit leaf
     cand[nc * 64] = tri;
@@ -168,7 +168,7 @@ __device__ bool occluded(const RenderParams& P, v3 o, v3 d, float limit, Ctr& c)
     if (STATS) c.nodes++;
     const int raw = __float_as_int(a.w);
     // bit 31: bounds identical to the parent's, which this ray hit -> hit
-    const bool h = (raw < 0) | slab(o, inv, a, b);   // branch-free: one LDS round trip per node
+    const bool h = slab(o, inv, a, b) || (raw < 0);   // branch-free: one LDS round trip per node
     const int tri = __float_as_int(b.w);
     if (h && tri >= 0) {
       if (STATS) c.leaves++;
@@ -1366,7 +1366,7 @@ __device__ __forceinline__ bool wf_lane_step(const RenderParams& P, WfLane& L, i
     nb = P.nodes[2 * L.k + 3];
   }
   const int raw = __float_as_int(L.a.w);
-  const bool h = (raw < 0) | slab(L.o, L.inv, L.a, L.b);
+  const bool h = slab(L.o, L.inv, L.a, L.b) || (raw < 0);
   const int tri = __float_as_int(L.b.w);
   const bool leaf_hit = h && tri >= 0;
   if (L.shadow) {
