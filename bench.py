@@ -97,9 +97,18 @@ def cpu_baseline(v, i, n, cam, light, W, H, spp, DEPTH, SSS):
     _, st = oracle_lib.render(v, i, n.reshape(-1), cam, light, W, H, n_batches=spp, max_depth=DEPTH,
                               sss_bounces=SSS, row_stride=stride, row_phase=0, nthreads=threads)
     dt = time.perf_counter() - t0
+    # the scalar traversal on one core, on every 16th row of those
+    s1 = stride * 16
+    t1 = time.perf_counter()
+    _, st1 = oracle_lib.render(v, i, n.reshape(-1), cam, light, W, H, n_batches=spp, max_depth=DEPTH,
+                               sss_bounces=SSS, row_stride=s1, row_phase=0, nthreads=1)
+    dt1 = time.perf_counter() - t1
     return {"value": round(float(st[0]) / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"rows y%{stride}==0 of the same {W}x{H}x{spp}spp frame ({H // stride} rows, "
-                      f"{int(st[0])} rays, {dt:.2f} s, {threads} std::threads, oracle/pt_oracle.cpp)"}
+                      f"{int(st[0])} rays, {dt:.2f} s, {threads} std::threads, oracle/pt_oracle.cpp)",
+            "host_cpus_visible": os.cpu_count(),
+            "single_thread": {"value": round(float(st1[0]) / dt1 / 1e6, 3), "unit": "Mrays/s", "cores": 1,
+                              "sample": f"rows y%{s1}==0 ({int(st1[0])} rays, {dt1:.2f} s)"}}
 
 
 KERNEL_NAMES = {1: "render_kernel<false,*>", 2: "render_sm_kernel<false,*>",
