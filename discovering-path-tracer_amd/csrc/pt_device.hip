@@ -192,6 +192,61 @@ __device__ bool occluded(const RenderParams& P, v3 o, v3 d, float limit, Ctr& c)
   return occ;
 }
 
+// An occlusion query S and a closest-hit walk C, interleaved one node each per
+// iteration: each walker visits exactly the node sequence of occluded() /
+// trace_closest() above, with the same tests, candidate queue and strict '<',
+// so both results are theirs bit for bit.  Interleaving only puts two
+// independent node round trips in flight per lane -- the walks are bound by
+// that latency (LDS or L2), not by issue.  has_s / has_c switch a walker off
+// (it starts finished).  Fast kernels only: stats mode walks one ray at a time.
+__device__ __forceinline__ void walk_pair(const RenderParams& P, bool has_s, v3 so, v3 sd, float limit, bool* occ,
+                                          bool has_c, v3 co, v3 cd, int* cand, Hit* hit) {
+  const int n = P.n_nodes;
+  const v3 sinv = mk(rcp_(sd.x), rcp_(sd.y), rcp_(sd.z));
+  const v3 cinv = mk(rcp_(cd.x), rcp_(cd.y), rcp_(cd.z));
+  int ks = has_s ? 0 : n, kc = has_c ? 0 : n;
+  bool oc = false;
+  float best = 1e30f;
+  int bt = -1, nc = 0;
+  while (ks < n || kc < n) {
+    // both loads first (a finished walker re-reads node 0, unused)
+    const int ls = ks < n ? ks : 0, lc = kc < n ? kc : 0;
+    const float4 sa = P.nodes[2 * ls], sb = P.nodes[2 * ls + 1];
+    const float4 ca = P.nodes[2 * lc], cb = P.nodes[2 * lc + 1];
+    if (ks < n) {
+      const int raw = __float_as_int(sa.w);
+      const bool h = slab(so, sinv, sa, sb) || (raw < 0);
+      const int tri = __float_as_int(sb.w);
+      int next = (h && tri < 0) ? ks + 1 : (raw & 0x7fffffff);
+      if (h && tri >= 0) {
+        const float4* T = P.tris + 3 * tri;
+        float t;
+        if (tri_test(so, sd, T[0], T[1], T[2], &t) && t < 1e30f && !(t >= limit)) {
+          oc = true;
+          next = n;
+        }
+      }
+      ks = next;
+    }
+    if (kc < n) {
+      const int raw = __float_as_int(ca.w);
+      const bool h = slab(co, cinv, ca, cb) || (raw < 0);
+      const int tri = __float_as_int(cb.w);
+      cand[nc * 64] = tri;
+      nc += (h && tri >= 0) ? 1 : 0;
+      if (nc == kCand) {
+        test_candidates(P, co, cd, cand, nc, &best, &bt);
+        nc = 0;
+      }
+      kc = (h && tri < 0) ? kc + 1 : (raw & 0x7fffffff);
+    }
+  }
+  test_candidates(P, co, cd, cand, nc, &best, &bt);
+  *occ = oc;
+  hit->t = best;
+  hit->tri = bt;
+}
+
 // Lights are read-only for the whole launch and indexed by a wave-uniform
 // loop counter: reading them through the constant address space lets the
 // compiler use scalar loads (scalar cache, one load per wave) instead of a
@@ -373,6 +428,129 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
   return rad;
 }
 
+
+// pathTrace (:300-418) for the fast kernels, with every shadow ray that has an
+// independent closest-hit ray next to it walked as a pair (walk_pair): the
+// last light's shadow ray of the direct term with the first SSS ray, and each
+// SSS step's last shadow ray with the next SSS ray.  The RNG draws, the float
+// operations and their order are path_trace's: a shadow result is only used
+// after the pair returns, to finish the same sums in the same order.
+template <bool PF>
+__device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, int* cand) {
+  const float OFFSET = 0.001f;
+  Ctr c = {0u, 0u, 0u};
+  v3 thr = mk(1.0f, 1.0f, 1.0f);
+  v3 rad = mk(0.0f, 0.0f, 0.0f);
+  uint32_t rng = seed;                                  // :307 re-seed
+  const int NL = P.n_lights;
+
+  Hit h0;
+  h0.t = 1e30f;
+  h0.tri = -1;
+  bool have_h0 = false;
+  for (int i = 0; i < NL; ++i) {                        // :311-328
+    const LightDev L = load_light(P, i);
+    float tl;
+    if (intersect_area_light(ro, rd, L, &tl)) {
+      if (!have_h0) {
+        h0 = trace_closest<false, PF>(P, ro, rd, c, cand);
+        have_h0 = true;
+      }
+      if (h0.tri < 0 || h0.t > tl) return mk(L.inten[0], L.inten[1], L.inten[2]);
+    }
+  }
+
+  const v3 albedo = mk(0.8f, 0.8f, 0.8f);
+  const v3 sss_albedo = mk(1.0f, 0.2f, 0.1f);           // :371-408
+  const float sss_radius = 1.0f;
+  for (int depth = 0; depth < P.max_depth; ++depth) {   // :331
+    Hit h;
+    if (depth == 0) {
+      if (!have_h0) {
+        h0 = trace_closest<false, PF>(P, ro, rd, c, cand);
+        have_h0 = true;
+      }
+      h = h0;
+    } else {
+      h = trace_closest<false, PF>(P, ro, rd, c, cand);
+    }
+    if (h.tri < 0) {
+      rad = add(rad, mul(thr, mk(0.0f, 0.0f, 0.0f)));  // background (:336)
+      break;
+    }
+    const v3 hp = add(ro, muls(rd, h.t));               // :188
+    const v3 hn = tri_normal(P, h.tri);                 // :189
+
+    // direct light (:345-366); the last light's shadow ray is deferred
+    v3 direct = mk(0.0f, 0.0f, 0.0f);
+    v3 s_o = hp, s_d = hp, s_c = hp;   // deferred shadow ray: origin, dir, contribution if visible
+    float s_lim = 0.0f;
+    for (int i = 0; i < NL; ++i) {
+      const LightDev L = load_light(P, i);
+      const v3 lp = sample_area_light(L, &rng);
+      const v3 ld = normalize(sub(lp, hp));
+      const float diff = fmax_(dot(hn, ld), 0.0f);
+      const float dist = length(sub(lp, hp));
+      const float d2 = dist * dist;
+      const v3 contrib = mul(albedo, muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), rcp_(fmax_(d2, 0.01f))));
+      if (i + 1 < NL) {
+        if (!occluded<false, PF>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c)) direct = add(direct, contrib);
+      } else {
+        s_o = add(hp, muls(hn, OFFSET));
+        s_d = ld;
+        s_lim = dist - OFFSET;
+        s_c = contrib;
+      }
+    }
+    v3 sss_thr = mk(1.0f, 1.0f, 1.0f);
+    v3 so = sub(hp, muls(hn, OFFSET));
+    v3 sd = sample_sphere(&rng);
+    Hit sh;
+    bool occ = false;
+    walk_pair(P, NL > 0, s_o, s_d, s_lim, &occ, P.sss_bounces > 0, so, sd, cand, &sh);
+    if (NL > 0 && !occ) direct = add(direct, s_c);
+    rad = add(rad, mul(thr, direct));
+
+    for (int k = 0; k < P.sss_bounces; ++k) {
+      if (sh.tri < 0) break;
+      const float travel = sh.t;
+      const v3 cp = add(so, muls(sd, travel));
+      const v3 sn = tri_normal(P, sh.tri);
+      v3 sl = mk(0.0f, 0.0f, 0.0f);
+      for (int i = 0; i < NL; ++i) {
+        const LightDev L = load_light(P, i);
+        const v3 lp = sample_area_light(L, &rng);
+        const v3 ed = normalize(sub(lp, cp));
+        const float ediff = fmax_(dot(sn, ed), 0.0f);
+        const float edist = length(sub(lp, cp));
+        const float d2 = edist * edist;
+        const v3 term = muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])),
+                             rcp_(fmax_(d2, 0.01f)));
+        if (i + 1 < NL) {
+          if (!occluded<false, PF>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c)) sl = add(sl, term);
+        } else {
+          s_o = add(cp, muls(sn, OFFSET));
+          s_d = ed;
+          s_lim = edist - OFFSET;
+          s_c = term;
+        }
+      }
+      const v3 thr_k = mul(thr, sss_thr);
+      sss_thr = mul(sss_thr, muls(sss_albedo, exp_(-travel / (sss_radius * 1.5f))));
+      so = sub(cp, muls(sn, OFFSET));
+      sd = sample_sphere(&rng);
+      walk_pair(P, NL > 0, s_o, s_d, s_lim, &occ, k + 1 < P.sss_bounces, so, sd, cand, &sh);
+      if (NL > 0 && !occ) sl = add(sl, s_c);
+      rad = add(rad, muls(mul(thr_k, sl), 1.0f + sss_radius * 0.5f));
+    }
+
+    const v3 bd = sample_hemisphere(hn, &rng);          // :411-414
+    thr = mul(thr, muls(albedo, dot(hn, bd)));
+    ro = add(hp, muls(hn, OFFSET));
+    rd = bd;
+  }
+  return rad;
+}
 
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #pragma unroll
@@ -624,7 +802,15 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
       // PF (prefetch node k+1) for walks from device memory; on an LDS-staged
       // scene it measured slower at every tile share (1080p box: +7 % on a
       // whole frame, +12 % on a 1/8 share: registers)
-      const v3 col = path_trace<STATS, !LDS>(P, origin, dir, seed, c, cand);
+      // Scenes walked from device memory pair each shadow ray with the next
+      // closest-hit ray (path_trace_fused: two node round trips in flight,
+      // sphere 20K tris -9 %); on an LDS-staged scene the round trip is short
+      // and the pair's registers cost more than it hides (box +11 %).
+      v3 col;
+      if (STATS || LDS)
+        col = path_trace<STATS, !LDS>(P, origin, dir, seed, c, cand);
+      else
+        col = path_trace_fused<true>(P, origin, dir, seed, cand);
       col4 = make_float4(col.x, col.y, col.z, 1.0f);                      // vec4(color, 1.0)
      }
      // hand the chunk's colours to the folding lanes of the same pixel
