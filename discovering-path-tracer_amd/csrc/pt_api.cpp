@@ -610,11 +610,17 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   // 8 spp 1022 vs 596 ms, 1M-triangle cloud 1 spp 191 vs 127 ms).
   const bool sm = c->opt_kernel == 2;
   // auto: the wavefront pipeline for scenes of at least kWfAutoTris triangles
-  // (not LDS-resident), the path-recursive kernel otherwise.  Measured at
-  // 1080p 8 spp (ms, recursive -> wavefront): displaced sphere 5K tris
-  // 39.5 -> 58.4, 20K 67 -> 72, 82K 560 -> 465; random cloud 100K 130 -> 76,
-  // 1M 923 -> 833; 10M (1 spp) 719 -> 667; box 0.38 -> 8.4.
-  const bool wf = c->opt_kernel == 3 || (c->opt_kernel == 0 && !lds && !c->stats_mode && c->n_tris >= kWfAutoTris);
+  // (not LDS-resident) when the launch holds enough paths to keep its node
+  // loads in flight, the path-recursive kernel otherwise.  Measured at 1080p
+  // (ms, recursive with paired walks -> wavefront): 1 spp (2M paths):
+  // displaced sphere 82K tris 101 -> 108, 10M cloud 735 -> 669; 8 spp (16.6M):
+  // sphere 550 -> 465, 100K cloud 113 -> 77; 1M cloud 2 spp 225 -> 236; a 1/8
+  // tile share of the 10M cloud: 1 spp (259K paths) 147 -> 273, 8 spp (2M)
+  // 742 -> 669; box 0.38 -> 8.4.
+  const long long paths = (long long)((p.blocks_total + p.nranks - 1 - p.rank) / p.nranks) * 256 * n_batches;
+  const bool wf_auto = c->n_tris >= kWfAutoTris && paths >= (1ll << 20) &&
+                       (c->n_tris >= (1 << 20) || paths >= (1ll << 23));
+  const bool wf = c->opt_kernel == 3 || (c->opt_kernel == 0 && !lds && !c->stats_mode && wf_auto);
   if (wf && c->stats_mode) return fail(PT_ERR_UNSUPPORTED, "stats mode runs the path-recursive kernel only");
   if (sm) p.spl = 1;
   p.n_cull = -1;

@@ -250,14 +250,17 @@ def test_random_triangles(ntri, int_bits):
     _assert_same(gpu, ref, f"random {ntri}")
 
 
-def test_grid_ties_and_two_lights():
+@pytest.mark.parametrize("lds", [0, 1])
+def test_grid_ties_and_two_lights(lds):
+    """lds=0 walks from device memory with paired shadow/closest walks: the
+    first light's shadow rays single, the second's paired."""
     gv, gi = scenes.grid_mesh(6)
     s = ptamd.Scene.from_arrays(gv, gi).build_bvh()
     v, i, n, _, _ = s.arrays()
     lights = np.concatenate([scenes.REFERENCE_LIGHT,
                              ptamd.pack_light([0.5, 0.5, 1.5], [0, 0, -1], [2, 4, 8], [0.5, 1.0])])
     cam = scenes.camera((0.0, 0.0, 3.0))
-    r = _setup(v, i, n, cam=cam, lights=lights, depth=3, sss=2)
+    r = _setup(v, i, n, cam=cam, lights=lights, depth=3, sss=2, lds=lds)
     r.resize_and_clear(64, 64)
     r.render(3, 2)
     gpu = r.read_accum()
@@ -265,11 +268,12 @@ def test_grid_ties_and_two_lights():
     _assert_same(gpu, ref, "grid")
 
 
-def test_edge_params():
+@pytest.mark.parametrize("lds", [0, 1])
+def test_edge_params(lds):
     v, i, n = _box()
     for depth, sss, lights in [(0, 3, scenes.REFERENCE_LIGHT), (4, 0, scenes.REFERENCE_LIGHT),
-                               (2, 1, np.zeros(0, np.float32))]:
-        r = _setup(v, i, n, depth=depth, sss=sss, lights=lights)
+                               (2, 1, np.zeros(0, np.float32)), (3, 1, scenes.REFERENCE_LIGHT)]:
+        r = _setup(v, i, n, depth=depth, sss=sss, lights=lights, lds=lds)
         r.resize_and_clear(48, 40)
         r.render(0, 2)
         ref, _ = _oracle(v, i, n, 48, 40, nb=2, depth=depth, sss=sss, lights=lights)
