@@ -29,7 +29,8 @@ struct LightRec {          // == pt_area_light / AreaLightData
 
 // Light with its sampling frame precomputed on the device (setup_lights_kernel).
 struct LightDev {
-  float pos[3], nraw[3], inten[3], right[3], up[3], size[2], half[2], pad;
+  float pos[3], nraw[3], inten[3], right[3], up[3], size[2], half[2];
+  float finite;   // 1 when every intensity channel is finite (shadow_needed)
 };
 
 // Partition order of the 16x16 blocks: tile b is block row by = b / blocks_x,

@@ -265,6 +265,17 @@ __device__ __forceinline__ LightDev load_light(const RenderParams& P, int i) {
 #endif
 }
 
+// Whether a shadow ray's answer can change the image.  Its light term is
+// I * diff * rcp(max(d2, 0.01)) (:352-363, :392-402).  When diff = max(dot, 0)
+// is 0 and I is finite, every channel of the term is +-0, and adding +-0 to
+// the running sum (direct / sssLight, which start at +0 and so are never -0)
+// leaves it bitwise unchanged: occluded or not, the result is the same, so the
+// fast kernels skip the walk.  (The RNG draws for the light sample are made
+// before, as in the reference.)  Stats mode still walks every shadow ray.
+__device__ __forceinline__ bool shadow_needed(const LightDev& L, float diff) {
+  return diff != 0.0f || L.finite == 0.0f;
+}
+
 // sampleAreaLight (:255-268); the light's frame (:261-264) is precomputed per
 // light by setup_lights_kernel with the same ops.
 __device__ __forceinline__ v3 sample_area_light(const LightDev& L, uint32_t* rng) {
@@ -382,7 +393,7 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
       const v3 ld = normalize(sub(lp, hp));
       const float diff = fmax_(dot(hn, ld), 0.0f);
       const float dist = length(sub(lp, hp));
-      if (!occluded<STATS, PF>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c)) {
+      if ((!STATS && !shadow_needed(L, diff)) || !occluded<STATS, PF>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c)) {
         const float d2 = dist * dist;
         const v3 contrib = muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), rcp_(fmax_(d2, 0.01f)));
         direct = add(direct, mul(albedo, contrib));
@@ -408,7 +419,7 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
         const v3 ed = normalize(sub(lp, cp));
         const float ediff = fmax_(dot(sn, ed), 0.0f);
         const float edist = length(sub(lp, cp));
-        if (!occluded<STATS, PF>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c)) {
+        if ((!STATS && !shadow_needed(L, ediff)) || !occluded<STATS, PF>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c)) {
           const float d2 = edist * edist;
           sl = add(sl, muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])),
                             rcp_(fmax_(d2, 0.01f))));
@@ -485,6 +496,7 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
     v3 direct = mk(0.0f, 0.0f, 0.0f);
     v3 s_o = hp, s_d = hp, s_c = hp;   // deferred shadow ray: origin, dir, contribution if visible
     float s_lim = 0.0f;
+    bool s_need = false;   // the deferred shadow ray can change the image (shadow_needed)
     for (int i = 0; i < NL; ++i) {
       const LightDev L = load_light(P, i);
       const v3 lp = sample_area_light(L, &rng);
@@ -494,8 +506,10 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
       const float d2 = dist * dist;
       const v3 contrib = mul(albedo, muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), rcp_(fmax_(d2, 0.01f))));
       if (i + 1 < NL) {
-        if (!occluded<false, PF>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c)) direct = add(direct, contrib);
+        if (!shadow_needed(L, diff) || !occluded<false, PF>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c))
+          direct = add(direct, contrib);
       } else {
+        s_need = shadow_needed(L, diff);
         s_o = add(hp, muls(hn, OFFSET));
         s_d = ld;
         s_lim = dist - OFFSET;
@@ -507,7 +521,7 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
     v3 sd = sample_sphere(&rng);
     Hit sh;
     bool occ = false;
-    walk_pair(P, NL > 0, s_o, s_d, s_lim, &occ, P.sss_bounces > 0, so, sd, cand, &sh);
+    walk_pair(P, NL > 0 && s_need, s_o, s_d, s_lim, &occ, P.sss_bounces > 0, so, sd, cand, &sh);
     if (NL > 0 && !occ) direct = add(direct, s_c);
     rad = add(rad, mul(thr, direct));
 
@@ -527,8 +541,10 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
         const v3 term = muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])),
                              rcp_(fmax_(d2, 0.01f)));
         if (i + 1 < NL) {
-          if (!occluded<false, PF>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c)) sl = add(sl, term);
+          if (!shadow_needed(L, ediff) || !occluded<false, PF>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c))
+            sl = add(sl, term);
         } else {
+          s_need = shadow_needed(L, ediff);
           s_o = add(cp, muls(sn, OFFSET));
           s_d = ed;
           s_lim = edist - OFFSET;
@@ -539,7 +555,7 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
       sss_thr = mul(sss_thr, muls(sss_albedo, exp_(-travel / (sss_radius * 1.5f))));
       so = sub(cp, muls(sn, OFFSET));
       sd = sample_sphere(&rng);
-      walk_pair(P, NL > 0, s_o, s_d, s_lim, &occ, k + 1 < P.sss_bounces, so, sd, cand, &sh);
+      walk_pair(P, NL > 0 && s_need, s_o, s_d, s_lim, &occ, k + 1 < P.sss_bounces, so, sd, cand, &sh);
       if (NL > 0 && !occ) sl = add(sl, s_c);
       rad = add(rad, muls(mul(thr_k, sl), 1.0f + sss_radius * 0.5f));
     }
@@ -887,7 +903,8 @@ __global__ __launch_bounds__(64) void setup_lights_kernel(const LightRec* __rest
   d.size[1] = L.size[1];
   d.half[0] = L.size[0] * 0.5f;
   d.half[1] = L.size[1] * 0.5f;
-  d.pad = 0.0f;
+  d.finite = (__builtin_isfinite(d.inten[0]) && __builtin_isfinite(d.inten[1]) && __builtin_isfinite(d.inten[2]))
+                 ? 1.0f : 0.0f;
   out[i] = d;
 }
 
