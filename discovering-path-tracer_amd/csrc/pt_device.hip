@@ -1055,6 +1055,16 @@ __device__ __forceinline__ void trav_start(Trav& T, v3 o, v3 d, bool shadow, flo
   T.cl = 0u;
 }
 
+// A shadow query whose answer cannot change the image (shadow_needed): it is
+// still handed out as a ray, so the path keeps its place in the ray rounds
+// (the wavefront lists stay phase-aligned, neighbouring paths coherent), but
+// it starts finished, unoccluded: no node is visited.  Skipping it inside
+// path_step instead measured +3 % on the displaced sphere (paths drift apart).
+__device__ __forceinline__ void trav_null(const RenderParams& P, Trav& T) {
+  T.k = P.n_nodes;
+  T.shadow = 2;
+}
+
 // One node of the walk; returns true when the ray is finished.
 template <bool STATS>
 __device__ __forceinline__ bool trav_step(const RenderParams& P, Trav& T, int* cand) {
@@ -1220,8 +1230,9 @@ __device__ bool path_step(const RenderParams& P, const CamFrame& F, PathSt& S, T
           const float dist = length(sub(lp, S.hp));
           const float d2 = dist * dist;
           S.pend = muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), rcp_(fmax_(d2, 0.01f)));
-          trav_start(T, add(S.hp, muls(S.hn, OFFSET)), ld, true, dist - OFFSET);
           S.k = 0;
+          trav_start(T, add(S.hp, muls(S.hn, OFFSET)), ld, true, dist - OFFSET);
+          if (!STATS && !shadow_needed(L, diff)) trav_null(P, T);
           return true;
         }
         S.rad = add(S.rad, mul(S.thr, S.acc3));
@@ -1256,6 +1267,7 @@ __device__ bool path_step(const RenderParams& P, const CamFrame& F, PathSt& S, T
           const float d2 = edist * edist;
           S.pend = muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])), rcp_(fmax_(d2, 0.01f)));
           trav_start(T, add(S.cp, muls(S.sn, OFFSET)), ed, true, edist - OFFSET);
+          if (!STATS && !shadow_needed(L, ediff)) trav_null(P, T);
           return true;
         }
         continue;
@@ -1275,6 +1287,7 @@ __device__ bool path_step(const RenderParams& P, const CamFrame& F, PathSt& S, T
           const float d2 = edist * edist;
           S.pend = muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])), rcp_(fmax_(d2, 0.01f)));
           trav_start(T, add(S.cp, muls(S.sn, OFFSET)), ed, true, edist - OFFSET);
+          if (!STATS && !shadow_needed(L, ediff)) trav_null(P, T);
           return true;
         }
         S.rad = add(S.rad, muls(mul(mul(S.thr, S.sss_thr), S.acc3), 1.0f + sss_radius * 0.5f));
@@ -1540,16 +1553,17 @@ struct WfLane {
   float lim;
 };
 
-__device__ __forceinline__ void wf_lane_start(const float4* __restrict__ ray, float4 root_a, float4 root_b,
-                                              WfLane& L) {
+__device__ __forceinline__ void wf_lane_start(const RenderParams& P, const float4* __restrict__ ray, float4 root_a,
+                                              float4 root_b, WfLane& L) {
   const float4 r0 = ray[0], r1 = ray[1];
   L.o = mk(r0.x, r0.y, r0.z);
   L.d = mk(r1.x, r1.y, r1.z);
   L.inv = mk(rcp_(L.d.x), rcp_(L.d.y), rcp_(L.d.z));
-  L.shadow = __float_as_int(r1.w);
+  const int kind = __float_as_int(r1.w);   // 0 closest, 1 shadow, 2 null shadow (trav_null)
+  L.shadow = kind ? 1 : 0;
   L.lim = L.shadow ? r0.w : 1e30f;
   L.res = L.shadow ? 0 : -1;
-  L.k = 0;
+  L.k = kind == 2 ? P.n_nodes : 0;
   L.nc = 0;
   L.a = root_a;
   L.b = root_b;
@@ -1675,7 +1689,7 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
         const int slot = base + (int)__popcll(gm & ((1ull << lead) - 1ull)) * PT_WF_GROUP + (lane - lead);
         if (slot < count) {
           p = slot;
-          wf_lane_start(rays + 2 * (size_t)slot, root_a, root_b, L);
+          wf_lane_start(P, rays + 2 * (size_t)slot, root_a, root_b, L);
         }
       }
     }
