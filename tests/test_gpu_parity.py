@@ -559,3 +559,30 @@ def test_wavefront_rejects_stats_mode():
     r.resize_and_clear(16, 16)
     with pytest.raises(ptamd.PTError):
         r.render(0, 1)
+
+
+# ---- shadow rays skipped when their answer cannot change the image ---------
+@pytest.mark.parametrize("lds", [0, 1])
+@pytest.mark.parametrize("kernel", [1, 2, 3])
+def test_shadow_skip_light_intensities(lds, kernel):
+    """shadow_needed: a light term with diff = 0 is +-0 only for a finite
+    intensity.  A negative intensity (terms -0: skipped) and an infinite one
+    (inf * 0 = NaN: must be traced) next to the reference light, on every
+    kernel.  NaNs are compared as NaN (their sign/payload is the platform's);
+    every other float bitwise."""
+    v, i, n = _box()
+    lights = np.concatenate([scenes.REFERENCE_LIGHT,
+                             ptamd.pack_light([2.5, 0.5, 0.0], [-1, 0, 0], [-3.0, 0.5, 2.0], [1.0, 1.0]),
+                             ptamd.pack_light([-2.5, 0.0, 0.5], [1, 0, 0], [np.inf, 1.0, 0.25], [0.5, 0.5])])
+    cam = scenes.camera((0.5, 1.5, 3.5))
+    r = _setup(v, i, n, cam=cam, lights=lights, lds=lds)
+    r.set_option(ptamd.PT_OPT_KERNEL, kernel)
+    r.resize_and_clear(40, 32)
+    r.render(0, 3)
+    gpu = r.read_accum()
+    ref, _ = _oracle(v, i, n, 40, 32, nb=3, cam=cam, lights=lights)
+    nan_g, nan_r = np.isnan(gpu), np.isnan(ref)
+    assert np.array_equal(nan_g, nan_r), f"NaN pattern differs in {np.count_nonzero(nan_g != nan_r)} floats"
+    assert nan_r.any() and (~nan_r).any()
+    _assert_same(np.where(nan_g, 0, gpu).astype(np.float32), np.where(nan_r, 0, ref).astype(np.float32),
+                 f"kernel {kernel} lds {lds}")
