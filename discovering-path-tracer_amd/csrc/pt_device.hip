@@ -79,7 +79,10 @@ __device__ __forceinline__ bool tri_test(v3 o, v3 d, float4 A, float4 B, float4 
 // in a wave whose lanes pass different leaves the triangle test then runs
 // max-over-lanes times instead of once per leaf any lane passed.  Candidates
 // are tested in visit order with the same strict '<', so the hit is the same.
-constexpr int kCand = 8;
+#ifndef PT_KCAND
+#define PT_KCAND 8
+#endif
+constexpr int kCand = PT_KCAND;
 
 // PF (prefetch): load node k+1 while node k is being tested — it is the next
 // visit whenever k is a hit internal node or a leaf (the node arrays carry one
@@ -340,12 +343,53 @@ __device__ __forceinline__ void add_ctr(Ctr& a, const Ctr& b) {
   a.leaves += b.leaves;
 }
 
+// LDS-staged scenes park path state in LDS during walks (PT_PARK) and run 6
+// waves per SIMD (80 VGPRs, 2 spilled) instead of 5 (96): box 1080p8 -3.8 %.
+// 7 waves spill 19 VGPRs and gain nothing; parking at 5 waves costs +1.7 %.
+#ifndef PT_PARK
+#define PT_PARK 1
+#endif
+constexpr int kPark = PT_PARK ? 12 : 0;   // floats of path state parked in LDS around a walk
+__device__ __forceinline__ void park3(float* pk, int i, v3 v) {
+  pk[i * 64] = v.x;
+  pk[(i + 1) * 64] = v.y;
+  pk[(i + 2) * 64] = v.z;
+}
+__device__ __forceinline__ v3 unpark3(const float* pk, int i) {
+  return mk(pk[i * 64], pk[(i + 1) * 64], pk[(i + 2) * 64]);
+}
+// PARK: the path state a walk does not read (throughput, radiance, hit
+// point and normal) waits in this lane's LDS column during the walk, so the
+// walk's registers peak lower.  The empty asm with a memory clobber keeps the
+// compiler from forwarding the stored values past the walk.
+#define PT_WALK2(PARK, stmt)                                                         \
+  do {                                                                               \
+    if (PARK) { park3(pk, 0, thr); park3(pk, 3, rad); __asm__ volatile("" ::: "memory"); } \
+    stmt;                                                                            \
+    if (PARK) { __asm__ volatile("" ::: "memory"); thr = unpark3(pk, 0); rad = unpark3(pk, 3); } \
+  } while (0)
+#define PT_WALK4(PARK, stmt)                                                         \
+  do {                                                                               \
+    if (PARK) {                                                                      \
+      park3(pk, 0, thr); park3(pk, 3, rad); park3(pk, 6, hp); park3(pk, 9, hn);      \
+      __asm__ volatile("" ::: "memory");                                             \
+    }                                                                                \
+    stmt;                                                                            \
+    if (PARK) {                                                                      \
+      __asm__ volatile("" ::: "memory");                                             \
+      thr = unpark3(pk, 0); rad = unpark3(pk, 3); hp = unpark3(pk, 6); hn = unpark3(pk, 9); \
+    }                                                                                \
+  } while (0)
+
 // pathTrace (:300-418)
 template <bool STATS, bool PF>
 __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr& c, int* cand) {
+  constexpr bool PARK = PT_PARK && !STATS && !PF;
+  float* pk = (float*)(cand + kCand * 64);
   const float OFFSET = 0.001f;
   v3 thr = mk(1.0f, 1.0f, 1.0f);
   v3 rad = mk(0.0f, 0.0f, 0.0f);
+  v3 hp, hn;
   uint32_t rng = seed;                                  // :307 re-seed
 
   Hit h0;
@@ -376,14 +420,14 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
       if (STATS) add_ctr(c, c0);
       h = h0;
     } else {
-      h = trace_closest<STATS, PF>(P, ro, rd, c, cand);
+      PT_WALK2(PARK, h = (trace_closest<STATS, PF>(P, ro, rd, c, cand)));
     }
     if (h.tri < 0) {
       rad = add(rad, mul(thr, mk(0.0f, 0.0f, 0.0f)));  // background (:336)
       break;
     }
-    const v3 hp = add(ro, muls(rd, h.t));               // :188
-    const v3 hn = tri_normal(P, h.tri);                 // :189
+    hp = add(ro, muls(rd, h.t));                        // :188
+    hn = tri_normal(P, h.tri);                          // :189
 
     const v3 albedo = mk(0.8f, 0.8f, 0.8f);
     v3 direct = mk(0.0f, 0.0f, 0.0f);
@@ -393,7 +437,9 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
       const v3 ld = normalize(sub(lp, hp));
       const float diff = fmax_(dot(hn, ld), 0.0f);
       const float dist = length(sub(lp, hp));
-      if ((!STATS && !shadow_needed(L, diff)) || !occluded<STATS, PF>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c)) {
+      bool vis = !STATS && !shadow_needed(L, diff);
+      if (!vis) PT_WALK4(PARK, vis = !(occluded<STATS, PF>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c)));
+      if (vis) {
         const float d2 = dist * dist;
         const v3 contrib = muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), rcp_(fmax_(d2, 0.01f)));
         direct = add(direct, mul(albedo, contrib));
@@ -407,7 +453,8 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
     v3 so = sub(hp, muls(hn, OFFSET));
     v3 sd = sample_sphere(&rng);
     for (int k = 0; k < P.sss_bounces; ++k) {
-      const Hit sh = trace_closest<STATS, PF>(P, so, sd, c, cand);
+      Hit sh;
+      PT_WALK4(PARK, sh = (trace_closest<STATS, PF>(P, so, sd, c, cand)));
       if (sh.tri < 0) break;
       const float travel = sh.t;
       const v3 cp = add(so, muls(sd, travel));
@@ -419,7 +466,9 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
         const v3 ed = normalize(sub(lp, cp));
         const float ediff = fmax_(dot(sn, ed), 0.0f);
         const float edist = length(sub(lp, cp));
-        if ((!STATS && !shadow_needed(L, ediff)) || !occluded<STATS, PF>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c)) {
+        bool vis = !STATS && !shadow_needed(L, ediff);
+        if (!vis) PT_WALK4(PARK, vis = !(occluded<STATS, PF>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c)));
+        if (vis) {
           const float d2 = edist * edist;
           sl = add(sl, muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])),
                             rcp_(fmax_(d2, 0.01f))));
@@ -686,7 +735,11 @@ template <bool STATS, bool LDS>
 #ifndef PT_RENDER_MIN_BLOCKS
 #define PT_RENDER_MIN_BLOCKS 5
 #endif
-__global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(RenderParams P) {
+#ifndef PT_RENDER_MIN_BLOCKS_LDS
+#define PT_RENDER_MIN_BLOCKS_LDS (PT_PARK ? 6 : PT_RENDER_MIN_BLOCKS)
+#endif
+__global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_RENDER_MIN_BLOCKS) void render_kernel(
+    RenderParams P) {
   const int tid = (int)threadIdx.x;
   // Work mapping.  A 16x16 pixel tile (the partition unit) is split into
   // SPL workgroups; lane l of wave w handles pixel q = w*(64/SPL) + l/SPL of
@@ -710,9 +763,12 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
   const int tile = (item / spl) * P.nranks + P.rank;
   const int part = item % spl;
   const int wave = tid >> 6, lane = tid & 63;
-  __shared__ int cand_buf[4][kCand][64];
-  __shared__ float4 col_buf[4][64];
+  // per wave: the leaf-candidate queue, then a [slot][lane] area that holds
+  // the path state parked during walks (kPark floats) and, between samples,
+  // the colour hand-off (4 floats) -- never both at once
+  __shared__ int cand_buf[4][kCand + (kPark > 4 ? kPark : 4)][64];
   int* cand = &cand_buf[wave][0][lane];
+  float* colw = (float*)&cand_buf[wave][kCand][0];   // colour hand-off, [channel][lane]
   const int q = wave * (64 / spl) + lane / spl;       // pixel within the workgroup
   const int j = lane % spl;                           // sample slot
   int bx, by;
@@ -830,7 +886,10 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
       col4 = make_float4(col.x, col.y, col.z, 1.0f);                      // vec4(color, 1.0)
      }
      // hand the chunk's colours to the folding lanes of the same pixel
-     col_buf[wave][lane] = col4;
+     colw[lane] = col4.x;
+     colw[64 + lane] = col4.y;
+     colw[128 + lane] = col4.z;
+     colw[192 + lane] = col4.w;
      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
      __builtin_amdgcn_wave_barrier();
      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -840,10 +899,10 @@ __global__ __launch_bounds__(256, PT_RENDER_MIN_BLOCKS) void render_kernel(Rende
       for (uint32_t t = 0; t < m; ++t) {
         const uint32_t batch = P.first_batch + base + t;
         const float fb = (float)batch, fb1 = (float)(batch + 1u);          // :468
-        const float* cc = (const float*)&col_buf[wave][first_lane + (int)t];
+        const float* cc = colw + first_lane + (int)t;
 #pragma unroll
         for (int ch = 0; ch < 4; ++ch)
-          if (ch % spl == j) acc[ch] = (acc[ch] * fb + cc[ch]) / fb1;
+          if (ch % spl == j) acc[ch] = (acc[ch] * fb + cc[ch * 64]) / fb1;
       }
      }
      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
