@@ -349,7 +349,13 @@ __device__ __forceinline__ void add_ctr(Ctr& a, const Ctr& b) {
 #ifndef PT_PARK
 #define PT_PARK 1
 #endif
-constexpr int kPark = PT_PARK ? 12 : 0;   // floats of path state parked in LDS around a walk
+// Parking in the paired walks of device-memory scenes (38 instead of 45
+// spilled VGPRs) measured neutral (sphere 5K tris +-0.3 %, 20K cloud -0.8 %):
+// off by default.
+#ifndef PT_PARK_FUSED
+#define PT_PARK_FUSED 0
+#endif
+constexpr int kPark = (PT_PARK || PT_PARK_FUSED) ? 12 : 0;   // floats of path state parked in LDS around a walk
 __device__ __forceinline__ void park3(float* pk, int i, v3 v) {
   pk[i * 64] = v.x;
   pk[(i + 1) * 64] = v.y;
@@ -497,10 +503,13 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
 // after the pair returns, to finish the same sums in the same order.
 template <bool PF>
 __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, int* cand) {
+  constexpr bool PARK = PT_PARK_FUSED != 0;
+  float* pk = (float*)(cand + kCand * 64);
   const float OFFSET = 0.001f;
   Ctr c = {0u, 0u, 0u};
   v3 thr = mk(1.0f, 1.0f, 1.0f);
   v3 rad = mk(0.0f, 0.0f, 0.0f);
+  v3 hp, hn;
   uint32_t rng = seed;                                  // :307 re-seed
   const int NL = P.n_lights;
 
@@ -532,14 +541,14 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
       }
       h = h0;
     } else {
-      h = trace_closest<false, PF>(P, ro, rd, c, cand);
+      PT_WALK2(PARK, h = (trace_closest<false, PF>(P, ro, rd, c, cand)));
     }
     if (h.tri < 0) {
       rad = add(rad, mul(thr, mk(0.0f, 0.0f, 0.0f)));  // background (:336)
       break;
     }
-    const v3 hp = add(ro, muls(rd, h.t));               // :188
-    const v3 hn = tri_normal(P, h.tri);                 // :189
+    hp = add(ro, muls(rd, h.t));                        // :188
+    hn = tri_normal(P, h.tri);                          // :189
 
     // direct light (:345-366); the last light's shadow ray is deferred
     v3 direct = mk(0.0f, 0.0f, 0.0f);
@@ -570,7 +579,7 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
     v3 sd = sample_sphere(&rng);
     Hit sh;
     bool occ = false;
-    walk_pair(P, NL > 0 && s_need, s_o, s_d, s_lim, &occ, P.sss_bounces > 0, so, sd, cand, &sh);
+    PT_WALK4(PARK, walk_pair(P, NL > 0 && s_need, s_o, s_d, s_lim, &occ, P.sss_bounces > 0, so, sd, cand, &sh));
     if (NL > 0 && !occ) direct = add(direct, s_c);
     rad = add(rad, mul(thr, direct));
 
@@ -604,7 +613,7 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
       sss_thr = mul(sss_thr, muls(sss_albedo, exp_(-travel / (sss_radius * 1.5f))));
       so = sub(cp, muls(sn, OFFSET));
       sd = sample_sphere(&rng);
-      walk_pair(P, NL > 0 && s_need, s_o, s_d, s_lim, &occ, k + 1 < P.sss_bounces, so, sd, cand, &sh);
+      PT_WALK4(PARK, walk_pair(P, NL > 0 && s_need, s_o, s_d, s_lim, &occ, k + 1 < P.sss_bounces, so, sd, cand, &sh));
       if (NL > 0 && !occ) sl = add(sl, s_c);
       rad = add(rad, muls(mul(thr_k, sl), 1.0f + sss_radius * 0.5f));
     }
