@@ -586,3 +586,34 @@ def test_shadow_skip_light_intensities(lds, kernel):
     assert nan_r.any() and (~nan_r).any()
     _assert_same(np.where(nan_g, 0, gpu).astype(np.float32), np.where(nan_r, 0, ref).astype(np.float32),
                  f"kernel {kernel} lds {lds}")
+
+
+# ---- launch timing (bench.py's kernel_ms / launch_interval_ms) -------------
+def test_launch_timing_sampling_and_span():
+    """PT_OPT_LAUNCH_TIMING k: an event pair around every k-th launch;
+    pt_launch_span_ms covers first timed start to last timed end and reports
+    how many launches that span holds.  Output does not depend on timing."""
+    v, i, n = _box()
+    r = _setup(v, i, n)
+    r.resize_and_clear(64, 48)
+    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+    r.render(0, 2)
+    want = r.read_accum()
+    with pytest.raises(ptamd.PTError):
+        r.set_option(ptamd.PT_OPT_LAUNCH_TIMING, -1)
+    for every, launches, timed, covered in [(1, 5, 5, 5), (3, 7, 3, 7), (4, 5, 2, 5)]:
+        r.set_option(ptamd.PT_OPT_LAUNCH_TIMING, every)
+        r.reset_launch_times()
+        for _ in range(launches):
+            r.render(0, 2)
+        t = r.launch_times_ms()
+        assert t.size == timed and np.all(t > 0), (every, t)
+        span, n_cov = r.launch_span_ms()
+        assert n_cov == covered and span >= t.max() > 0, (every, span, n_cov)
+        _assert_same(r.read_accum(), want, f"timing every {every}")
+    r.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 0)
+    r.reset_launch_times()
+    r.render(0, 2)
+    assert r.launch_times_ms().size == 0
+    with pytest.raises(ptamd.PTError):
+        r.launch_span_ms()
