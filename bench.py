@@ -202,7 +202,14 @@ def main():
     # N=1 too: measures the exchange's own overhead on a 1-GPU box
     if world > 1 or os.environ.get("PT_BENCH_FORCE_DIST") == "1":
         import torch.distributed as dist
-        kw = {"device_id": dev} if backend == "nccl" else {}
+        kw = {}
+        if backend == "nccl":
+            # the gather's RCCL kernels run on a high-priority stream: they get
+            # CUs as soon as render workgroups retire, instead of queueing
+            # behind two frames' worth of them
+            opts = dist.ProcessGroupNCCL.Options()
+            opts.is_high_priority_stream = True
+            kw = {"device_id": dev, "pg_options": opts}
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
 
     def allreduce_max(t):
