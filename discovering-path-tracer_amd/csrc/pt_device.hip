@@ -79,6 +79,12 @@ __device__ __forceinline__ bool tri_test(v3 o, v3 d, float4 A, float4 B, float4 
 // in a wave whose lanes pass different leaves the triangle test then runs
 // max-over-lanes times instead of once per leaf any lane passed.  Candidates
 // are tested in visit order with the same strict '<', so the hit is the same.
+#ifndef PT_WF_PF
+#define PT_WF_PF 0
+#endif
+#ifndef PT_REC_PF
+#define PT_REC_PF 0
+#endif
 #ifndef PT_KCAND
 #define PT_KCAND 8
 #endif
@@ -86,9 +92,12 @@ constexpr int kCand = PT_KCAND;
 
 // PF (prefetch): load node k+1 while node k is being tested — it is the next
 // visit whenever k is a hit internal node or a leaf (the node arrays carry one
-// node of padding so k+1 is always readable).  Worth 12 % on a 1M-triangle
-// scene walked from HBM/L2, a 5 % loss on LDS-staged scenes (registers), so
-// the kernel enables it exactly when the scene is not in LDS.
+// node of padding so k+1 is always readable).  It was worth 12 % on a
+// 1M-triangle scene in the first kernel; re-measured after the candidate queue,
+// paired walks and null shadow rays it costs more than it hides: wavefront 1M
+// cloud 400 -> 337 ms and 10M cloud 662 -> 616 ms without it, sphere 452 ->
+// 423, recursive 5K sphere -2.5 %.  Off by default (PT_WF_PF, PT_REC_PF); an
+// LDS-staged walk never used it.
 
 __device__ __forceinline__ void test_candidates(const RenderParams& P, v3 o, v3 d, const int* cand, int nc,
                                                 float* best, int* bt) {
@@ -891,7 +900,7 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
       if (STATS || LDS)
         col = path_trace<STATS, !LDS>(P, origin, dir, seed, c, cand);
       else
-        col = path_trace_fused<true>(P, origin, dir, seed, cand);
+        col = path_trace_fused<PT_REC_PF != 0>(P, origin, dir, seed, cand);
       col4 = make_float4(col.x, col.y, col.z, 1.0f);                      // vec4(color, 1.0)
      }
      // hand the chunk's colours to the folding lanes of the same pixel
@@ -1763,7 +1772,7 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
     }
     if (!more && __ballot(p >= 0) == 0ull) break;
     for (int it = 0; it < PT_WF_STEPS; ++it) {
-      if (p >= 0 && wf_lane_step<!LDS>(P, L, cand)) {
+      if (p >= 0 && wf_lane_step<PT_WF_PF && !LDS>(P, L, cand)) {
         B.hits[p] = make_float2(L.lim, __int_as_float(L.res));
         p = -1;
       }
