@@ -1712,7 +1712,7 @@ constexpr unsigned long long kGroupLead =
     : PT_WF_GROUP == 8 ? 0x0101010101010101ull
                        : 0x0001000100010001ull;
 #ifndef PT_WF_MIN_BLOCKS
-#define PT_WF_MIN_BLOCKS 6
+#define PT_WF_MIN_BLOCKS 7   // 72 VGPRs (11 spilled): sphere -7 %, 1M cloud -0.6 % vs 6; 8 spills 30 (+50 %)
 #endif
 template <bool LDS>
 __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderParams P, WfBuffers B, int cur) {
