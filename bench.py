@@ -230,9 +230,6 @@ def main():
     r.set_params(DEPTH, SSS)
     r.set_partition(max(world, emu), rank)
     r.set_option(ptamd.PT_OPT_LAUNCH_TIMING, args.timing_every)
-    for kv in args.opt:
-        k, _, val = kv.partition("=")
-        r.set_option(int(k), int(val))
     # One explicit stream for the renderer and every torch op/collective: the
     # legacy default stream has handle 0, which pt_set_stream reads as "the
     # context's own stream", so it cannot be shared by handle.
@@ -259,6 +256,11 @@ def main():
             dist.all_reduce(t)
         counts = t.cpu().numpy()
     rays_per_frame = float(counts[0])
+    # output-invariant kernel options apply to the timed frames (the stats
+    # pass above always runs the path-recursive kernel)
+    for kv in args.opt:
+        k, _, val = kv.partition("=")
+        r.set_option(int(k), int(val))
 
     # --- the step ---------------------------------------------------------
     r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)

@@ -347,6 +347,11 @@ struct pt_context {
     int w = 0, h = 0;
   } rb[2];
   hipStream_t copy_stream = nullptr;
+  // Launches that write context-owned buffers (the accumulation buffer, the
+  // wavefront path buffers) are ordered across streams: the next such launch
+  // waits for the last one when it runs on another stream (order_shared).
+  hipEvent_t shared_ev = nullptr;
+  hipStream_t shared_stream = nullptr;
   int rb_next_ticket = 1;
   bool timed = false;
   // ring of event pairs, one per render launch since pt_reset_launch_times
@@ -374,6 +379,25 @@ struct pt_scene {
 // lanes), so only live ones are launched.
 // Pixels of columns [g0, g0+n) (or rows) whose NDC origin (the kernel's
 // ndc = 2*p/res - 1) lies in [lo, hi].
+// Before a launch that writes context-owned buffers: wait for the previous
+// such launch if it ran on another stream.
+static int order_shared(pt_context* c) {
+  if (c->shared_stream && c->shared_stream != c->stream) PT_HIP(hipStreamWaitEvent(c->stream, c->shared_ev, 0));
+  return PT_OK;
+}
+// After it (or after the last launch that reads those buffers back).
+static int mark_shared(pt_context* c) {
+  PT_HIP(hipEventRecord(c->shared_ev, c->stream));
+  c->shared_stream = c->stream;
+  return PT_OK;
+}
+// Before buffers that launches on any stream may still read are freed or
+// overwritten from the host (list rebuilds, reallocation): all of them done.
+static int quiesce(pt_context* c) {
+  PT_HIP(hipDeviceSynchronize());
+  return PT_OK;
+}
+
 static int pixels_in(int g0, int n, int res, float lo, float hi) {
   int k = 0;
   for (int i = 0; i < n; ++i) {
@@ -434,7 +458,7 @@ static int compact_items(pt_context* c, ptd::RenderParams* p) {
   if (key.size() != c->items_key.size() || memcmp(key.data(), c->items_key.data(), key.size() * 4) != 0) {
     std::vector<int> live, culled;
     item_lists(*p, p->rank, &live, &culled);
-    PT_HIP(hipStreamSynchronize(c->stream));   // the previous list may still be in use
+    { const int rc_ = quiesce(c); if (rc_) return rc_; }   // the previous list may still be in use
     c->h_items = live;
     c->h_items.insert(c->h_items.end(), culled.begin(), culled.end());
     if (c->h_items.size() > c->items_cap) {
@@ -488,7 +512,7 @@ int unpack_table(pt_context* c, const ptd::RenderParams& p) {
     for (size_t i = 0; i < live.size(); ++i) table.insert(table.end(), {r, live[i], (int)i});
     for (int it : culled) table.insert(table.end(), {r, it, -1});
   }
-  PT_HIP(hipStreamSynchronize(c->stream));
+  { const int rc_ = quiesce(c); if (rc_) return rc_; }
   const int rc = upload_ints(table, &c->d_unpack, &c->unpack_cap);
   if (rc) return rc;
   c->n_unpack = (int)(table.size() / 3);
@@ -501,7 +525,7 @@ int wf_reserve(pt_context* c, long long pixels, uint32_t batches, long long* chu
   if (want > 0x7fffffffll) return fail(PT_ERR_UNSUPPORTED, "frame too large for the wavefront kernel");
   *chunk_paths = want;
   if (want <= c->wf.cap) return PT_OK;
-  PT_HIP(hipStreamSynchronize(c->stream));
+  { const int rc_ = quiesce(c); if (rc_) return rc_; }
   dev_free(c->wf_block);
   c->wf = ptd::WfBuffers{};
   const size_t n = (size_t)want;
@@ -659,7 +683,9 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
       c->opt_fresh = fresh;
       if (rc) return rc;
       c->packed_key = key;
-      return pt_items_pack(c, pack_out);
+      const int rp = pt_items_pack(c, pack_out);
+      if (rp) return rp;
+      return mark_shared(c);   // the pack read the accumulation buffer
     }
     if (as.src) {
       const int rc = unpack_table(c, p);
@@ -674,6 +700,13 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     c->packed_key = key;
   }
   p.pack_out = pack_out;
+  // every launch but the path-recursive render_packed writes the context's
+  // accumulation buffer or wavefront buffers
+  const bool shared = !pack_out || wf || sm || c->stats_mode;
+  if (shared) {
+    const int ro = order_shared(c);
+    if (ro) return ro;
+  }
   if (wf) {
     const long long tiles = (p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;
     const long long items = p.items ? p.n_items : tiles * p.spl;
@@ -685,6 +718,10 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     PT_HIP(ptd::launch_wavefront(p, b, lds, c->stream));
   } else {
     PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream));
+  }
+  if (shared) {
+    const int rm = mark_shared(c);
+    if (rm) return rm;
   }
   if (timed) {
     PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
@@ -726,6 +763,7 @@ int pt_create(int device_ordinal, pt_context** out) {
     e = hipEventCreate(&c->ring[i][0]);
     if (e == hipSuccess) e = hipEventCreate(&c->ring[i][1]);
   }
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&c->shared_ev, hipEventDisableTiming);
   if (e != hipSuccess) {
     pt_destroy(c);
     return fail(PT_ERR_HIP, std::string("context setup: ") + hipGetErrorString(e));
@@ -757,6 +795,7 @@ int pt_destroy(pt_context* c) {
     if (r.done) (void)hipEventDestroy(r.done);
   }
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  if (c->shared_ev) (void)hipEventDestroy(c->shared_ev);
   for (int i = 0; i < pt_context::kRing; ++i)
     for (int j = 0; j < 2; ++j)
       if (c->ring[i][j]) (void)hipEventDestroy(c->ring[i][j]);
@@ -800,7 +839,7 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   float lo[3] = {threaded[0].x, threaded[0].y, threaded[0].z};   // node 0 is the root
   float hi[3] = {threaded[1].x, threaded[1].y, threaded[1].z};
   PT_HIP(hipSetDevice(c->device));
-  PT_HIP(hipStreamSynchronize(c->stream));
+  { const int rc_ = quiesce(c); if (rc_) return rc_; }
   dev_free(c->d_nodes);
   dev_free(c->d_nodes_full);
   dev_free(c->d_tris);
@@ -842,7 +881,7 @@ int pt_upload_lights(pt_context* c, const pt_area_light* lights, size_t n) {
   if (n && !lights) return fail(PT_ERR_INVALID, "null lights");
   if (n > 1024) return fail(PT_ERR_UNSUPPORTED, "more than 1024 lights");
   PT_HIP(hipSetDevice(c->device));
-  PT_HIP(hipStreamSynchronize(c->stream));
+  { const int rc_ = quiesce(c); if (rc_) return rc_; }
   dev_free(c->d_lights);
   dev_free(c->d_lights_dev);
   c->n_lights = 0;
@@ -886,8 +925,10 @@ int pt_clear_accum(pt_context* c) {
   if (!c) return fail(PT_ERR_INVALID, "null context");
   if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
   PT_HIP(hipSetDevice(c->device));
+  const int ro = order_shared(c);
+  if (ro) return ro;
   PT_HIP(ptd::launch_clear(c->d_accum, c->width, c->height, c->nranks, c->rank, c->stream));
-  return PT_OK;
+  return mark_shared(c);
 }
 
 int pt_resize_and_clear(pt_context* c, int w, int h) {
@@ -895,7 +936,7 @@ int pt_resize_and_clear(pt_context* c, int w, int h) {
   if (w <= 0 || h <= 0 || (long long)w * h > (1ll << 31)) return fail(PT_ERR_INVALID, "bad resolution");
   PT_HIP(hipSetDevice(c->device));
   if (!(c->own_accum && c->width == w && c->height == h)) {
-    PT_HIP(hipStreamSynchronize(c->stream));
+    { const int rc_ = quiesce(c); if (rc_) return rc_; }
     if (c->own_accum) dev_free(c->d_accum);
     c->d_accum = nullptr;
     c->own_accum = false;
@@ -912,7 +953,7 @@ int pt_bind_accum(pt_context* c, void* ptr, int w, int h) {
   if (w <= 0 || h <= 0) return fail(PT_ERR_INVALID, "bad resolution");
   if (((uintptr_t)ptr) & 15) return fail(PT_ERR_INVALID, "accumulation buffer must be 16-B aligned");
   PT_HIP(hipSetDevice(c->device));
-  PT_HIP(hipStreamSynchronize(c->stream));
+  { const int rc_ = quiesce(c); if (rc_) return rc_; }
   if (c->own_accum) dev_free(c->d_accum);
   c->d_accum = (float4*)ptr;
   c->own_accum = false;
@@ -929,6 +970,8 @@ int pt_read_accum(pt_context* c, float* rgba, size_t n) {
   const size_t need = (size_t)c->width * c->height * 4;
   if (n < need) return fail(PT_ERR_INVALID, "output buffer too small: need " + std::to_string(need) + " floats");
   PT_HIP(hipSetDevice(c->device));
+  const int ro = order_shared(c);
+  if (ro) return ro;
   PT_HIP(hipMemcpyAsync(rgba, c->d_accum, need * sizeof(float), hipMemcpyDeviceToHost, c->stream));
   PT_HIP(hipStreamSynchronize(c->stream));
   return PT_OK;
@@ -1019,6 +1062,10 @@ int pt_readback_begin(pt_context* c, int* ticket) {
   }
   if (!r.snap) PT_HIP(hipEventCreateWithFlags(&r.snap, hipEventDisableTiming));
   if (!r.done) PT_HIP(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
+  {
+    const int ro = order_shared(c);
+    if (ro) return ro;
+  }
   PT_HIP(hipMemcpyAsync(r.dev, c->d_accum, bytes, hipMemcpyDeviceToDevice, c->stream));
   PT_HIP(hipEventRecord(r.snap, c->stream));
   PT_HIP(hipStreamWaitEvent(c->copy_stream, r.snap, 0));
@@ -1108,8 +1155,10 @@ int pt_tiles_pack(pt_context* c, void* dst) {
   if (!c || !dst) return fail(PT_ERR_INVALID, "null argument");
   if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
   PT_HIP(hipSetDevice(c->device));
+  const int ro = order_shared(c);
+  if (ro) return ro;
   PT_HIP(ptd::launch_tiles(true, c->d_accum, (float4*)dst, c->width, c->height, c->nranks, c->rank, c->stream));
-  return PT_OK;
+  return mark_shared(c);
 }
 
 int pt_tiles_unpack(pt_context* c, const void* src, int src_rank, void* frame) {
@@ -1143,14 +1192,16 @@ int pt_items_pack(pt_context* c, void* dst) {
   if (key != c->pack_key) {
     std::vector<int> live, culled;
     item_lists(c->last, c->last.rank, &live, &culled);
-    PT_HIP(hipStreamSynchronize(c->stream));
+    { const int rc_ = quiesce(c); if (rc_) return rc_; }
     const int rc = upload_ints(live, &c->d_pack_items, &c->pack_cap);
     if (rc) return rc;
     c->n_pack_items = (int)live.size();
     c->pack_key = key;
   }
+  const int ro = order_shared(c);
+  if (ro) return ro;
   PT_HIP(ptd::launch_items_pack(c->last, c->d_accum, (float4*)dst, c->d_pack_items, c->n_pack_items, c->stream));
-  return PT_OK;
+  return mark_shared(c);
 }
 
 int pt_items_unpack_all(pt_context* c, const void* src, size_t slot_floats, void* frame) {

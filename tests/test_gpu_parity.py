@@ -617,3 +617,40 @@ def test_launch_timing_sampling_and_span():
     assert r.launch_times_ms().size == 0
     with pytest.raises(ptamd.PTError):
         r.launch_span_ms()
+
+
+@pytest.mark.parametrize("kernel", [0, 3])
+def test_render_packed_on_alternating_streams(kernel):
+    """bench.py's N>1 step: one context renders frames k = 0..5 with
+    pt_render_packed on two alternating streams without host synchronisation,
+    frame k also assembling frame k-2's slot.  The wavefront kernel renders
+    through context buffers (accumulation, path lists), so its launches on
+    different streams must be ordered by the library (order_shared); every
+    assembled frame equals the oracle bitwise."""
+    import torch
+    v, i, n = _box()
+    W, H = 96, 64
+    r = _setup(v, i, n, cam=CULL_CAMS[1])
+    if kernel:
+        r.set_option(ptamd.PT_OPT_KERNEL, kernel)
+    r.set_partition(1, 0)
+    r.resize_and_clear(W, H)
+    r.render(0, 4)
+    per = r.items_live(0)[1]
+    slot = max(4, r.items_live(0)[0] * per * 4)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    # frame k writes slot buffer k % 4 and assembles buffer (k - 2) % 4, both
+    # last touched on its own stream: only the library's buffers are shared
+    bufs = [torch.full((1, slot), float("nan"), dtype=torch.float32, device="cuda") for _ in range(4)]
+    frames = [torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda") for _ in range(4)]
+    torch.cuda.synchronize()
+    for k in range(6):
+        r.set_stream(streams[k % 2].cuda_stream)
+        if k >= 2:
+            r.render_packed(4, bufs[k % 4].data_ptr(), bufs[(k - 2) % 4].data_ptr(), slot, frames[k - 2].data_ptr())
+        else:
+            r.render_packed(4, bufs[k % 4].data_ptr())
+    torch.cuda.synchronize()
+    ref, _ = _oracle(v, i, n, W, H, nb=4, cam=CULL_CAMS[1])
+    for k in range(4):
+        _assert_same(frames[k].cpu().numpy().reshape(-1), ref, f"kernel {kernel} frame {k}")
