@@ -228,7 +228,10 @@ def main():
     r.upload_lights(light)
     r.set_camera(cam)
     r.set_params(DEPTH, SSS)
-    r.set_partition(max(world, emu), rank)
+    # PT_BENCH_EMULATE_RANK=r: emulate rank r's step instead of the root's
+    # (its share, no assembly) -- to compare the ranks' loads
+    emu_rank = int(os.environ.get("PT_BENCH_EMULATE_RANK", "0")) if emu > 1 else rank
+    r.set_partition(max(world, emu), emu_rank)
     r.set_option(ptamd.PT_OPT_LAUNCH_TIMING, args.timing_every)
     # One explicit stream for the renderer and every torch op/collective: the
     # legacy default stream has handle 0, which pt_set_stream reads as "the
@@ -297,7 +300,7 @@ def main():
         per = r.items_live(0)[1]
         slot = max(r.items_live(k)[0] for k in range(nparts)) * per * 4
         slot = max(slot, 4)
-        root = rank == 0
+        root = rank == 0 and emu_rank == 0
         # Frame k uses buffer set k % nbuf and, under --assemble 2, assembles
         # frame k - depth from that same set in its own launch; depth = streams,
         # so frame k waits only for frame k - depth's gather (which follows
@@ -338,7 +341,7 @@ def main():
                 else:
                     finish(work, pbuf)
             # emulation: the root's own slot is written in place, no transfer
-            dst = recv[buf][0] if dist is None else send[buf]
+            dst = (recv[buf][0] if root else send[buf]) if dist is None else send[buf]
             if args.assemble == 0:
                 r.render(0, SPP)
                 r.items_pack(dst.data_ptr())
@@ -486,7 +489,7 @@ def main():
                                          "unit": "G wave-instr/s", "frac": round(gi / VALU_PEAK_GINST, 4),
                                          "valu_wave_instr_per_launch": int(prof[2]), "source": prof[0]}
         if emu > 1:
-            out_line["metric"] = f"EMULATED (1 GPU, not a multi-GPU result): rank 0 of {emu}, " + out_line["metric"]
+            out_line["metric"] = f"EMULATED (1 GPU, not a multi-GPU result): rank {emu_rank} of {emu}, " + out_line["metric"]
             out_line["emulated_ranks"] = emu
             out_line["config"]["parallelism"] = f"emulated-tiles{emu}-sparse-gather"
         if no_cull is not None:
