@@ -157,6 +157,9 @@ def main():
     ap.add_argument("--timing-every", type=int, default=None,
                     help="HIP event pair around every k-th launch (default 4 on one stream, where a pair "
                          "costs ~7 us of device time per launch, 1 on two streams, where it is hidden)")
+    ap.add_argument("--root-slots", type=int, default=-1,
+                    help="gather path: partition slots of the root out of 16 per other rank "
+                         "(-1 auto: the root gives up the share its frame assembly costs; 0: equal shares)")
     ap.add_argument("--packed", action="store_true", help="N=1: run the gather path (render_packed + assembly)")
     ap.add_argument("--compare-no-cull", action="store_true",
                     help="N=1: also time the same steps with primary-ray culling off (reported as primary_cull_off)")
@@ -240,6 +243,52 @@ def main():
     torch.cuda.set_stream(stream)
     r.set_stream(stream.cuda_stream)   # order with torch's collectives
     r.resize_and_clear(W, H)
+
+    # Root share (gather path).  The root also assembles every gathered frame
+    # (a full-frame write, ~7.5 us at 1080p), so with equal shares it is the
+    # slowest rank.  Partition slots: 16 per rank, the root 16*(1 - 0.75*N*A/T1)
+    # where A = the root's assembly as a launch of its own, T1 = a full frame
+    # on one GPU, both timed here on the root (untimed setup); every rank
+    # applies the root's choice.  0.75: the part of a standalone assembly
+    # launch the pipelined step pays (emulated root vs other ranks at N=2/4/8:
+    # 12 of 16 slots balance them at N=8, 15 at N=2).
+    nparts = max(world, emu)
+    slots = None
+    if nparts > 1 and args.collective == "gather" and args.root_slots != 0:
+        s0 = args.root_slots
+        if s0 < 0:
+            s0 = 16
+            if rank == 0:
+                def time_ms(fn, reps=5):
+                    fn()
+                    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    ev0.record()
+                    for _ in range(reps):
+                        fn()
+                    ev1.record()
+                    ev1.synchronize()
+                    return ev0.elapsed_time(ev1) / reps
+                r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+                r.set_partition(1, 0)
+                t1 = time_ms(lambda: r.render(0, SPP))
+                r.set_partition(nparts, 0)
+                r.render(0, SPP)
+                cnt = max(r.items_live(k)[0] for k in range(nparts)) * r.items_live(0)[1] * 4
+                src = torch.zeros((nparts, max(cnt, 4)), dtype=torch.float32, device=dev)
+                frm = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+                t_asm = time_ms(lambda: r.items_unpack_all(src.data_ptr(), src.shape[1], frm.data_ptr()))
+                del src, frm
+                r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 0)
+                s0 = int(min(16, max(1, round(16 * (1.0 - 0.75 * nparts * t_asm / t1)))))
+                print(f"bench: root share: full frame {t1:.4f} ms, assembly {t_asm:.4f} ms -> "
+                      f"{s0} of 16 slots", file=sys.stderr, flush=True)
+            if dist is not None:
+                t = torch.tensor([s0], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
+                dist.broadcast(t, 0)
+                s0 = int(t.item())
+        slots = [s0] + [16] * (nparts - 1)
+        r.set_partition(nparts, emu_rank, slots)
+        r.resize_and_clear(W, H)
 
     # Stats pass (untimed): the reference's exact traversal counts for one frame.
     r.set_stats_mode(True)
@@ -463,6 +512,7 @@ def main():
             "data": "synthetic (reference scene, camera and light; progressive sample batches 0-%d)" % (SPP - 1),
             "config": {"workload": wl, "width": W, "height": H, "spp": SPP, "max_depth": DEPTH,
                        "sss_bounces": SSS,
+                       "partition_slots": slots,
                        "parallelism": (f"tiles{world}-" + ("sparse-gather" if args.collective == "gather" else "reduce"))
                        if world > 1 else ("single-packed" if args.packed else "single"),
                        "streams": args.streams,

@@ -299,6 +299,10 @@ struct pt_context {
   bool has_scene = false;
   pt_params params{4, 3};
   int nranks = 1, rank = 0;
+  std::vector<int> slots{1};    // partition slots per rank (pt_set_partition_slots)
+  int* d_parts = nullptr;       // every rank's slot positions, kMaxSlots ints each (rank_tile)
+  size_t parts_cap = 0;
+  std::vector<int> parts_key;
   bool stats_mode = false;
   int opt_scene_lds = 1;   // PT_OPT_SCENE_IN_LDS: 0 never, 1 auto, 2 always
   int opt_sample_lanes = 0;   // PT_OPT_SAMPLE_LANES: 0 auto, else 1/2/4/8
@@ -413,14 +417,56 @@ static int pixels_in(int g0, int n, int res, float lo, float hi) {
 // rectangle (cull[0]: full paths, ~9 rays per sample on box.obj) x 8 + pixels
 // inside a light rectangle (pre-pass only).  Output does not depend on the
 // order; every consumer (launch, pack, unpack table) uses this one list.
-static void item_lists(const ptd::RenderParams& p, int rank, std::vector<int>* live, std::vector<int>* culled) {
+// Rank r's share of the slotted partition (pt_device.h Part): the period's
+// slots ordered by (k + 1/2) / slots[rank] for each rank's k-th slot (ties by
+// rank), so every rank's slots are spread evenly over the period.
+static ptd::Part part_of(const pt_context* c, int r) {
+  std::vector<std::pair<double, int>> seq;
+  for (int i = 0; i < (int)c->slots.size(); ++i)
+    for (int k = 0; k < c->slots[i]; ++k) seq.push_back({(k + 0.5) / c->slots[i], i});
+  std::stable_sort(seq.begin(), seq.end());
+  ptd::Part pt{};
+  pt.m = (int)seq.size();
+  for (int v = 0; v < pt.m; ++v)
+    if (seq[v].second == r) pt.pos[pt.cnt++] = v;
+  return pt;
+}
+
+// Upload every rank's slot positions when the partition changed; the device
+// copy of rank r's starts at d_parts + r * kMaxSlots.
+static int upload_ints_(const std::vector<int>& h, int** d, size_t* cap) {
+  if (h.size() > *cap) {
+    dev_free(*d);
+    *cap = 0;
+    PT_HIP(hipMalloc((void**)d, h.size() * sizeof(int)));
+    *cap = h.size();
+  }
+  if (!h.empty()) PT_HIP(hipMemcpy(*d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice));
+  return PT_OK;
+}
+static int sync_parts(pt_context* c) {
+  std::vector<int> all((size_t)c->nranks * ptd::kMaxSlots, 0);
+  for (int r = 0; r < c->nranks; ++r) {
+    const ptd::Part pt = part_of(c, r);
+    for (int i = 0; i < pt.cnt; ++i) all[(size_t)r * ptd::kMaxSlots + i] = pt.pos[i];
+  }
+  if (all == c->parts_key && c->d_parts) return PT_OK;
+  { const int rc_ = quiesce(c); if (rc_) return rc_; }
+  const int rc = upload_ints_(all, &c->d_parts, &c->parts_cap);
+  if (rc) return rc;
+  c->parts_key = all;
+  return PT_OK;
+}
+
+static void item_lists(const ptd::RenderParams& p, const ptd::Part& part, std::vector<int>* live,
+                       std::vector<int>* culled) {
   const int W = p.width, H = p.height, spl = p.spl, rows = 16 / spl;
-  const int tiles = (p.blocks_total + p.nranks - 1 - rank) / p.nranks;
+  const int tiles = ptd::part_count(part, p.blocks_total);
   live->clear();
   culled->clear();
   std::vector<std::pair<int, int>> weighted;   // (-weight, item)
   for (int li = 0; li < tiles; ++li) {
-    const int b = li * p.nranks + rank;
+    const int b = ptd::part_tile(part, li);
     int bx, by;
     ptd::tile_block(b, p.blocks_x, &bx, &by);
     const int gx0 = bx * 16;
@@ -452,12 +498,14 @@ static void item_lists(const ptd::RenderParams& p, int rank, std::vector<int>* l
 }
 
 static int compact_items(pt_context* c, ptd::RenderParams* p) {
-  std::vector<float> key = {(float)p->width, (float)p->height, (float)p->nranks, (float)p->rank, (float)p->spl,
+  const ptd::Part pt = part_of(c, p->rank);
+  std::vector<float> key = {(float)p->width, (float)p->height, (float)pt.m, (float)pt.cnt,
+                            (float)pt.pos[0], (float)p->rank, (float)p->spl,
                             (float)p->n_cull, (float)p->item_order};
   for (int r = 0; r < p->n_cull; ++r) key.insert(key.end(), p->cull[r], p->cull[r] + 4);
   if (key.size() != c->items_key.size() || memcmp(key.data(), c->items_key.data(), key.size() * 4) != 0) {
     std::vector<int> live, culled;
-    item_lists(*p, p->rank, &live, &culled);
+    item_lists(*p, pt, &live, &culled);
     { const int rc_ = quiesce(c); if (rc_) return rc_; }   // the previous list may still be in use
     c->h_items = live;
     c->h_items.insert(c->h_items.end(), culled.begin(), culled.end());
@@ -481,10 +529,11 @@ static int compact_items(pt_context* c, ptd::RenderParams* p) {
 }
 
 namespace {
-std::vector<float> frame_key(const ptd::RenderParams& p) {
+std::vector<float> frame_key(const pt_context* c, const ptd::RenderParams& p) {
   std::vector<float> key = {(float)p.width, (float)p.height, (float)p.nranks, (float)p.rank, (float)p.spl,
                             (float)p.n_cull, (float)p.blocks_x, (float)p.blocks_total, (float)p.item_order};
   for (int r = 0; r < p.n_cull; ++r) key.insert(key.end(), p.cull[r], p.cull[r] + 4);
+  for (int sl : c->slots) key.push_back((float)sl);   // every rank's share (the assembly table)
   return key;
 }
 int upload_ints(const std::vector<int>& h, int** d, size_t* cap) {
@@ -502,15 +551,18 @@ int upload_ints(const std::vector<int>& h, int** d, size_t* cap) {
 constexpr long long kWfMaxPaths = 1ll << 24;
 constexpr int kWfAutoTris = 32768;
 // The root's assembly table for frames rendered with params p: per rank its
-// live items {rank, item, slot} and its culled items {rank, item, -1}.
+// live items {rank, tile*8 + part, slot} and its culled items {rank, tile*8 + part, -1}.
 int unpack_table(pt_context* c, const ptd::RenderParams& p) {
-  const std::vector<float> key = frame_key(p);
+  const std::vector<float> key = frame_key(c, p);
   if (key == c->unpack_key) return PT_OK;
   std::vector<int> table, live, culled;
   for (int r = 0; r < p.nranks; ++r) {
-    item_lists(p, r, &live, &culled);
-    for (size_t i = 0; i < live.size(); ++i) table.insert(table.end(), {r, live[i], (int)i});
-    for (int it : culled) table.insert(table.end(), {r, it, -1});
+    const ptd::Part pt = part_of(c, r);
+    item_lists(p, pt, &live, &culled);
+    // {rank, tile*8 + part, slot}: tile and part of the item (unpack_pixel)
+    auto tp = [&](int item) { return ptd::part_tile(pt, item / p.spl) * 8 + item % p.spl; };
+    for (size_t i = 0; i < live.size(); ++i) table.insert(table.end(), {r, tp(live[i]), (int)i});
+    for (int it : culled) table.insert(table.end(), {r, tp(it), -1});
   }
   { const int rc_ = quiesce(c); if (rc_) return rc_; }
   const int rc = upload_ints(table, &c->d_unpack, &c->unpack_cap);
@@ -599,6 +651,15 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.blocks_total = p.blocks_x * ((c->height + 15) / 16);
   p.nranks = c->nranks;
   p.rank = c->rank;
+  const ptd::Part hpart = part_of(c, c->rank);
+  {
+    const int rc = sync_parts(c);
+    if (rc) return rc;
+  }
+  p.part_m = hpart.m;
+  p.part_cnt = hpart.cnt;
+  p.part_pos = c->d_parts + (size_t)c->rank * ptd::kMaxSlots;
+  p.n_tiles = ptd::part_count(hpart, p.blocks_total);
   p.fresh = pack_out ? 1 : c->opt_fresh;
   p.item_order = c->opt_item_order;
   p.pack_out = nullptr;
@@ -641,7 +702,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   // sphere 550 -> 465, 100K cloud 113 -> 77; 1M cloud 2 spp 225 -> 236; a 1/8
   // tile share of the 10M cloud: 1 spp (259K paths) 147 -> 273, 8 spp (2M)
   // 742 -> 669; box 0.38 -> 8.4.
-  const long long paths = (long long)((p.blocks_total + p.nranks - 1 - p.rank) / p.nranks) * 256 * n_batches;
+  const long long paths = (long long)p.n_tiles * 256 * n_batches;
   const bool wf_auto = c->n_tris >= kWfAutoTris && paths >= (1ll << 20) &&
                        (c->n_tris >= (1 << 20) || paths >= (1ll << 23));
   const bool wf = c->opt_kernel == 3 || (c->opt_kernel == 0 && !lds && !c->stats_mode && wf_auto);
@@ -667,7 +728,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.n_unpack = 0;
   p.unpack_slot_f4 = 0;
   if (pack_out) {
-    const std::vector<float> key = frame_key(p);
+    const std::vector<float> key = frame_key(c, p);
     if (as.src && key != c->packed_key)
       return fail(PT_ERR_INVALID, "pt_render_packed: the frame to assemble has another item layout (size, partition, lanes, culling)");
     if (wf || sm) {
@@ -696,7 +757,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
       p.n_unpack = c->n_unpack;
       p.unpack_slot_f4 = (long long)(as.slot_floats / 4);
     }
-    if (!p.items) p.n_items = (int)(((p.blocks_total + p.nranks - 1 - p.rank) / p.nranks) * p.spl);
+    if (!p.items) p.n_items = p.n_tiles * p.spl;
     c->packed_key = key;
   }
   p.pack_out = pack_out;
@@ -708,7 +769,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     if (ro) return ro;
   }
   if (wf) {
-    const long long tiles = (p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;
+    const long long tiles = p.n_tiles;
     const long long items = p.items ? p.n_items : tiles * p.spl;
     long long chunk_paths = 0;
     const int rc = wf_reserve(c, items * (256 / p.spl), n_batches, &chunk_paths);
@@ -796,6 +857,7 @@ int pt_destroy(pt_context* c) {
   }
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->shared_ev) (void)hipEventDestroy(c->shared_ev);
+  dev_free(c->d_parts);
   for (int i = 0; i < pt_context::kRing; ++i)
     for (int j = 0; j < 2; ++j)
       if (c->ring[i][j]) (void)hipEventDestroy(c->ring[i][j]);
@@ -918,6 +980,22 @@ int pt_set_partition(pt_context* c, int nranks, int rank) {
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(PT_ERR_INVALID, "bad partition");
   c->nranks = nranks;
   c->rank = rank;
+  c->slots.assign((size_t)nranks, 1);
+  return PT_OK;
+}
+
+int pt_set_partition_slots(pt_context* c, int nranks, int rank, const int* slots) {
+  if (!c || !slots) return fail(PT_ERR_INVALID, "null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(PT_ERR_INVALID, "bad partition");
+  long long m = 0;
+  for (int r = 0; r < nranks; ++r) {
+    if (slots[r] < 1 || slots[r] > ptd::kMaxSlots) return fail(PT_ERR_INVALID, "partition slots must be 1..64 per rank");
+    m += slots[r];
+  }
+  if (m > 4096) return fail(PT_ERR_INVALID, "more than 4096 partition slots");
+  c->nranks = nranks;
+  c->rank = rank;
+  c->slots.assign(slots, slots + nranks);
   return PT_OK;
 }
 
@@ -927,7 +1005,12 @@ int pt_clear_accum(pt_context* c) {
   PT_HIP(hipSetDevice(c->device));
   const int ro = order_shared(c);
   if (ro) return ro;
-  PT_HIP(ptd::launch_clear(c->d_accum, c->width, c->height, c->nranks, c->rank, c->stream));
+  {
+    const int rc = sync_parts(c);
+    if (rc) return rc;
+  }
+  PT_HIP(ptd::launch_clear(c->d_accum, c->width, c->height, part_of(c, c->rank),
+                           c->d_parts + (size_t)c->rank * ptd::kMaxSlots, c->stream));
   return mark_shared(c);
 }
 
@@ -1147,7 +1230,7 @@ int pt_set_option(pt_context* c, int key, int value) {
 int pt_tiles_owned(pt_context* c, int* n_tiles) {
   if (!c || !n_tiles) return fail(PT_ERR_INVALID, "null argument");
   if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
-  *n_tiles = ptd::owned_tiles(c->width, c->height, c->nranks, c->rank);
+  *n_tiles = ptd::owned_tiles(c->width, c->height, part_of(c, c->rank));
   return PT_OK;
 }
 
@@ -1157,7 +1240,12 @@ int pt_tiles_pack(pt_context* c, void* dst) {
   PT_HIP(hipSetDevice(c->device));
   const int ro = order_shared(c);
   if (ro) return ro;
-  PT_HIP(ptd::launch_tiles(true, c->d_accum, (float4*)dst, c->width, c->height, c->nranks, c->rank, c->stream));
+  {
+    const int rc = sync_parts(c);
+    if (rc) return rc;
+  }
+  PT_HIP(ptd::launch_tiles(true, c->d_accum, (float4*)dst, c->width, c->height, part_of(c, c->rank),
+                           c->d_parts + (size_t)c->rank * ptd::kMaxSlots, c->stream));
   return mark_shared(c);
 }
 
@@ -1167,7 +1255,12 @@ int pt_tiles_unpack(pt_context* c, const void* src, int src_rank, void* frame) {
   if (src_rank < 0 || src_rank >= c->nranks) return fail(PT_ERR_INVALID, "src_rank out of range");
   if ((((uintptr_t)src) & 15) || (((uintptr_t)frame) & 15)) return fail(PT_ERR_INVALID, "buffers must be 16-B aligned");
   PT_HIP(hipSetDevice(c->device));
-  PT_HIP(ptd::launch_tiles(false, (float4*)frame, (float4*)src, c->width, c->height, c->nranks, src_rank, c->stream));
+  {
+    const int rc = sync_parts(c);
+    if (rc) return rc;
+  }
+  PT_HIP(ptd::launch_tiles(false, (float4*)frame, (float4*)src, c->width, c->height, part_of(c, src_rank),
+                           c->d_parts + (size_t)src_rank * ptd::kMaxSlots, c->stream));
   return PT_OK;
 }
 
@@ -1176,9 +1269,9 @@ int pt_tiles_unpack(pt_context* c, const void* src, int src_rank, void* frame) {
 int pt_items_live(pt_context* c, int rank, int* n_items, int* item_pixels) {
   if (!c || !n_items || !item_pixels) return fail(PT_ERR_INVALID, "null argument");
   if (!c->last_valid) return fail(PT_ERR_INVALID, "no path-recursive pt_render yet");
-  if (rank < 0 || rank >= c->last.nranks) return fail(PT_ERR_INVALID, "rank out of range");
+  if (rank < 0 || rank >= c->last.nranks || rank >= (int)c->slots.size()) return fail(PT_ERR_INVALID, "rank out of range");
   std::vector<int> live, culled;
-  item_lists(c->last, rank, &live, &culled);
+  item_lists(c->last, part_of(c, rank), &live, &culled);
   *n_items = (int)live.size();
   *item_pixels = 256 / c->last.spl;
   return PT_OK;
@@ -1188,10 +1281,10 @@ int pt_items_pack(pt_context* c, void* dst) {
   if (!c || !dst) return fail(PT_ERR_INVALID, "null argument");
   if (!c->last_valid || !c->d_accum) return fail(PT_ERR_INVALID, "no path-recursive pt_render yet");
   PT_HIP(hipSetDevice(c->device));
-  const std::vector<float> key = frame_key(c->last);
+  const std::vector<float> key = frame_key(c, c->last);
   if (key != c->pack_key) {
     std::vector<int> live, culled;
-    item_lists(c->last, c->last.rank, &live, &culled);
+    item_lists(c->last, part_of(c, c->last.rank), &live, &culled);
     { const int rc_ = quiesce(c); if (rc_) return rc_; }
     const int rc = upload_ints(live, &c->d_pack_items, &c->pack_cap);
     if (rc) return rc;

@@ -47,6 +47,33 @@ __host__ __device__ inline int block_tile(int bx, int by, int blocks_x) {
   return by * blocks_x + (bx - by % blocks_x + blocks_x) % blocks_x;
 }
 
+// A rank's tiles under a slotted partition: tiles are dealt in periods of m
+// slots and a rank owns cnt of them, at the ascending positions pos[] of each
+// period, i.e. tile b iff b % m is one of pos[].  One slot per rank (m =
+// nranks, pos = {rank}) is "b % nranks == rank".  Unequal slot counts let the
+// root, which also assembles the frame, render a smaller share
+// (pt_set_partition_slots); the host spreads every rank's slots evenly over
+// the period, since runs of neighbouring tiles would land unevenly on a
+// centred object.
+constexpr int kMaxSlots = 64;
+struct Part {
+  int m, cnt;
+  int pos[kMaxSlots];
+};
+__host__ __device__ inline int part_tile(const Part& p, int li) { return (li / p.cnt) * p.m + p.pos[li % p.cnt]; }
+__host__ __device__ inline int part_count(const Part& p, int total) {
+  const int rem = total % p.m;
+  int n = (total / p.m) * p.cnt;
+  for (int i = 0; i < p.cnt; ++i) n += p.pos[i] < rem ? 1 : 0;
+  return n;
+}
+__host__ __device__ inline bool part_owns(const Part& p, int b) {
+  const int v = b % p.m;
+  bool own = false;
+  for (int i = 0; i < p.cnt; ++i) own = own || p.pos[i] == v;
+  return own;
+}
+
 struct RenderParams {
   const float4* nodes;
   const float4* tris;
@@ -65,7 +92,11 @@ struct RenderParams {
   // tan(radians(fov * 0.5))
   float cam_right[3], cam_upv[3], tan_fov;
   int blocks_x, blocks_total;   // 16x16-pixel blocks
-  int nranks, rank;             // tile b (partition order, tile_block) is rendered iff b % nranks == rank
+  int nranks, rank;             // this rank of nranks
+  // its tiles (Part on the host): the period, its slot count, its slot
+  // positions in device memory (rank_tile), and how many tiles it owns
+  int part_m, part_cnt, n_tiles;
+  const int* part_pos;
   int spl;                      // sample lanes per pixel: 1, 2, 4 or 8
   int fresh;                    // first_batch == 0 starts from +0 without reading accum
   int sm_batch;                 // state-machine kernel: lanes that must be waiting before shading runs
@@ -98,10 +129,11 @@ constexpr int kMaxCullRects = 8;
 hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices, int n_tris, float4* d_tris,
                              hipStream_t stream);
 hipError_t launch_setup_lights(const LightRec* d_in, int n, LightDev* d_out, hipStream_t stream);
-int owned_tiles(int width, int height, int nranks, int rank);
-hipError_t launch_tiles(bool pack, float4* frame, float4* packed, int width, int height, int nranks, int rank,
+int owned_tiles(int width, int height, const Part& part);
+hipError_t launch_tiles(bool pack, float4* frame, float4* packed, int width, int height, const Part& part,
+                        const int* d_pos,
                         hipStream_t stream);
-hipError_t launch_clear(float4* accum, int width, int height, int nranks, int rank, hipStream_t stream);
+hipError_t launch_clear(float4* accum, int width, int height, const Part& part, const int* d_pos, hipStream_t stream);
 // live-item exchange: pack this rank's listed items (256/spl pixels each) of
 // frame densely; unpack entries {rank, item, slot} from per-rank slots of
 // slot_f4 float4s into frame, slot -1 = culled item -> (0,0,0,1)

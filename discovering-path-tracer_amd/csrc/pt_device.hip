@@ -38,6 +38,12 @@ struct Ctr {
   uint32_t rays, nodes, leaves;
 };
 
+// This rank's li-th tile (pt_device.h Part; slot positions in device memory:
+// a kernel argument array indexed at run time would be copied to scratch).
+__device__ __forceinline__ int rank_tile(const RenderParams& P, int li) {
+  return (li / P.part_cnt) * P.part_m + P.part_pos[li % P.part_cnt];
+}
+
 struct Hit {
   float t;
   int tri;   // -1 = miss
@@ -694,7 +700,7 @@ __device__ __forceinline__ void fill_culled(const RenderParams& P, const int* __
     const long long g = ((long long)block * kPixPerFill + k) * 256 + threadIdx.x;
     if (g >= total) return;
     const int item = items[g / per_item], q = (int)(g % per_item);
-    const int tile = (item / spl) * P.nranks + P.rank, part = item % spl;
+    const int tile = rank_tile(P, item / spl), part = item % spl;
     int bx, by;
     tile_block(tile, P.blocks_x, &bx, &by);
     const int px = bx * 16 + q % 16;
@@ -711,10 +717,9 @@ __device__ __forceinline__ void fill_culled(const RenderParams& P, const int* __
   }
 }
 
-// Pixel q of item `item` of rank `rank` (the render kernel's mapping).
-__device__ __forceinline__ bool item_pixel(const RenderParams& P, int rank, int item, int q, size_t* pix) {
+// Pixel q of part `part` of tile `tile` (the render kernel's mapping).
+__device__ __forceinline__ bool tile_pixel(const RenderParams& P, int tile, int part, int q, size_t* pix) {
   const int spl = P.spl;
-  const int tile = (item / spl) * P.nranks + rank, part = item % spl;
   int bx, by;
   tile_block(tile, P.blocks_x, &bx, &by);
   const int px = bx * 16 + q % 16;
@@ -733,7 +738,7 @@ __device__ __forceinline__ void unpack_pixel(const RenderParams& P, float4* __re
   const int* e = table + 3 * (g / per);
   const int q = (int)(g % per);
   size_t pix;
-  if (!item_pixel(P, e[0], e[1], q, &pix)) return;
+  if (!tile_pixel(P, e[1] >> 3, e[1] & 7, q, &pix)) return;   // e = {rank, tile*8 + part, slot}
   frame[pix] = e[2] >= 0 ? src[(size_t)e[0] * slot_f4 + (size_t)e[2] * per + q] : make_float4(0.0f, 0.0f, 0.0f, 1.0f);
 }
 
@@ -778,7 +783,7 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
   // item = (owned tile, part); with culling the host launches only items that
   // can hold a live pixel, listed in P.items
   const int item = P.items ? P.items[blockIdx.x] : (int)blockIdx.x;
-  const int tile = (item / spl) * P.nranks + P.rank;
+  const int tile = rank_tile(P, item / spl);
   const int part = item % spl;
   const int wave = tid >> 6, lane = tid & 63;
   // per wave: the leaf-candidate queue, then a [slot][lane] area that holds
@@ -985,24 +990,27 @@ __global__ __launch_bounds__(64) void setup_lights_kernel(const LightRec* __rest
   out[i] = d;
 }
 
-__global__ __launch_bounds__(256) void clear_kernel(float4* accum, int W, int H, int nranks, int rank) {
+__global__ __launch_bounds__(256) void clear_kernel(float4* accum, int W, int H, int m, int cnt,
+                                                    const int* __restrict__ pos) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (size_t)W * (size_t)H) return;
   const int x = (int)(i % (size_t)W), y = (int)(i / (size_t)W);
   const int blocks_x = (W + 15) / 16;
   const int b = block_tile(x / 16, y / 16, blocks_x);
-  const float z = (b % nranks == rank) ? 0.0f : -0.0f;
+  bool own = false;
+  for (int i = 0; i < cnt; ++i) own = own || pos[i] == b % m;
+  const float z = own ? 0.0f : -0.0f;
   accum[i] = make_float4(z, z, z, z);
 }
 
-// Owned 16x16 tiles <-> a dense buffer (tile o = owned tile rank + o*nranks,
+// Owned 16x16 tiles <-> a dense buffer (tile o = the rank's o-th tile, part_tile,
 // 256 float4 row-major inside the tile, zeros outside the image): what a rank
 // ships to the root so the frame can be assembled by a gather.
 template <bool PACK>
 __global__ __launch_bounds__(256) void tiles_kernel(float4* frame, float4* packed, int W, int H, int blocks_x,
-                                                    int nranks, int rank) {
+                                                    int m, int cnt, const int* __restrict__ pos) {
   const int o = (int)blockIdx.x;
-  const int b = o * nranks + rank;
+  const int b = (o / cnt) * m + pos[o % cnt];
   const int t = (int)threadIdx.x;
   int bx, by;
   tile_block(b, blocks_x, &bx, &by);
@@ -1023,7 +1031,8 @@ __global__ __launch_bounds__(256) void items_pack_kernel(RenderParams P, const f
   const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
   if (g >= (long long)n * per) return;
   size_t pix;
-  const bool in = item_pixel(P, P.rank, items[g / per], (int)(g % per), &pix);
+  const int item = items[g / per];
+  const bool in = tile_pixel(P, rank_tile(P, item / P.spl), item % P.spl, (int)(g % per), &pix);
   packed[g] = in ? frame[pix] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 }
 
@@ -1440,7 +1449,7 @@ __global__ __launch_bounds__(256, PT_SM_MIN_BLOCKS) void render_sm_kernel(Render
   }
   // one pixel per lane, all its samples in order: 16x16 tile per workgroup,
   // 8x8 per wave
-  const int tile = (int)blockIdx.x * P.nranks + P.rank;
+  const int tile = rank_tile(P, (int)blockIdx.x);
   const int wave = tid >> 6, lane = tid & 63;
   __shared__ int cand_buf[4][kCand][64];
   int* cand = &cand_buf[wave][0][lane];
@@ -1566,7 +1575,7 @@ __device__ __forceinline__ bool wf_pixel(const RenderParams& P, long long pp, in
   const int spl = P.spl, per = 256 / spl;
   const int idx = (int)(pp / per), q = (int)(pp % per);
   const int item = P.items ? P.items[idx] : idx;
-  const int tile = (item / spl) * P.nranks + P.rank, part = item % spl;
+  const int tile = rank_tile(P, item / spl), part = item % spl;
   int bx, by;
   tile_block(tile, P.blocks_x, &bx, &by);
   *px = bx * 16 + q % 16;
@@ -1872,20 +1881,19 @@ hipError_t launch_setup_lights(const LightRec* d_in, int n, LightDev* d_out, hip
   return hipGetLastError();
 }
 
-int owned_tiles(int width, int height, int nranks, int rank) {
-  const int total = ((width + 15) / 16) * ((height + 15) / 16);
-  return total > rank ? (total - rank + nranks - 1) / nranks : 0;
+int owned_tiles(int width, int height, const Part& part) {
+  return part_count(part, ((width + 15) / 16) * ((height + 15) / 16));
 }
 
-hipError_t launch_tiles(bool pack, float4* frame, float4* packed, int width, int height, int nranks, int rank,
-                        hipStream_t stream) {
-  const int n = owned_tiles(width, height, nranks, rank);
+hipError_t launch_tiles(bool pack, float4* frame, float4* packed, int width, int height, const Part& part,
+                        const int* d_pos, hipStream_t stream) {
+  const int n = owned_tiles(width, height, part);
   if (n <= 0) return hipSuccess;
   const int bx = (width + 15) / 16;
   if (pack)
-    tiles_kernel<true><<<n, 256, 0, stream>>>(frame, packed, width, height, bx, nranks, rank);
+    tiles_kernel<true><<<n, 256, 0, stream>>>(frame, packed, width, height, bx, part.m, part.cnt, d_pos);
   else
-    tiles_kernel<false><<<n, 256, 0, stream>>>(frame, packed, width, height, bx, nranks, rank);
+    tiles_kernel<false><<<n, 256, 0, stream>>>(frame, packed, width, height, bx, part.m, part.cnt, d_pos);
   return hipGetLastError();
 }
 
@@ -1905,17 +1913,17 @@ hipError_t launch_items_unpack(const RenderParams& p, float4* frame, const float
   return hipGetLastError();
 }
 
-hipError_t launch_clear(float4* accum, int width, int height, int nranks, int rank, hipStream_t stream) {
+hipError_t launch_clear(float4* accum, int width, int height, const Part& part, const int* d_pos, hipStream_t stream) {
   const size_t n = (size_t)width * (size_t)height;
   if (n == 0) return hipSuccess;
-  clear_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(accum, width, height, nranks, rank);
+  clear_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(accum, width, height, part.m, part.cnt, d_pos);
   return hipGetLastError();
 }
 
 hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool state_machine, hipStream_t stream) {
   if (p.spl != 1 && p.spl != 2 && p.spl != 4 && p.spl != 8) return hipErrorInvalidValue;
-  // owned tiles b = rank + i*nranks; the recursive kernel splits each into spl workgroups
-  const long long tiles = (long long)(p.blocks_total + p.nranks - 1 - p.rank) / p.nranks;
+  // owned tiles (part_tile); the recursive kernel splits each into spl workgroups
+  const long long tiles = p.n_tiles;
   long long grid = state_machine ? tiles : tiles * p.spl;
   if (grid <= 0 || p.n_batches == 0) return hipSuccess;
   if (p.pack_out && (state_machine || stats)) return hipErrorInvalidValue;
@@ -1944,7 +1952,7 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
   if (p0.spl != 1 && p0.spl != 2 && p0.spl != 4 && p0.spl != 8) return hipErrorInvalidValue;
   if (p0.n_batches == 0) return hipSuccess;
   const int per = 256 / p0.spl;
-  const long long tiles = (long long)(p0.blocks_total + p0.nranks - 1 - p0.rank) / p0.nranks;
+  const long long tiles = p0.n_tiles;
   const long long items = p0.items ? p0.n_items : tiles * p0.spl;
   if (p0.items && p0.n_culled_items > 0) {
     const long long px = (long long)p0.n_culled_items * per;

@@ -40,6 +40,7 @@ EXPORTS = [
     "pt_default_camera", "pt_primary_cull_rects", "pt_scene_save", "pt_scene_load_cache",
     "pt_progressive_camera", "pt_progressive_advance", "pt_readback_begin", "pt_readback_end", "pt_write_image",
     "pt_items_live", "pt_items_pack", "pt_items_unpack_all", "pt_render_packed", "pt_launch_span_ms",
+    "pt_set_partition_slots",
 ]
 
 
@@ -79,6 +80,7 @@ def lib():
             "pt_clear_accum": ([vp], i32), "pt_accum_device_ptr": ([vp], vp),
             "pt_read_accum": ([vp, vp, sz], i32), "pt_dispatch": ([vp, u32], i32),
             "pt_render": ([vp, u32, u32], i32), "pt_set_partition": ([vp, i32, i32], i32),
+            "pt_set_partition_slots": ([vp, i32, i32, vp], i32),
             "pt_set_stats_mode": ([vp, i32], i32), "pt_set_option": ([vp, i32, i32], i32), "pt_last_kernel": ([vp, ctypes.POINTER(ctypes.c_int)], i32),
             "pt_tiles_owned": ([vp, ctypes.POINTER(i32)], i32), "pt_tiles_pack": ([vp, vp], i32),
             "pt_tiles_unpack": ([vp, vp, i32, vp], i32), "pt_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
@@ -229,14 +231,26 @@ def device_math_exhaustive(fn, device=0):
     return bad.value, first.value
 
 
-def partition_owned(width, height, nranks, rank):
-    """Pixels a rank renders under pt_set_partition: 16x16 blocks, block
-    (bx, by) is tile b = by*blocks_x + (bx - by) mod blocks_x (rows rotated),
-    owned iff b % nranks == rank.  Returns a (H, W) bool mask."""
+def partition_slot_positions(nranks, rank, slots=None):
+    """(m, positions) of rank's slots in a period of the slotted partition
+    (pt_api.cpp part_of): slots ordered by (k + 1/2) / slots[r] for each
+    rank's k-th slot, ties by rank."""
+    s = [1] * nranks if slots is None else [int(x) for x in slots]
+    seq = sorted(((k + 0.5) / s[r], r) for r in range(nranks) for k in range(s[r]))
+    return len(seq), [v for v, (_, r) in enumerate(seq) if r == rank]
+
+
+def partition_owned(width, height, nranks, rank, slots=None):
+    """Pixels a rank renders under pt_set_partition(_slots): 16x16 blocks,
+    block (bx, by) is tile b = by*blocks_x + (bx - by) mod blocks_x (rows
+    rotated); the rank owns tile b iff b % m is one of its slot positions
+    (partition_slot_positions; one slot per rank: b % nranks == rank).
+    Returns a (H, W) bool mask."""
+    m, pos = partition_slot_positions(nranks, rank, slots)
     nbx = (width + 15) // 16
     ys, xs = np.mgrid[0:height, 0:width]
     by, bx = ys // 16, xs // 16
-    return (by * nbx + (bx - by) % nbx) % nranks == rank
+    return np.isin((by * nbx + (bx - by) % nbx) % m, pos)
 
 
 def primary_cull_rects(camera_ubo, width, height, root_min, root_max, lights16, max_rects=8):
@@ -302,8 +316,16 @@ class Renderer:
         p = Params(max_depth, sss_bounces)
         _check(lib().pt_set_params(self._c, ctypes.byref(p)), "pt_set_params")
 
-    def set_partition(self, nranks, rank):
-        _check(lib().pt_set_partition(self._c, nranks, rank), "pt_set_partition")
+    def set_partition(self, nranks, rank, slots=None):
+        """Tile split over nranks (pt_set_partition); `slots` (one int per
+        rank) gives unequal shares (pt_set_partition_slots)."""
+        if slots is None:
+            _check(lib().pt_set_partition(self._c, nranks, rank), "pt_set_partition")
+            return
+        sl = np.ascontiguousarray(slots, np.int32)
+        if sl.size != nranks:
+            raise PTError("one slot count per rank")
+        _check(lib().pt_set_partition_slots(self._c, nranks, rank, sl.ctypes.data), "pt_set_partition_slots")
 
     def tiles_owned(self):
         n = ctypes.c_int()

@@ -156,6 +156,12 @@ int pt_readback_end(pt_context* ctx, int ticket, float* rgba, size_t n_floats);
  * owned pixels and -0 (the IEEE additive identity) to the others, so a sum
  * reduction of all ranks' buffers is bit-identical to a single-GPU frame. */
 int pt_set_partition(pt_context* ctx, int nranks, int rank);
+/* Unequal shares: tiles are dealt in periods of sum(slots) slots, rank r
+ * owning slots[r] consecutive ones (1..64 each, at most 4096 in all).
+ * pt_set_partition is the case of one slot per rank.  Every rank must pass
+ * the same slots.  bench.py gives the root, which also assembles the
+ * gathered frame, fewer slots. */
+int pt_set_partition_slots(pt_context* ctx, int nranks, int rank, const int* slots);
 /* Gather-based assembly (cheaper than a full-frame sum for N > 2): a rank
  * packs the tiles it owns into a dense device buffer of
  * n_tiles * 16*16 float4 (pt_tiles_owned), ships it to the root, and the

@@ -654,3 +654,51 @@ def test_render_packed_on_alternating_streams(kernel):
     ref, _ = _oracle(v, i, n, W, H, nb=4, cam=CULL_CAMS[1])
     for k in range(4):
         _assert_same(frames[k].cpu().numpy().reshape(-1), ref, f"kernel {kernel} frame {k}")
+
+
+# ---- slotted partition (pt_set_partition_slots) -----------------------------
+@pytest.mark.parametrize("slots", [[2, 1, 3], [6, 8, 8, 8], [1, 5]])
+def test_partition_slots_sum_and_sparse_exchange(slots):
+    """Unequal shares: the -0/+0 cleared partials of all ranks sum to the
+    single-GPU frame; the dense tile gather and the sparse live-item exchange
+    with pt_render_packed (the root assembling every rank's slot) give it
+    bitwise too; the ranks' item counts follow the slots."""
+    import torch
+    v, i, n = _box()
+    W, H, nb = 150, 70, 4
+    N = len(slots)
+    want, _ = _oracle(v, i, n, W, H, nb=nb, cam=CULL_CAMS[1])
+    acc = np.full(W * H * 4, -0.0, np.float32)
+    rs = []
+    for rank in range(N):
+        r = _setup(v, i, n, cam=CULL_CAMS[1])
+        r.set_partition(N, rank, slots)
+        r.resize_and_clear(W, H)
+        r.render(0, nb)
+        acc = (acc + r.read_accum()).astype(np.float32)
+        owned = ptamd.partition_owned(W, H, N, rank, slots).reshape(-1)
+        assert r.tiles_owned() * 256 >= np.count_nonzero(owned)
+        rs.append(r)
+    _assert_same(acc, want, f"sum over slots {slots}")
+    # dense tiles: pack every rank's owned tiles, unpack them all on rank 0
+    frame = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+    for k, r in enumerate(rs):
+        buf = torch.empty((max(r.tiles_owned(), 1) * 256 * 4,), dtype=torch.float32, device="cuda")
+        r.tiles_pack(buf.data_ptr())
+        r.synchronize()
+        rs[0].tiles_unpack(buf.data_ptr(), k, frame.data_ptr())
+        rs[0].synchronize()
+    _assert_same(frame.cpu().numpy().reshape(-1), want, f"tile gather, slots {slots}")
+    # sparse: render_packed on every rank, assembly on the root
+    per = rs[0].items_live(0)[1]
+    counts = [rs[0].items_live(k)[0] for k in range(N)]
+    slot = max(4, max(counts) * per * 4)
+    src = torch.full((N, slot), float("nan"), dtype=torch.float32, device="cuda")
+    for k, r in enumerate(rs):
+        r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+        r.render_packed(nb, src[k].data_ptr())
+        r.synchronize()
+    frame2 = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+    rs[0].items_unpack_all(src.data_ptr(), slot, frame2.data_ptr())
+    rs[0].synchronize()
+    _assert_same(frame2.cpu().numpy().reshape(-1), want, f"sparse exchange, slots {slots}")

@@ -234,3 +234,17 @@ def test_partition_spreads_centred_geometry_evenly():
     for n in (2, 4, 8):
         share = np.array([np.count_nonzero(live & ptamd.partition_owned(W, H, n, r)) for r in range(n)], float)
         assert share.max() / share.mean() < 1.01, (n, share)
+
+
+def test_partition_slots_masks_tile_the_frame():
+    """pt_set_partition_slots shares: every pixel owned exactly once, and the
+    shares follow the slot counts (box 1080p, the root with 6 of 62 slots)."""
+    W, H = 1920, 1080
+    slots = [6] + [8] * 7
+    m = np.stack([ptamd.partition_owned(W, H, 8, r, slots) for r in range(8)])
+    assert np.all(m.sum(0) == 1)
+    share = m.reshape(8, -1).mean(1)
+    assert abs(share[0] / share[1:].mean() - 6 / 8) < 0.02
+    for n in (2, 3):   # one slot each is the plain partition
+        for r in range(n):
+            assert np.array_equal(ptamd.partition_owned(W, H, n, r, [1] * n), ptamd.partition_owned(W, H, n, r))
