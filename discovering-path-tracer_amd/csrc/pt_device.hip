@@ -364,11 +364,12 @@ __device__ __forceinline__ void add_ctr(Ctr& a, const Ctr& b) {
 #ifndef PT_PARK
 #define PT_PARK 1
 #endif
-// Parking in the paired walks of device-memory scenes (38 instead of 45
-// spilled VGPRs) measured neutral (sphere 5K tris +-0.3 %, 20K cloud -0.8 %):
-// off by default.
+// Parking in the paired walks of device-memory scenes (25 instead of 35
+// spilled VGPRs, at 5 waves/SIMD): sphere 5K tris -1.0 %, 20K cloud -2.0 %
+// (neutral while the k+1 prefetch held 8 more registers).  4 waves without
+// spills: +12 %.
 #ifndef PT_PARK_FUSED
-#define PT_PARK_FUSED 0
+#define PT_PARK_FUSED 1
 #endif
 constexpr int kPark = (PT_PARK || PT_PARK_FUSED) ? 12 : 0;   // floats of path state parked in LDS around a walk
 __device__ __forceinline__ void park3(float* pk, int i, v3 v) {
