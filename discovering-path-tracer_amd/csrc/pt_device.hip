@@ -118,7 +118,11 @@ __device__ __forceinline__ void test_candidates(const RenderParams& P, v3 o, v3 
   }
 }
 
-template <bool STATS, bool PF>
+// FLUSH_OUT: the candidate queue is tested when the walk ends or the queue is
+// full, by an outer loop around the node loop, instead of by a branch inside
+// it.  Device-memory walks (path_trace_fused) gain 7 % (sphere 5K tris);
+// LDS walks lose 1.6 % (box), so they keep the inner branch.
+template <bool STATS, bool PF, bool FLUSH_OUT = false>
 __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* cand) {
   const v3 inv = mk(rcp_(d.x), rcp_(d.y), rcp_(d.z));
   float best = 1e30f;
@@ -128,6 +132,8 @@ __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* can
   const int n = P.n_nodes;
   float4 a = P.nodes[0], b = P.nodes[1];
   while (k < n) {
+   // FLUSH_OUT: walk until the walk ends or the queue is full, then test it
+   while (k < n && (!FLUSH_OUT || nc < kCand)) {
     float4 na, nb;
     if (PF) {
       na = P.nodes[2 * k + 2];
@@ -143,7 +149,7 @@ __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* can
     const bool leaf_hit = h && tri >= 0;
     if (STATS) c.leaves += leaf_hit ? 1u : 0u;
     nc += leaf_hit ? 1 : 0;
-    if (nc == kCand) {
+    if (!FLUSH_OUT && nc == kCand) {
       test_candidates(P, o, d, cand, nc, &best, &bt);
       nc = 0;
     }
@@ -156,6 +162,11 @@ __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* can
       b = P.nodes[2 * next + 1];
     }
     k = next;
+   }
+   if (FLUSH_OUT && nc == kCand) {
+     test_candidates(P, o, d, cand, nc, &best, &bt);
+     nc = 0;
+   }
   }
   test_candidates(P, o, d, cand, nc, &best, &bt);
   Hit r;
@@ -538,7 +549,7 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
     float tl;
     if (intersect_area_light(ro, rd, L, &tl)) {
       if (!have_h0) {
-        h0 = trace_closest<false, PF>(P, ro, rd, c, cand);
+        h0 = trace_closest<false, PF, true>(P, ro, rd, c, cand);
         have_h0 = true;
       }
       if (h0.tri < 0 || h0.t > tl) return mk(L.inten[0], L.inten[1], L.inten[2]);
@@ -552,12 +563,12 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
     Hit h;
     if (depth == 0) {
       if (!have_h0) {
-        h0 = trace_closest<false, PF>(P, ro, rd, c, cand);
+        h0 = trace_closest<false, PF, true>(P, ro, rd, c, cand);
         have_h0 = true;
       }
       h = h0;
     } else {
-      PT_WALK2(PARK, h = (trace_closest<false, PF>(P, ro, rd, c, cand)));
+      PT_WALK2(PARK, h = (trace_closest<false, PF, true>(P, ro, rd, c, cand)));
     }
     if (h.tri < 0) {
       rad = add(rad, mul(thr, mk(0.0f, 0.0f, 0.0f)));  // background (:336)
