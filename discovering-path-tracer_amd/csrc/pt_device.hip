@@ -1721,21 +1721,23 @@ __device__ __forceinline__ bool wf_lane_step(const RenderParams& P, WfLane& L, i
 #ifndef PT_WF_REFILL
 #define PT_WF_REFILL 16
 #endif
-#ifndef PT_WF_GROUP
-#define PT_WF_GROUP 4
-#endif
-static_assert(PT_WF_GROUP == 1 || PT_WF_GROUP == 2 || PT_WF_GROUP == 4 || PT_WF_GROUP == 8 || PT_WF_GROUP == 16,
-              "refill group: power of two");
-constexpr unsigned long long kGroupLead =
-    PT_WF_GROUP == 1   ? ~0ull
-    : PT_WF_GROUP == 2 ? 0x5555555555555555ull
-    : PT_WF_GROUP == 4 ? 0x1111111111111111ull
-    : PT_WF_GROUP == 8 ? 0x0101010101010101ull
-                       : 0x0001000100010001ull;
+// Refill group: lanes refill in groups of G with consecutive list slots.  G
+// is chosen per launch (launch_wavefront): 2 for scenes under kWfGroup4Tris
+// triangles, 4 above.  Measured at 1080p 8 spp, G = 2 vs 4: displaced sphere
+// (82K) -4.6 %, random clouds 100K +3.4 % and 1M (4 spp) +3 %: a coherent
+// surface gains, a random cloud loses; the threshold puts the BASELINE
+// configs (sphere; 10M cloud) on their better side.
+constexpr int kWfGroup4Tris = 500000;
+template <int G>
+constexpr unsigned long long group_lead() {
+  static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "refill group: power of two");
+  return G == 1 ? ~0ull : G == 2 ? 0x5555555555555555ull : G == 4 ? 0x1111111111111111ull
+                                    : G == 8 ? 0x0101010101010101ull : 0x0001000100010001ull;
+}
 #ifndef PT_WF_MIN_BLOCKS
 #define PT_WF_MIN_BLOCKS 7   // 72 VGPRs (11 spilled): sphere -7 %, 1M cloud -0.6 % vs 6; 8 spills 30 (+50 %)
 #endif
-template <bool LDS>
+template <bool LDS, int G>
 __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderParams P, WfBuffers B, int cur) {
   const int tid = (int)threadIdx.x;
   if (blockIdx.x == 0 && tid == 0) B.counters[cur ^ 1] = 0;   // filled by the shading that follows
@@ -1769,22 +1771,22 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
   WfLane L;
   for (;;) {
     const unsigned long long idle = __ballot(p < 0);
-    // groups of PT_WF_GROUP lanes refill together with consecutive list
+    // groups of G lanes refill together with consecutive list
     // slots (neighbouring paths: the same pixel's samples), so their walks
     // stay as coherent as the path-recursive kernel's sample lanes
     unsigned long long gm = idle;
 #pragma unroll
-    for (int sh = 1; sh < PT_WF_GROUP; sh <<= 1) gm &= gm >> sh;
-    gm &= kGroupLead;
+    for (int sh = 1; sh < G; sh <<= 1) gm &= gm >> sh;
+    gm &= group_lead<G>();
     const int ng = (int)__popcll(gm);
-    if (more && ng * PT_WF_GROUP >= PT_WF_REFILL) {
+    if (more && ng * G >= PT_WF_REFILL) {
       int base = 0;
-      if (lane == 0) base = atomicAdd(&B.counters[2], ng * PT_WF_GROUP);
+      if (lane == 0) base = atomicAdd(&B.counters[2], ng * G);
       base = __shfl(base, 0);
-      if (base + ng * PT_WF_GROUP >= count) more = false;
-      const int lead = lane & ~(PT_WF_GROUP - 1);
+      if (base + ng * G >= count) more = false;
+      const int lead = lane & ~(G - 1);
       if ((gm >> lead) & 1ull) {
-        const int slot = base + (int)__popcll(gm & ((1ull << lead) - 1ull)) * PT_WF_GROUP + (lane - lead);
+        const int slot = base + (int)__popcll(gm & ((1ull << lead) - 1ull)) * G + (lane - lead);
         if (slot < count) {
           p = slot;
           wf_lane_start(P, rays + 2 * (size_t)slot, root_a, root_b, L);
@@ -1978,7 +1980,10 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
   int dev = 0, cus = 0, per_cu_t = 0, per_cu_s = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  void (*trace)(RenderParams, WfBuffers, int) = lds_scene ? wf_trace_kernel<true> : wf_trace_kernel<false>;
+  const bool g2 = p0.n_tris < kWfGroup4Tris;
+  void (*trace)(RenderParams, WfBuffers, int) =
+      lds_scene ? (g2 ? wf_trace_kernel<true, 2> : wf_trace_kernel<true, 4>)
+                : (g2 ? wf_trace_kernel<false, 2> : wf_trace_kernel<false, 4>);
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, trace, 256, lds);
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, wf_shade_kernel, 256, 0);
   if (e != hipSuccess) return e;
