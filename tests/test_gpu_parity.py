@@ -702,3 +702,8 @@ def test_partition_slots_sum_and_sparse_exchange(slots):
     rs[0].items_unpack_all(src.data_ptr(), slot, frame2.data_ptr())
     rs[0].synchronize()
     _assert_same(frame2.cpu().numpy().reshape(-1), want, f"sparse exchange, slots {slots}")
+    for bad in ([0] + slots[1:], [65] + slots[1:]):   # 1..64 slots per rank
+        with pytest.raises(ptamd.PTError):
+            rs[0].set_partition(N, 0, bad)
+    with pytest.raises(ptamd.PTError):
+        rs[0].set_partition(N, 0, slots[:-1])
