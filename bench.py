@@ -534,6 +534,11 @@ def main():
                                        f"{args.streams} streams)" if args.streams > 1 else "kernel_ms",
                          "algorithmic_bytes_per_launch": int(own_bytes)},
         }
+        if r.last_kernel() == 1 and achieved > HBM_PEAK_GBS:
+            out_line["roofline"]["note"] = ("frac > 1: the scene is staged in LDS per workgroup, so the algorithmic "
+                                            "node/triangle bytes are served from LDS; HBM sees `traffic` (about one "
+                                            "frame write per launch).  The launch is bound by VALU issue and LDS "
+                                            "latency: see roofline_valu")
         if prof is not None and prof[2]:
             # the box frame is bound by vector-instruction issue, not HBM (its
             # scene lives in LDS): VALU wave-instructions per launch from the
