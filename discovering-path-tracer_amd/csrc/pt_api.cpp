@@ -356,6 +356,17 @@ struct pt_context {
   // waits for the last one when it runs on another stream (order_shared).
   hipEvent_t shared_ev = nullptr;
   hipStream_t shared_stream = nullptr;
+  // Every stream this context has enqueued work on that reads its buffers
+  // (node/triangle arrays, item tables, accumulation and wavefront buffers),
+  // with an event recorded after the last such work (note_use).  A host-side
+  // rebuild of those buffers waits on these events only (quiesce), never on
+  // the whole device, so it does not wait on another component's RCCL or
+  // torch work sharing the GPU.
+  struct Use {
+    hipStream_t stream;
+    hipEvent_t ev;
+  };
+  std::vector<Use> uses;
   int rb_next_ticket = 1;
   bool timed = false;
   // ring of event pairs, one per render launch since pt_reset_launch_times
@@ -389,16 +400,39 @@ static int order_shared(pt_context* c) {
   if (c->shared_stream && c->shared_stream != c->stream) PT_HIP(hipStreamWaitEvent(c->stream, c->shared_ev, 0));
   return PT_OK;
 }
+// After enqueueing work that reads or writes context-owned buffers on
+// c->stream: record it in that stream's use event (a context rarely sees more
+// than a handful of streams; past kMaxUses the oldest entry is waited for and
+// dropped).
+constexpr size_t kMaxUses = 16;
+static int note_use(pt_context* c) {
+  for (auto& u : c->uses)
+    if (u.stream == c->stream) {
+      PT_HIP(hipEventRecord(u.ev, c->stream));
+      return PT_OK;
+    }
+  if (c->uses.size() >= kMaxUses) {
+    PT_HIP(hipEventSynchronize(c->uses.front().ev));
+    PT_HIP(hipEventDestroy(c->uses.front().ev));
+    c->uses.erase(c->uses.begin());
+  }
+  pt_context::Use u{c->stream, nullptr};
+  PT_HIP(hipEventCreateWithFlags(&u.ev, hipEventDisableTiming));
+  c->uses.push_back(u);
+  PT_HIP(hipEventRecord(u.ev, c->stream));
+  return PT_OK;
+}
 // After it (or after the last launch that reads those buffers back).
 static int mark_shared(pt_context* c) {
   PT_HIP(hipEventRecord(c->shared_ev, c->stream));
   c->shared_stream = c->stream;
-  return PT_OK;
+  return note_use(c);
 }
 // Before buffers that launches on any stream may still read are freed or
-// overwritten from the host (list rebuilds, reallocation): all of them done.
+// overwritten from the host (list rebuilds, reallocation): wait for this
+// context's own work on every stream it used -- not for the whole device.
 static int quiesce(pt_context* c) {
-  PT_HIP(hipDeviceSynchronize());
+  for (auto& u : c->uses) PT_HIP(hipEventSynchronize(u.ev));
   return PT_OK;
 }
 
@@ -499,9 +533,11 @@ static void item_lists(const ptd::RenderParams& p, const ptd::Part& part, std::v
 
 static int compact_items(pt_context* c, ptd::RenderParams* p) {
   const ptd::Part pt = part_of(c, p->rank);
+  // every slot position of this rank's share: two slot sets with the same
+  // period, count and first position still deal different tiles
   std::vector<float> key = {(float)p->width, (float)p->height, (float)pt.m, (float)pt.cnt,
-                            (float)pt.pos[0], (float)p->rank, (float)p->spl,
-                            (float)p->n_cull, (float)p->item_order};
+                            (float)p->rank, (float)p->spl, (float)p->n_cull, (float)p->item_order};
+  for (int k = 0; k < pt.cnt; ++k) key.push_back((float)pt.pos[k]);
   for (int r = 0; r < p->n_cull; ++r) key.insert(key.end(), p->cull[r], p->cull[r] + 4);
   if (key.size() != c->items_key.size() || memcmp(key.data(), c->items_key.data(), key.size() * 4) != 0) {
     std::vector<int> live, culled;
@@ -783,6 +819,9 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   if (shared) {
     const int rm = mark_shared(c);
     if (rm) return rm;
+  } else {
+    const int ru = note_use(c);   // render_packed reads the scene and item tables
+    if (ru) return ru;
   }
   if (timed) {
     PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
@@ -838,6 +877,9 @@ int pt_destroy(pt_context* c) {
   if (!c) return PT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)quiesce(c);
+  for (auto& u : c->uses) (void)hipEventDestroy(u.ev);
+  c->uses.clear();
   dev_free(c->d_nodes);
   dev_free(c->d_nodes_full);
   dev_free(c->d_tris);
@@ -981,6 +1023,7 @@ int pt_set_partition(pt_context* c, int nranks, int rank) {
   c->nranks = nranks;
   c->rank = rank;
   c->slots.assign((size_t)nranks, 1);
+  c->items_key.clear();   // the cached item lists follow the partition
   return PT_OK;
 }
 
@@ -996,6 +1039,7 @@ int pt_set_partition_slots(pt_context* c, int nranks, int rank, const int* slots
   c->nranks = nranks;
   c->rank = rank;
   c->slots.assign(slots, slots + nranks);
+  c->items_key.clear();
   return PT_OK;
 }
 
@@ -1150,6 +1194,10 @@ int pt_readback_begin(pt_context* c, int* ticket) {
     if (ro) return ro;
   }
   PT_HIP(hipMemcpyAsync(r.dev, c->d_accum, bytes, hipMemcpyDeviceToDevice, c->stream));
+  {
+    const int ru = note_use(c);
+    if (ru) return ru;
+  }
   PT_HIP(hipEventRecord(r.snap, c->stream));
   PT_HIP(hipStreamWaitEvent(c->copy_stream, r.snap, 0));
   PT_HIP(hipMemcpyAsync(r.host, r.dev, bytes, hipMemcpyDeviceToHost, c->copy_stream));
@@ -1261,7 +1309,7 @@ int pt_tiles_unpack(pt_context* c, const void* src, int src_rank, void* frame) {
   }
   PT_HIP(ptd::launch_tiles(false, (float4*)frame, (float4*)src, c->width, c->height, part_of(c, src_rank),
                            c->d_parts + (size_t)src_rank * ptd::kMaxSlots, c->stream));
-  return PT_OK;
+  return note_use(c);
 }
 
 // ---- sparse tile exchange (live items only) --------------------------------
@@ -1309,7 +1357,7 @@ int pt_items_unpack_all(pt_context* c, const void* src, size_t slot_floats, void
   if (rc) return rc;
   PT_HIP(ptd::launch_items_unpack(c->last, (float4*)frame, (const float4*)src, slot_floats / 4, c->d_unpack,
                                   c->n_unpack, c->stream));
-  return PT_OK;
+  return note_use(c);
 }
 
 int pt_set_stats_mode(pt_context* c, int enabled) {
@@ -1335,7 +1383,7 @@ int pt_reset_stats(pt_context* c) {
   if (!c) return fail(PT_ERR_INVALID, "null context");
   PT_HIP(hipSetDevice(c->device));
   PT_HIP(hipMemsetAsync(c->d_stats, 0, 4 * sizeof(unsigned long long), c->stream));
-  return PT_OK;
+  return note_use(c);
 }
 
 int pt_last_launch_ms(pt_context* c, float* ms) {

@@ -363,6 +363,7 @@ struct Scene {
   const uint32_t* I;
   const float* N;          // BVHNode[] as 8 floats
   size_t nn;
+  bool int_bits = false;   // child/triangle links stored as int32 bit patterns (PT_NODES_INT_BITS)
   std::vector<Light> lights;
   vec3 cpos, cdir, cup;
   float fov;
@@ -418,8 +419,16 @@ static Hit trace(const Scene& s, vec3 o, vec3 d, Stats* st) {
     const float* n = s.N + (size_t)ni * 8;
     st->nodes++;
     if (aabb(o, d, V(n[0], n[1], n[2]), V(n[4], n[5], n[6]))) {
-      int l = (int)n[3];
-      int r = (int)n[7];
+      int l, r;
+      if (s.int_bits) {
+        // N >= 2^24 layout variant: the float cannot hold the index exactly
+        // (BoundingVolumeHierarchy.cpp:74,77), so it travels as int32 bits
+        memcpy(&l, &n[3], 4);
+        memcpy(&r, &n[7], 4);
+      } else {
+        l = (int)n[3];                                           // :173-174
+        r = (int)n[7];
+      }
       if (l == -1) {
         uint32_t ti = (uint32_t)r;
         vec3 v0 = vtx(s, s.I[ti * 3 + 0]);
@@ -654,15 +663,20 @@ int oracle_bvh_build(const float* verts, const uint32_t* idx_in, size_t n_idx,
 // that % nranks == rank.
 // accum is W*H*4 floats (RGBA32F, row-major, y*W+x), read-modify-written.
 // stats[0..2] += traceRay calls, nodes visited, leaf triangle tests.
-int oracle_render(const float* verts, const uint32_t* idx, const float* nodes, size_t n_nodes,
-                  const float* camera16, const float* lights16, size_t n_lights,
-                  int W, int H, uint32_t first_batch, uint32_t n_batches,
-                  int max_depth, int sss_bounces,
-                  int row_stride, int row_phase, int tile, int nranks, int rank,
-                  float* accum, uint64_t* stats, int nthreads) {
+// flags: ORACLE_INT_BITS = node links are int32 bit patterns.
+// Threads take runs of 32 pixels of the selected rows (a row subset of a
+// large scene is then balanced over the threads).
+enum { ORACLE_INT_BITS = 1 };
+int oracle_render_ex(const float* verts, const uint32_t* idx, const float* nodes, size_t n_nodes,
+                     const float* camera16, const float* lights16, size_t n_lights,
+                     int W, int H, uint32_t first_batch, uint32_t n_batches,
+                     int max_depth, int sss_bounces,
+                     int row_stride, int row_phase, int tile, int nranks, int rank,
+                     float* accum, uint64_t* stats, int nthreads, uint32_t flags) {
   if (W <= 0 || H <= 0 || n_nodes == 0 || row_stride <= 0 || tile <= 0 || nranks <= 0) return -1;
   Scene S;
   S.V = verts; S.I = idx; S.N = nodes; S.nn = n_nodes;
+  S.int_bits = (flags & ORACLE_INT_BITS) != 0;
   S.cpos = V(camera16[0], camera16[1], camera16[2]);
   S.cdir = V(camera16[4], camera16[5], camera16[6]);
   S.cup = V(camera16[8], camera16[9], camera16[10]);
@@ -680,15 +694,22 @@ int oracle_render(const float* verts, const uint32_t* idx, const float* nodes, s
   const int tiles_x = (W + tile - 1) / tile;
   if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
   if (nthreads <= 0) nthreads = 1;
-  std::atomic<int> next_row{0};
+  std::vector<int> rows;
+  for (int y = 0; y < H; ++y)
+    if (y % row_stride == row_phase) rows.push_back(y);
+  constexpr int kRun = 32;
+  const int runs_per_row = (W + kRun - 1) / kRun;
+  const long long n_runs = (long long)rows.size() * runs_per_row;
+  std::atomic<long long> next_run{0};
   std::vector<Stats> per(nthreads);
   auto work = [&](int tid) {
     Stats& st = per[tid];
     for (;;) {
-      int y = next_row.fetch_add(1);
-      if (y >= H) break;
-      if (y % row_stride != row_phase) continue;
-      for (int x = 0; x < W; ++x) {
+      const long long j = next_run.fetch_add(1);
+      if (j >= n_runs) break;
+      const int y = rows[(size_t)(j / runs_per_row)];
+      const int x0 = (int)(j % runs_per_row) * kRun, x1 = std::min(W, x0 + kRun);
+      for (int x = x0; x < x1; ++x) {
         // partition order of the product (pt_device.h tile_block): rows rotated by their index
         const int by = y / tile, bx = x / tile;
         const int tid2 = by * tiles_x + (bx - by % tiles_x + tiles_x) % tiles_x;
@@ -709,6 +730,17 @@ int oracle_render(const float* verts, const uint32_t* idx, const float* nodes, s
     for (auto& s : per) { stats[0] += s.rays; stats[1] += s.nodes; stats[2] += s.leaves; }
   }
   return 0;
+}
+
+int oracle_render(const float* verts, const uint32_t* idx, const float* nodes, size_t n_nodes,
+                  const float* camera16, const float* lights16, size_t n_lights,
+                  int W, int H, uint32_t first_batch, uint32_t n_batches,
+                  int max_depth, int sss_bounces,
+                  int row_stride, int row_phase, int tile, int nranks, int rank,
+                  float* accum, uint64_t* stats, int nthreads) {
+  return oracle_render_ex(verts, idx, nodes, n_nodes, camera16, lights16, n_lights, W, H, first_batch, n_batches,
+                          max_depth, sss_bounces, row_stride, row_phase, tile, nranks, rank, accum, stats,
+                          nthreads, 0u);
 }
 
 // Math entry points for tests/test_math.py (bitwise agreement with the

@@ -34,6 +34,7 @@ def lib():
                                     ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     F32P, U64P, ctypes.c_int]
+        L.oracle_render_ex.argtypes = L.oracle_render.argtypes + [ctypes.c_uint32]
         L.oracle_math.argtypes = [ctypes.c_int, F32P, F32P, sz]
         L.oracle_rng.argtypes = [ctypes.c_uint32, F32P, sz]
         L.oracle_trace.argtypes = [F32P, U32P, F32P, sz, F32P, F32P, F32P, U64P]
@@ -70,16 +71,21 @@ def bvh_build(verts, idx):
 
 def render(verts, idx, nodes, camera16, lights16, W, H, first_batch=0, n_batches=1,
            max_depth=4, sss_bounces=3, row_stride=1, row_phase=0, tile=16, nranks=1, rank=0,
-           accum=None, nthreads=0):
+           accum=None, nthreads=0, int_bits=False):
+    """Sequential 1-spp batches of raytrace_comp.comp over the selected pixels.
+    int_bits: the nodes' link fields are int32 bit patterns (PT_NODES_INT_BITS,
+    the >= 2^24-node layout) instead of float-encoded indices."""
     if accum is None:
         accum = np.zeros(W * H * 4, np.float32)
     stats = np.zeros(3, np.uint64)
     lights16 = np.ascontiguousarray(lights16, np.float32).reshape(-1)
-    rc = lib().oracle_render(np.ascontiguousarray(verts, np.float32), np.ascontiguousarray(idx, np.uint32),
-                             np.ascontiguousarray(nodes, np.float32), nodes.size // 8,
-                             np.ascontiguousarray(camera16, np.float32), lights16, lights16.size // 16,
-                             W, H, first_batch, n_batches, max_depth, sss_bounces,
-                             row_stride, row_phase, tile, nranks, rank, accum, stats, nthreads)
+    nodes = np.ascontiguousarray(nodes, np.float32).reshape(-1)
+    rc = lib().oracle_render_ex(np.ascontiguousarray(verts, np.float32), np.ascontiguousarray(idx, np.uint32),
+                                nodes, nodes.size // 8,
+                                np.ascontiguousarray(camera16, np.float32), lights16, lights16.size // 16,
+                                W, H, first_batch, n_batches, max_depth, sss_bounces,
+                                row_stride, row_phase, tile, nranks, rank, accum, stats, nthreads,
+                                1 if int_bits else 0)
     if rc:
         raise ValueError(f"oracle_render rc={rc}")
     return accum, stats

@@ -243,10 +243,7 @@ def test_random_triangles(ntri, int_bits):
     r.resize_and_clear(96, 64)
     r.render(0, 2)
     gpu = r.read_accum()
-    if int_bits:   # the oracle reads the reference float layout: re-encode exactly
-        s2 = ptamd.Scene.from_arrays(tv, ti).build_bvh(int_bits=False)
-        v, i, n, _, _ = s2.arrays()
-    ref, _ = _oracle(v, i, n, 96, 64, nb=2, cam=cam)
+    ref, _ = _oracle(v, i, n, 96, 64, nb=2, cam=cam, int_bits=int_bits)
     _assert_same(gpu, ref, f"random {ntri}")
 
 
@@ -707,3 +704,34 @@ def test_partition_slots_sum_and_sparse_exchange(slots):
             rs[0].set_partition(N, 0, bad)
     with pytest.raises(ptamd.PTError):
         rs[0].set_partition(N, 0, slots[:-1])
+
+
+def test_reslotting_one_renderer_keeps_item_lists_right():
+    """Re-slotting a live context ([3,3,1] -> [3,2,2]: same period, count and
+    first slot position for rank 0, different tiles) must rebuild the cached
+    compact-launch item lists: the -0/+0 partials of the re-slotted renderers
+    still sum to the oracle's frame, and each rank's sparse live-item pack
+    assembles it (items_key lacked the other slot positions)."""
+    import torch
+    v, i, n = _box()
+    W, H, nb = 150, 70, 3
+    want, _ = _oracle(v, i, n, W, H, nb=nb, cam=CULL_CAMS[1])
+    rs = [_setup(v, i, n, cam=CULL_CAMS[1]) for _ in range(3)]
+    for slots in ([3, 3, 1], [3, 2, 2], [1, 1, 1]):
+        acc = np.full(W * H * 4, -0.0, np.float32)
+        for rank, r in enumerate(rs):
+            r.set_partition(3, rank, slots)
+            r.resize_and_clear(W, H)
+            r.render(0, nb)
+            acc = (acc + r.read_accum()).astype(np.float32)
+        _assert_same(acc, want, f"sum after re-slotting to {slots}")
+        per = rs[0].items_live(0)[1]
+        slot = max(max(rs[0].items_live(k)[0] for k in range(3)) * per * 4, 4)
+        recv = torch.zeros((3, slot), dtype=torch.float32, device="cuda")
+        for rank, r in enumerate(rs):
+            r.items_pack(recv[rank].data_ptr())
+            r.synchronize()
+        frame = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+        rs[0].items_unpack_all(recv.data_ptr(), slot, frame.data_ptr())
+        rs[0].synchronize()
+        _assert_same(frame.cpu().numpy().reshape(-1), want, f"sparse exchange after re-slotting to {slots}")
