@@ -15,6 +15,25 @@ Mrays/s counts the reference's traceRay invocations of all kinds: light
 pre-pass, primary/bounce, shadow, SSS and SSS-shadow.  A stats-mode pass of
 the same frame, run before the timed region, measures them.
 
+The kernel skips work the reference does without changing a bit of the
+output (culled primary rays, shadow rays whose answer cannot change the
+image, the repeated pre-pass ray): a counting pass of the fast kernel
+(PT_OPT_COUNT_TRACED, untimed) reports the walks it really starts as
+config.rays_traced next to the reference-equivalent rays_per_frame.
+
+roofline (the dominant kernel): HBM bytes per launch from the committed
+rocprofv3 FETCH_SIZE/WRITE_SIZE summary of this exact kernel source
+(profiles/, matched by SHA-1 of pt_device.hip and by workload) over the
+kernel time measured here with HIP events.  The algorithmic bytes of
+SURVEY §8d (exhaustive reference counts) over the same time are reported as
+effective_GBps: on box.obj the scene is staged in LDS, so that figure is far
+above the HBM peak and is not a bandwidth.
+
+At N = 1 the line also carries `configs`: config 3 (the level-6 displaced
+icosphere standing in for the missing Sylveon.obj) and config 5 (10M random
+triangles) at 1920x1080x8spp, each timed, counted and roofline-priced the
+same way (--no-scene-legs skips them).
+
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run, one process per GPU.  Rank 0 prints one JSON line.
 Other workloads: --scene sphere (the labelled Sylveon substitute) or
@@ -64,33 +83,65 @@ def load_scene(name):
     raise SystemExit(f"unknown scene {name}")
 
 
-def profiled_traffic():
-    """HBM bytes per launch of the current kernel source from the newest
-    committed rocprofv3 PMC summary (tools/gpu_profile.sh ->
-    tools/summarize_profile.py): FETCH_SIZE (x2, gfx950) + WRITE_SIZE.
-    None if no summary was taken of this exact pt_device.hip.  Also returns
-    the summary's VALU wave-instruction count per launch when present."""
-    import glob
+def kernel_sha1():
     import hashlib
     src = os.path.join(ROOT, "discovering-path-tracer_amd", "csrc", "pt_device.hip")
-    h = hashlib.sha1(open(src, "rb").read()).hexdigest()
+    return hashlib.sha1(open(src, "rb").read()).hexdigest()
+
+
+def profiled_traffic(workload=None):
+    """HBM bytes per launch (per frame for the wavefront pipeline) of the
+    current kernel source from the newest committed rocprofv3 PMC summary
+    (tools/gpu_profile.sh / tools/gpu_scene_profile.sh ->
+    tools/summarize_profile.py) whose pt_device.hip SHA-1 and workload match.
+    None if there is none.  Returns the summary dict and its path."""
+    import glob
+    h = kernel_sha1()
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "*_summary.json"), recursive=True)):
         try:
             d = json.load(open(p))
         except ValueError:
             continue
-        if d.get("pt_device_hip_sha1") == h and "hbm_bytes_per_launch" in d:
-            best = (os.path.relpath(p, ROOT), d["hbm_bytes_per_launch"]["total"],
-                    d.get("sq_per_launch", {}).get("SQ_INSTS_VALU"))
+        if d.get("pt_device_hip_sha1") != h or "hbm_bytes_per_launch" not in d:
+            continue
+        if workload is not None and d.get("workload") != workload:
+            continue
+        if workload is None and d.get("workload") not in (None, "box"):
+            continue
+        best = (os.path.relpath(p, ROOT), d)
     return best
+
+
+def cpu_threads():
+    """Cores this process can actually use: its sched affinity, capped by the
+    cgroup CPU quota (the GPU box shows all 256 host CPUs but grants 16 --
+    256 threads on a 16-CPU quota measured 22 Mrays/s against 33 on 16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    q = cpu_quota()
+    if q is not None:
+        n = min(n, max(1, int(-(-q // 1))))
+    return n
+
+
+def cpu_quota():
+    """cgroup v2 CPU quota in CPUs (None when unlimited or unreadable)."""
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline(v, i, n, cam, light, W, H, spp, DEPTH, SSS):
     """The oracle (scalar C++ restatement of raytrace_comp.comp) on this host,
-    all cores, on a bounded sample of the same workload."""
+    on every CPU the process may use, on a bounded sample of the same
+    workload, plus the same traversal on one core."""
     import oracle_lib
-    threads = min(16, os.cpu_count() or 1)
+    threads = cpu_threads()
     stride = 1 if W * H <= 1920 * 1080 else 4
     oracle_lib.render(v, i, n.reshape(-1), cam, light, 64, 64, n_batches=1, nthreads=threads)   # warm
     t0 = time.perf_counter()
@@ -106,13 +157,136 @@ def cpu_baseline(v, i, n, cam, light, W, H, spp, DEPTH, SSS):
     return {"value": round(float(st[0]) / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"rows y%{stride}==0 of the same {W}x{H}x{spp}spp frame ({H // stride} rows, "
                       f"{int(st[0])} rays, {dt:.2f} s, {threads} std::threads, oracle/pt_oracle.cpp)",
-            "host_cpus_visible": os.cpu_count(),
+            "host_cpus_visible": os.cpu_count(), "cpus_allowed": threads, "cgroup_cpu_quota": cpu_quota(),
             "single_thread": {"value": round(float(st1[0]) / dt1 / 1e6, 3), "unit": "Mrays/s", "cores": 1,
                               "sample": f"rows y%{s1}==0 ({int(st1[0])} rays, {dt1:.2f} s)"}}
 
 
 KERNEL_NAMES = {1: "render_kernel<false,*>", 2: "render_sm_kernel<false,*>",
                 3: "wavefront pipeline (wf_gen + wf_trace/wf_shade x rays + wf_fold), per frame"}
+
+TRACED_KEYS = ("closest_walks", "shadow_walks", "nodes", "tri_tests", "primaries")
+
+
+def reference_and_traced_counts(r, spp):
+    """One untimed frame in stats mode (the reference-exhaustive traversal:
+    every traceRay with its exhaustive node and leaf counts) and one with the
+    fast kernel's counters on (PT_OPT_COUNT_TRACED: the walks, node visits
+    and triangle tests it really performs).  Both frames are bit-identical
+    to the timed ones."""
+    import ptamd
+    r.set_stats_mode(True)
+    r.reset_stats()
+    r.clear()
+    r.render(0, spp)
+    st = r.stats()
+    r.set_stats_mode(False)
+    r.set_option(ptamd.PT_OPT_COUNT_TRACED, 1)
+    r.reset_stats()
+    r.render(0, spp)
+    traced = r.traced()
+    r.set_option(ptamd.PT_OPT_COUNT_TRACED, 0)
+    return np.array([st["rays"], st["nodes"], st["leaf_tests"], st["samples"]], np.float64), traced
+
+
+def add_traced(cfg, traced, seconds_per_frame):
+    """config.rays_traced (walks the kernel really starts: closest-hit plus
+    shadow) beside the reference-equivalent rays_per_frame, and its rate."""
+    rays = traced["closest_walks"] + traced["shadow_walks"]
+    cfg["rays_traced"] = int(rays)
+    cfg["rays_traced_per_s_M"] = round(rays / seconds_per_frame / 1e6, 3)
+    cfg["traced"] = {k: int(traced[k]) for k in TRACED_KEYS}
+    if cfg.get("rays_per_frame"):
+        cfg["rays_traced_frac_of_reference"] = round(rays / cfg["rays_per_frame"], 4)
+
+
+def roofline_block(prof, time_ms, alg_bytes, kernel, kernel_ms, interval_ms, n_timed, time_basis):
+    """The HBM roofline of the dominant kernel: committed-profile HBM bytes per
+    launch (FETCH_SIZE x2 per the guide's gfx950 correction, + WRITE_SIZE)
+    over the kernel time measured in this run.  The algorithmic bytes of
+    SURVEY §8d over the same time are `effective_GBps`."""
+    traffic = None if prof is None else prof[1]["hbm_bytes_per_launch"]["total"]
+    achieved = None if traffic is None else traffic / (time_ms * 1e-3) / 1e9
+    eff = alg_bytes / (time_ms * 1e-3) / 1e9 if alg_bytes else None
+    out = {"bound": "hbm",
+           "achieved": None if achieved is None else round(achieved, 2),
+           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": None if achieved is None else round(achieved / HBM_PEAK_GBS, 5),
+           "traffic": None if traffic is None else int(traffic),
+           "traffic_source": None if prof is None else prof[0],
+           "kernel": kernel, "kernel_ms": round(kernel_ms, 4), "launch_interval_ms": round(interval_ms, 4),
+           "timed_launches": n_timed, "time_basis": time_basis,
+           "algorithmic_bytes_per_launch": None if not alg_bytes else int(alg_bytes),
+           "effective_GBps": None if eff is None else round(eff, 2)}
+    if prof is not None:
+        hb = prof[1]["hbm_bytes_per_launch"]
+        if "raw_fetch_kib" in hb:
+            raw = (hb["raw_fetch_kib"] + hb["raw_write_kib"]) * 1024
+            out["traffic_raw_counters"] = int(raw)
+            out["frac_raw_counters"] = round(raw / (time_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+        if "fetch_calibration" in prof[1]:
+            out["fetch_calibration"] = prof[1]["fetch_calibration"]
+    if traffic is None:
+        out["note"] = "no committed rocprofv3 summary of this kernel source and workload: traffic unmeasured"
+    elif eff is not None and eff > HBM_PEAK_GBS:
+        out["note"] = ("effective_GBps exceeds the HBM peak because the algorithmic node/triangle bytes are "
+                       "served from LDS/L2, not HBM; frac is the measured HBM traffic over the kernel time")
+    return out
+
+
+LEG_WORKLOADS = {"sphere": "sphere_1080p8", "synthetic:10000000": "synthetic10M_1080p8"}
+
+
+def scene_leg(scene_name, W, H, spp, depth, sss, steps, device):
+    """One BASELINE config on one GPU (N = 1 only): the reference rays of a
+    stats-mode frame, the walks of a counting frame, `steps` timed frames
+    after one warmup, and the roofline priced from the committed profile of
+    this workload (tools/gpu_scene_profile.sh)."""
+    import ptamd
+    import scenes
+    import torch
+    t_setup = time.perf_counter()
+    scene, cam, int_bits, desc = load_scene(scene_name)
+    v, i, n, _, _ = scene.arrays()
+    del scene
+    r = ptamd.Renderer(device)
+    r.upload_scene(v, i, n, int_bits=int_bits)
+    ntri = i.size // 3
+    del v, i, n
+    r.upload_lights(scenes.REFERENCE_LIGHT)
+    r.set_camera(cam)
+    r.set_params(depth, sss)
+    r.resize_and_clear(W, H)
+    setup_s = time.perf_counter() - t_setup
+    t0 = time.perf_counter()
+    ref, traced = reference_and_traced_counts(r, spp)
+    counts_s = time.perf_counter() - t0
+    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+    r.render(0, spp)
+    r.synchronize()
+    torch.cuda.synchronize()
+    r.reset_launch_times()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        r.render(0, spp)
+    r.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    kt = r.launch_times_ms()
+    kernel_ms = float(np.mean(kt)) if kt.size else float("nan")
+    alg = algorithmic_bytes({"nodes": ref[1], "leaf_tests": ref[2], "samples": ref[3]})
+    prof = profiled_traffic(LEG_WORKLOADS[scene_name])
+    cfg = {"workload": f"{desc} {W}x{H} {spp}spp {depth} bounces {sss} sss", "triangles": int(ntri),
+           "int_bits_nodes": bool(int_bits), "rays_per_frame": int(ref[0])}
+    add_traced(cfg, traced, dt)
+    out = {"metric": "Mrays/s (reference-equivalent traceRay calls)", "value": round(ref[0] / dt / 1e6, 3),
+           "unit": "Mrays/s", "ms_per_step": round(dt * 1e3, 2), "steps": steps, "warmup": 1,
+           "kernel": KERNEL_NAMES.get(r.last_kernel(), "?"), "config": cfg,
+           "roofline": roofline_block(prof, kernel_ms, alg, KERNEL_NAMES.get(r.last_kernel(), "?"), kernel_ms,
+                                      kernel_ms, int(kt.size), "kernel_ms (HIP events around each frame's "
+                                                               "launches on the render stream)"),
+           "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
+    del r
+    return out
 
 
 class _StreamWork:
@@ -161,8 +335,14 @@ def main():
                     help="gather path: partition slots of the root out of 16 per other rank "
                          "(-1 auto: the root gives up the share its frame assembly costs; 0: equal shares)")
     ap.add_argument("--packed", action="store_true", help="N=1: run the gather path (render_packed + assembly)")
-    ap.add_argument("--compare-no-cull", action="store_true",
-                    help="N=1: also time the same steps with primary-ray culling off (reported as primary_cull_off)")
+    ap.add_argument("--compare-no-cull", type=int, choices=[0, 1], default=None,
+                    help="N=1: also time the same steps with primary-ray culling off (reported as "
+                         "primary_cull_off); default on for the box headline at N=1")
+    ap.add_argument("--no-scene-legs", action="store_true",
+                    help="N=1: skip the config-3 and config-5 legs (`configs` in the JSON line)")
+    ap.add_argument("--profile-run", action="store_true",
+                    help="only the warmup and timed frames (no stats/counting passes, legs or CPU baseline): "
+                         "the command tools/gpu_*profile.sh runs under rocprofv3")
     args = ap.parse_args()
     W, H, SPP = args.width, args.height, args.spp
     if args.streams is None:
@@ -294,24 +474,27 @@ def main():
         r.set_partition(nparts, emu_rank, slots)
         r.resize_and_clear(W, H)
 
-    # Stats pass (untimed): the reference's exact traversal counts for one frame.
-    r.set_stats_mode(True)
-    r.reset_stats()
-    r.clear()
-    r.render(0, SPP)
-    st = r.stats()
-    r.set_stats_mode(False)
-    mine = np.array([st["rays"], st["nodes"], st["leaf_tests"], st["samples"]], np.float64)
-    counts = mine
-    if dist is not None:
-        t = torch.tensor(mine, dtype=torch.float64, device=dev)
+    def sum_ranks(x):
+        if dist is None:
+            return np.asarray(x, np.float64)
+        t = torch.tensor(np.asarray(x, np.float64), dtype=torch.float64, device=dev)
         if backend == "nccl":
             dist.all_reduce(t)
         else:
             t = t.cpu()
             dist.all_reduce(t)
-        counts = t.cpu().numpy()
-    rays_per_frame = float(counts[0])
+        return t.cpu().numpy()
+
+    if args.profile_run:
+        mine = np.zeros(4)
+        rays_per_frame = float("nan")
+        traced = None
+    else:
+        # Stats pass (untimed): the reference's exact traversal counts for one frame.
+        mine, traced = reference_and_traced_counts(r, SPP)
+        counts = sum_ranks(mine)
+        rays_per_frame = float(counts[0])
+        traced = dict(zip(TRACED_KEYS, (int(x) for x in sum_ranks([traced[k] for k in TRACED_KEYS]))))
     # output-invariant kernel options apply to the timed frames (the stats
     # pass above always runs the path-recursive kernel)
     for kv in args.opt:
@@ -453,6 +636,9 @@ def main():
     roof_ms = interval_ms if args.streams > 1 else kernel_ms
 
     no_cull = None
+    default_cfg = args.scene == "box" and (W, H, SPP, DEPTH, SSS) == (1920, 1080, 8, 4, 3)
+    if args.compare_no_cull is None:
+        args.compare_no_cull = int(world == 1 and emu == 1 and default_cfg and not args.packed and not args.profile_run)
     if world == 1 and args.compare_no_cull:
         # the same frames with primary-ray culling off (every pixel generated
         # and traced), for reference next to the default
@@ -494,15 +680,14 @@ def main():
     if rank == 0:
         ms_per_step = dt / args.steps * 1e3
         value = rays_per_frame * args.steps / dt / 1e6
+        value = None if value != value else value
         # per-GPU launch: rank 0's share of the algorithmic bytes over the slowest rank's kernel time
         own_bytes = algorithmic_bytes({"nodes": mine[1], "leaf_tests": mine[2], "samples": mine[3]})
-        achieved = own_bytes / (roof_ms * 1e-3) / 1e9
-        default_cfg = args.scene == "box" and (W, H, SPP, DEPTH, SSS) == (1920, 1080, 8, 4, 3)
         prof = profiled_traffic() if (world == 1 and emu == 1 and default_cfg and not args.packed) else None
         wl = f"{scene_desc} {W}x{H} {SPP}spp {DEPTH} bounces {SSS} sss"
         out_line = {
             "metric": "Mrays/s at 1920x1080x8spp, box.obj BVH" if default_cfg else f"Mrays/s, {wl}",
-            "value": round(value, 3),
+            "value": None if value is None else round(value, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -520,33 +705,25 @@ def main():
                        "parallelism": (f"tiles{world}-" + ("sparse-gather" if args.collective == "gather" else "reduce"))
                        if world > 1 else ("single-packed" if args.packed else "single"),
                        "streams": args.streams,
-                       "rays_per_frame": int(rays_per_frame),
+                       "rays_per_frame": None if rays_per_frame != rays_per_frame else int(rays_per_frame),
                        "primary_cull": True,
                        "msamples_per_s": round(W * H * SPP * args.steps / dt / 1e6, 3)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None if prof is None else int(prof[1]),
-                         "traffic_source": None if prof is None else prof[0],
-                         "kernel": KERNEL_NAMES.get(r.last_kernel(), "?"), "kernel_ms": round(kernel_ms, 4),
-                         "launch_interval_ms": round(interval_ms, 4),
-                         "timed_launches": int(kt.size),
-                         "time_basis": "launch_interval_ms (busy span / launches; launches overlap on "
-                                       f"{args.streams} streams)" if args.streams > 1 else "kernel_ms",
-                         "algorithmic_bytes_per_launch": int(own_bytes)},
+            "roofline": roofline_block(prof, roof_ms, own_bytes, KERNEL_NAMES.get(r.last_kernel(), "?"),
+                                       kernel_ms, interval_ms, int(kt.size),
+                                       "launch_interval_ms (busy span / launches; launches overlap on "
+                                       f"{args.streams} streams)" if args.streams > 1 else "kernel_ms"),
         }
-        if r.last_kernel() == 1 and achieved > HBM_PEAK_GBS:
-            out_line["roofline"]["note"] = ("frac > 1: the scene is staged in LDS per workgroup, so the algorithmic "
-                                            "node/triangle bytes are served from LDS; HBM sees `traffic` (about one "
-                                            "frame write per launch).  The launch is bound by VALU issue and LDS "
-                                            "latency: see roofline_valu")
-        if prof is not None and prof[2]:
+        if traced is not None:
+            add_traced(out_line["config"], traced, dt / args.steps)
+        if prof is not None and prof[1].get("sq_per_launch", {}).get("SQ_INSTS_VALU"):
             # the box frame is bound by vector-instruction issue, not HBM (its
             # scene lives in LDS): VALU wave-instructions per launch from the
             # committed PMC profile over the measured kernel time
-            gi = prof[2] / (roof_ms * 1e-3) / 1e9
+            valu = prof[1]["sq_per_launch"]["SQ_INSTS_VALU"]
+            gi = valu / (roof_ms * 1e-3) / 1e9
             out_line["roofline_valu"] = {"bound": "valu_issue", "achieved": round(gi, 2), "peak": VALU_PEAK_GINST,
                                          "unit": "G wave-instr/s", "frac": round(gi / VALU_PEAK_GINST, 4),
-                                         "valu_wave_instr_per_launch": int(prof[2]), "source": prof[0]}
+                                         "valu_wave_instr_per_launch": int(valu), "source": prof[0]}
         if emu > 1:
             out_line["metric"] = f"EMULATED (1 GPU, not a multi-GPU result): rank {emu_rank} of {emu}, " + out_line["metric"]
             out_line["emulated_ranks"] = emu
@@ -555,8 +732,14 @@ def main():
             out_line["primary_cull_off"] = no_cull
         if verified is not None:
             out_line["verified_bitwise_vs_single_gpu"] = verified
-        if world == 1 and emu == 1 and not args.no_cpu_baseline:
+        if world == 1 and emu == 1 and not args.no_cpu_baseline and not args.profile_run:
             out_line["cpu_baseline"] = cpu_baseline(v, i, n, cam, light, W, H, SPP, DEPTH, SSS)
+        if world == 1 and emu == 1 and default_cfg and not (args.no_scene_legs or args.profile_run or args.packed):
+            del r
+            out_line["configs"] = {}
+            for key, scene_name, steps in (("config3", "sphere", 3), ("config5", "synthetic:10000000", 1)):
+                print(f"bench: {key} leg ({scene_name})", file=sys.stderr, flush=True)
+                out_line["configs"][key] = scene_leg(scene_name, W, H, SPP, DEPTH, SSS, steps, device)
         print(json.dumps(out_line), flush=True)
     if dist is not None:
         dist.barrier()

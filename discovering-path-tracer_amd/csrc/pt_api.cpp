@@ -312,6 +312,7 @@ struct pt_context {
   int opt_sm_batch = 1;       // PT_OPT_SM_BATCH
   int opt_cull = 1;           // PT_OPT_PRIMARY_CULL
   int opt_wf_paths = 0;       // PT_OPT_WF_PATHS (0 = 2^24)
+  int opt_count = 0;          // PT_OPT_COUNT_TRACED
   int last_kernel = 0;        // kernel of the last render (1 recursive, 2 state machine, 3 wavefront)
   // compact-launch item lists (live items, then culled ones), rebuilt when
   // the frame, partition, sample lanes or cull rectangles change
@@ -744,6 +745,8 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   const bool wf = c->opt_kernel == 3 || (c->opt_kernel == 0 && !lds && !c->stats_mode && wf_auto);
   if (wf && c->stats_mode) return fail(PT_ERR_UNSUPPORTED, "stats mode runs the path-recursive kernel only");
   if (sm) p.spl = 1;
+  const bool cnt = c->opt_count != 0 && !c->stats_mode;
+  if (cnt && sm) return fail(PT_ERR_UNSUPPORTED, "PT_OPT_COUNT_TRACED: not with the state-machine kernel");
   p.n_cull = -1;
   p.items = nullptr;
   p.culled_items = nullptr;
@@ -812,9 +815,9 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     if (rc) return rc;
     ptd::WfBuffers b = c->wf;
     b.cap = chunk_paths;   // paths per chunk (the allocation may be larger)
-    PT_HIP(ptd::launch_wavefront(p, b, lds, c->stream));
+    PT_HIP(ptd::launch_wavefront(p, b, lds, c->stream, cnt));
   } else {
-    PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream));
+    PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream, cnt));
   }
   if (shared) {
     const int rm = mark_shared(c);
@@ -857,8 +860,8 @@ int pt_create(int device_ordinal, pt_context** out) {
   pt_context* c = new pt_context();
   c->device = device_ordinal;
   hipError_t e = hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, 4 * sizeof(unsigned long long));
-  if (e == hipSuccess) e = hipMemset(c->d_stats, 0, 4 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMalloc((void**)&c->d_stats, ptd::kStatsWords * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemset(c->d_stats, 0, ptd::kStatsWords * sizeof(unsigned long long));
   for (int i = 0; i < pt_context::kRing && e == hipSuccess; ++i) {
     e = hipEventCreate(&c->ring[i][0]);
     if (e == hipSuccess) e = hipEventCreate(&c->ring[i][1]);
@@ -1237,6 +1240,10 @@ int pt_set_option(pt_context* c, int key, int value) {
       if (value < 0 || value > 3) return fail(PT_ERR_INVALID, "PT_OPT_KERNEL takes 0, 1, 2 or 3");
       c->opt_kernel = value;
       return PT_OK;
+    case PT_OPT_COUNT_TRACED:
+      if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_COUNT_TRACED takes 0 or 1");
+      c->opt_count = value;
+      return PT_OK;
     case PT_OPT_PRIMARY_CULL:
       if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_PRIMARY_CULL takes 0 or 1");
       c->opt_cull = value;
@@ -1379,10 +1386,24 @@ int pt_get_stats(pt_context* c, pt_stats* out) {
   return PT_OK;
 }
 
+int pt_get_traced(pt_context* c, pt_traced* out) {
+  if (!c || !out) return fail(PT_ERR_INVALID, "null argument");
+  unsigned long long h[ptd::kStatsWords];
+  PT_HIP(hipSetDevice(c->device));
+  PT_HIP(hipMemcpyAsync(h, c->d_stats, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  PT_HIP(hipStreamSynchronize(c->stream));
+  out->closest_walks = h[4];
+  out->shadow_walks = h[5];
+  out->nodes = h[6];
+  out->tri_tests = h[7];
+  out->primaries = h[8];
+  return PT_OK;
+}
+
 int pt_reset_stats(pt_context* c) {
   if (!c) return fail(PT_ERR_INVALID, "null context");
   PT_HIP(hipSetDevice(c->device));
-  PT_HIP(hipMemsetAsync(c->d_stats, 0, 4 * sizeof(unsigned long long), c->stream));
+  PT_HIP(hipMemsetAsync(c->d_stats, 0, ptd::kStatsWords * sizeof(unsigned long long), c->stream));
   return note_use(c);
 }
 

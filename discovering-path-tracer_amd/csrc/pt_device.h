@@ -79,7 +79,9 @@ struct RenderParams {
   const float4* tris;
   const LightDev* lights;
   float4* accum;
-  unsigned long long* stats;   // rays, nodes, leaf tests, samples (stats mode only)
+  // [0..3] rays, nodes, leaf tests, samples (stats mode); [4..8] closest walks,
+  // shadow walks, nodes visited, triangle tests, primaries (counting mode)
+  unsigned long long* stats;
   int n_nodes;
   int n_tris;
   int n_lights;
@@ -125,6 +127,7 @@ struct RenderParams {
   int item_order;   // host only: PT_OPT_ITEM_ORDER for the item lists
 };
 constexpr int kMaxCullRects = 8;
+constexpr int kStatsWords = 9;   // RenderParams::stats
 
 hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices, int n_tris, float4* d_tris,
                              hipStream_t stream);
@@ -146,7 +149,9 @@ constexpr size_t kMaxSceneLds = 48 * 1024;
 inline size_t scene_lds_bytes(const RenderParams& p) {
   return ((size_t)2 * p.n_nodes + (size_t)3 * p.n_tris) * 16;
 }
-hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool state_machine, hipStream_t stream);
+// cnt: the fast kernel with traced-work counters (PT_OPT_COUNT_TRACED)
+hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool state_machine, hipStream_t stream,
+                         bool cnt = false);
 // Wavefront pipeline (PT_OPT_KERNEL 3): one path per (pixel, sample) held in
 // HBM; generate, then alternate a persistent traversal kernel over the list of
 // paths waiting for a ray and a shading kernel that consumes the hits and
@@ -169,7 +174,8 @@ constexpr size_t kWfBytesPerPath = (size_t)kWfStateF4 * 16 + 16 + 2 * (4 + 32) +
 inline int wf_max_rays(const RenderParams& p) {
   return 1 + p.max_depth * (p.n_lights + p.sss_bounces * (1 + p.n_lights) + 1);
 }
-hipError_t launch_wavefront(const RenderParams& p, const WfBuffers& b, bool lds_scene, hipStream_t stream);
+hipError_t launch_wavefront(const RenderParams& p, const WfBuffers& b, bool lds_scene, hipStream_t stream,
+                            bool cnt = false);
 hipError_t launch_math(int fn, const float* x, float* y, size_t n, hipStream_t stream);
 hipError_t launch_exhaustive(int fn, unsigned long long* bad, uint32_t* first_bad, hipStream_t stream);
 

@@ -34,8 +34,13 @@ using namespace ptm;
 
 namespace {
 
+// Per-lane counters.  STATS (reference-exhaustive mode): rays = every
+// reference traceRay, nodes/leaves = its exhaustive visits.  CNT (the fast
+// kernels with counters, PT_OPT_COUNT_TRACED): rays = closest-hit walks and
+// srays = shadow walks actually started, nodes = nodes actually visited,
+// leaves = triangle tests actually run, prim = primary rays generated.
 struct Ctr {
-  uint32_t rays, nodes, leaves;
+  uint32_t rays, nodes, leaves, srays, prim;
 };
 
 // This rank's li-th tile (pt_device.h Part; slot positions in device memory:
@@ -122,12 +127,12 @@ __device__ __forceinline__ void test_candidates(const RenderParams& P, v3 o, v3 
 // full, by an outer loop around the node loop, instead of by a branch inside
 // it.  Device-memory walks (path_trace_fused) gain 7 % (sphere 5K tris);
 // LDS walks lose 1.6 % (box), so they keep the inner branch.
-template <bool STATS, bool PF, bool FLUSH_OUT = false>
+template <bool STATS, bool PF, bool FLUSH_OUT = false, bool CNT = false>
 __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* cand) {
   const v3 inv = mk(rcp_(d.x), rcp_(d.y), rcp_(d.z));
   float best = 1e30f;
   int bt = -1;
-  if (STATS) c.rays++;
+  if (STATS || CNT) c.rays++;
   int k = 0, nc = 0;
   const int n = P.n_nodes;
   float4 a = P.nodes[0], b = P.nodes[1];
@@ -139,7 +144,7 @@ __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* can
       na = P.nodes[2 * k + 2];
       nb = P.nodes[2 * k + 3];
     }
-    if (STATS) c.nodes++;
+    if (STATS || CNT) c.nodes++;
     const int raw = __float_as_int(a.w);
     // bit 31: bounds identical to the parent's, which this ray hit -> hit
     const bool h = slab(o, inv, a, b) || (raw < 0);   // branch-free: one LDS round trip per node
@@ -147,7 +152,7 @@ __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* can
     // slot nc is free: write it unconditionally, keep it only for a hit leaf
     cand[nc * 64] = tri;
     const bool leaf_hit = h && tri >= 0;
-    if (STATS) c.leaves += leaf_hit ? 1u : 0u;
+    if (STATS || CNT) c.leaves += leaf_hit ? 1u : 0u;
     nc += leaf_hit ? 1 : 0;
     if (!FLUSH_OUT && nc == kCand) {
       test_candidates(P, o, d, cand, nc, &best, &bt);
@@ -180,11 +185,12 @@ __device__ Hit trace_closest(const RenderParams& P, v3 o, v3 d, Ctr& c, int* can
 // Triangles are tested as soon as their leaf is reached (no candidate queue):
 // the early exit is worth more than the compaction for shadow rays (queueing
 // 2/4/8 candidates measured 1-15 % slower on box.obj).
-template <bool STATS, bool PF>
+template <bool STATS, bool PF, bool CNT = false>
 __device__ bool occluded(const RenderParams& P, v3 o, v3 d, float limit, Ctr& c) {
   const v3 inv = mk(rcp_(d.x), rcp_(d.y), rcp_(d.z));
   bool occ = false;
   if (STATS) c.rays++;
+  if (CNT) c.srays++;
   int k = 0;
   const int n = P.n_nodes;
   float4 a = P.nodes[0], b = P.nodes[1];
@@ -194,13 +200,13 @@ __device__ bool occluded(const RenderParams& P, v3 o, v3 d, float limit, Ctr& c)
       na = P.nodes[2 * k + 2];
       nb = P.nodes[2 * k + 3];
     }
-    if (STATS) c.nodes++;
+    if (STATS || CNT) c.nodes++;
     const int raw = __float_as_int(a.w);
     // bit 31: bounds identical to the parent's, which this ray hit -> hit
     const bool h = slab(o, inv, a, b) || (raw < 0);   // branch-free: one LDS round trip per node
     const int tri = __float_as_int(b.w);
     if (h && tri >= 0) {
-      if (STATS) c.leaves++;
+      if (STATS || CNT) c.leaves++;
       const float4* T = P.tris + 3 * tri;
       float t;
       if (tri_test(o, d, T[0], T[1], T[2], &t) && t < 1e30f && !(t >= limit)) {
@@ -228,12 +234,17 @@ __device__ bool occluded(const RenderParams& P, v3 o, v3 d, float limit, Ctr& c)
 // independent node round trips in flight per lane -- the walks are bound by
 // that latency (LDS or L2), not by issue.  has_s / has_c switch a walker off
 // (it starts finished).  Fast kernels only: stats mode walks one ray at a time.
+template <bool CNT = false>
 __device__ __forceinline__ void walk_pair(const RenderParams& P, bool has_s, v3 so, v3 sd, float limit, bool* occ,
-                                          bool has_c, v3 co, v3 cd, int* cand, Hit* hit) {
+                                          bool has_c, v3 co, v3 cd, int* cand, Hit* hit, Ctr& c) {
   const int n = P.n_nodes;
   const v3 sinv = mk(rcp_(sd.x), rcp_(sd.y), rcp_(sd.z));
   const v3 cinv = mk(rcp_(cd.x), rcp_(cd.y), rcp_(cd.z));
   int ks = has_s ? 0 : n, kc = has_c ? 0 : n;
+  if (CNT) {
+    c.srays += has_s ? 1u : 0u;
+    c.rays += has_c ? 1u : 0u;
+  }
   bool oc = false;
   float best = 1e30f;
   int bt = -1, nc = 0;
@@ -247,7 +258,9 @@ __device__ __forceinline__ void walk_pair(const RenderParams& P, bool has_s, v3 
       const bool h = slab(so, sinv, sa, sb) || (raw < 0);
       const int tri = __float_as_int(sb.w);
       int next = (h && tri < 0) ? ks + 1 : (raw & 0x7fffffff);
+      if (CNT) c.nodes++;
       if (h && tri >= 0) {
+        if (CNT) c.leaves++;
         const float4* T = P.tris + 3 * tri;
         float t;
         if (tri_test(so, sd, T[0], T[1], T[2], &t) && t < 1e30f && !(t >= limit)) {
@@ -263,6 +276,10 @@ __device__ __forceinline__ void walk_pair(const RenderParams& P, bool has_s, v3 
       const int tri = __float_as_int(cb.w);
       cand[nc * 64] = tri;
       nc += (h && tri >= 0) ? 1 : 0;
+      if (CNT) {
+        c.nodes++;
+        c.leaves += (h && tri >= 0) ? 1u : 0u;
+      }
       if (nc == kCand) {
         test_candidates(P, co, cd, cand, nc, &best, &bt);
         nc = 0;
@@ -367,6 +384,8 @@ __device__ __forceinline__ void add_ctr(Ctr& a, const Ctr& b) {
   a.rays += b.rays;
   a.nodes += b.nodes;
   a.leaves += b.leaves;
+  a.srays += b.srays;
+  a.prim += b.prim;
 }
 
 // LDS-staged scenes park path state in LDS during walks (PT_PARK) and run 6
@@ -415,7 +434,7 @@ __device__ __forceinline__ v3 unpark3(const float* pk, int i) {
   } while (0)
 
 // pathTrace (:300-418)
-template <bool STATS, bool PF>
+template <bool STATS, bool PF, bool CNT = false>
 __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr& c, int* cand) {
   constexpr bool PARK = PT_PARK && !STATS && !PF;
   float* pk = (float*)(cand + kCand * 64);
@@ -429,13 +448,14 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
   h0.t = 1e30f;
   h0.tri = -1;
   bool have_h0 = false;
-  Ctr c0 = {0u, 0u, 0u};
+  Ctr c0 = {0u, 0u, 0u, 0u, 0u};
+  Ctr& cp0 = CNT ? c : c0;   // CNT: the one walk is counted once
   for (int i = 0; i < P.n_lights; ++i) {                // :311-328
     const LightDev L = load_light(P, i);
     float tl;
     if (intersect_area_light(ro, rd, L, &tl)) {
       if (!have_h0) {
-        h0 = trace_closest<STATS, PF>(P, ro, rd, c0, cand);
+        h0 = trace_closest<STATS, PF, false, CNT>(P, ro, rd, cp0, cand);
         have_h0 = true;
       }
       if (STATS) add_ctr(c, c0);
@@ -447,13 +467,13 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
     Hit h;
     if (depth == 0) {
       if (!have_h0) {
-        h0 = trace_closest<STATS, PF>(P, ro, rd, c0, cand);
+        h0 = trace_closest<STATS, PF, false, CNT>(P, ro, rd, cp0, cand);
         have_h0 = true;
       }
       if (STATS) add_ctr(c, c0);
       h = h0;
     } else {
-      PT_WALK2(PARK, h = (trace_closest<STATS, PF>(P, ro, rd, c, cand)));
+      PT_WALK2(PARK, h = (trace_closest<STATS, PF, false, CNT>(P, ro, rd, c, cand)));
     }
     if (h.tri < 0) {
       rad = add(rad, mul(thr, mk(0.0f, 0.0f, 0.0f)));  // background (:336)
@@ -471,7 +491,7 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
       const float diff = fmax_(dot(hn, ld), 0.0f);
       const float dist = length(sub(lp, hp));
       bool vis = !STATS && !shadow_needed(L, diff);
-      if (!vis) PT_WALK4(PARK, vis = !(occluded<STATS, PF>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c)));
+      if (!vis) PT_WALK4(PARK, vis = !(occluded<STATS, PF, CNT>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c)));
       if (vis) {
         const float d2 = dist * dist;
         const v3 contrib = muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), rcp_(fmax_(d2, 0.01f)));
@@ -487,7 +507,7 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
     v3 sd = sample_sphere(&rng);
     for (int k = 0; k < P.sss_bounces; ++k) {
       Hit sh;
-      PT_WALK4(PARK, sh = (trace_closest<STATS, PF>(P, so, sd, c, cand)));
+      PT_WALK4(PARK, sh = (trace_closest<STATS, PF, false, CNT>(P, so, sd, c, cand)));
       if (sh.tri < 0) break;
       const float travel = sh.t;
       const v3 cp = add(so, muls(sd, travel));
@@ -500,7 +520,7 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
         const float ediff = fmax_(dot(sn, ed), 0.0f);
         const float edist = length(sub(lp, cp));
         bool vis = !STATS && !shadow_needed(L, ediff);
-        if (!vis) PT_WALK4(PARK, vis = !(occluded<STATS, PF>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c)));
+        if (!vis) PT_WALK4(PARK, vis = !(occluded<STATS, PF, CNT>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c)));
         if (vis) {
           const float d2 = edist * edist;
           sl = add(sl, muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])),
@@ -528,12 +548,11 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
 // SSS step's last shadow ray with the next SSS ray.  The RNG draws, the float
 // operations and their order are path_trace's: a shadow result is only used
 // after the pair returns, to finish the same sums in the same order.
-template <bool PF>
-__device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, int* cand) {
+template <bool PF, bool CNT = false>
+__device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, int* cand, Ctr& c) {
   constexpr bool PARK = PT_PARK_FUSED != 0;
   float* pk = (float*)(cand + kCand * 64);
   const float OFFSET = 0.001f;
-  Ctr c = {0u, 0u, 0u};
   v3 thr = mk(1.0f, 1.0f, 1.0f);
   v3 rad = mk(0.0f, 0.0f, 0.0f);
   v3 hp, hn;
@@ -549,7 +568,7 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
     float tl;
     if (intersect_area_light(ro, rd, L, &tl)) {
       if (!have_h0) {
-        h0 = trace_closest<false, PF, true>(P, ro, rd, c, cand);
+        h0 = trace_closest<false, PF, true, CNT>(P, ro, rd, c, cand);
         have_h0 = true;
       }
       if (h0.tri < 0 || h0.t > tl) return mk(L.inten[0], L.inten[1], L.inten[2]);
@@ -563,12 +582,12 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
     Hit h;
     if (depth == 0) {
       if (!have_h0) {
-        h0 = trace_closest<false, PF, true>(P, ro, rd, c, cand);
+        h0 = trace_closest<false, PF, true, CNT>(P, ro, rd, c, cand);
         have_h0 = true;
       }
       h = h0;
     } else {
-      PT_WALK2(PARK, h = (trace_closest<false, PF, true>(P, ro, rd, c, cand)));
+      PT_WALK2(PARK, h = (trace_closest<false, PF, true, CNT>(P, ro, rd, c, cand)));
     }
     if (h.tri < 0) {
       rad = add(rad, mul(thr, mk(0.0f, 0.0f, 0.0f)));  // background (:336)
@@ -591,7 +610,7 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
       const float d2 = dist * dist;
       const v3 contrib = mul(albedo, muls(muls(mk(L.inten[0], L.inten[1], L.inten[2]), diff), rcp_(fmax_(d2, 0.01f))));
       if (i + 1 < NL) {
-        if (!shadow_needed(L, diff) || !occluded<false, PF>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c))
+        if (!shadow_needed(L, diff) || !occluded<false, PF, CNT>(P, add(hp, muls(hn, OFFSET)), ld, dist - OFFSET, c))
           direct = add(direct, contrib);
       } else {
         s_need = shadow_needed(L, diff);
@@ -606,7 +625,7 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
     v3 sd = sample_sphere(&rng);
     Hit sh;
     bool occ = false;
-    PT_WALK4(PARK, walk_pair(P, NL > 0 && s_need, s_o, s_d, s_lim, &occ, P.sss_bounces > 0, so, sd, cand, &sh));
+    PT_WALK4(PARK, walk_pair<CNT>(P, NL > 0 && s_need, s_o, s_d, s_lim, &occ, P.sss_bounces > 0, so, sd, cand, &sh, c));
     if (NL > 0 && !occ) direct = add(direct, s_c);
     rad = add(rad, mul(thr, direct));
 
@@ -626,7 +645,7 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
         const v3 term = muls(mul(muls(sss_albedo, ediff), mk(L.inten[0], L.inten[1], L.inten[2])),
                              rcp_(fmax_(d2, 0.01f)));
         if (i + 1 < NL) {
-          if (!shadow_needed(L, ediff) || !occluded<false, PF>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c))
+          if (!shadow_needed(L, ediff) || !occluded<false, PF, CNT>(P, add(cp, muls(sn, OFFSET)), ed, edist - OFFSET, c))
             sl = add(sl, term);
         } else {
           s_need = shadow_needed(L, ediff);
@@ -640,7 +659,7 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
       sss_thr = mul(sss_thr, muls(sss_albedo, exp_(-travel / (sss_radius * 1.5f))));
       so = sub(cp, muls(sn, OFFSET));
       sd = sample_sphere(&rng);
-      PT_WALK4(PARK, walk_pair(P, NL > 0 && s_need, s_o, s_d, s_lim, &occ, k + 1 < P.sss_bounces, so, sd, cand, &sh));
+      PT_WALK4(PARK, walk_pair<CNT>(P, NL > 0 && s_need, s_o, s_d, s_lim, &occ, k + 1 < P.sss_bounces, so, sd, cand, &sh, c));
       if (NL > 0 && !occ) sl = add(sl, s_c);
       rad = add(rad, muls(mul(thr_k, sl), 1.0f + sss_radius * 0.5f));
     }
@@ -657,6 +676,20 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
+}
+
+// CNT kernels: add the wave's traced-work counters to P.stats[4..8]
+// (closest walks, shadow walks, nodes visited, triangle tests, primaries).
+__device__ __forceinline__ void flush_traced(const RenderParams& P, const Ctr& c, int lane) {
+  const unsigned long long v0 = wave_sum(c.rays), v1 = wave_sum(c.srays), v2 = wave_sum(c.nodes),
+                           v3_ = wave_sum(c.leaves), v4 = wave_sum(c.prim);
+  if (lane == 0) {
+    atomicAdd(&P.stats[4], v0);
+    atomicAdd(&P.stats[5], v1);
+    atomicAdd(&P.stats[6], v2);
+    atomicAdd(&P.stats[7], v3_);
+    atomicAdd(&P.stats[8], v4);
+  }
 }
 
 // Running mean of n_batches constant colours (0,0,0,1) over this lane's
@@ -766,7 +799,7 @@ __device__ __forceinline__ void unpack_block(const RenderParams& P, int block) {
 // LDS=true stages the whole scene (threaded nodes + triangle records) in LDS
 // once per workgroup; chosen by the host for scenes of at most a few tens of
 // KB (box.obj is 1.3 KB), where every lane re-reads the same few nodes.
-template <bool STATS, bool LDS>
+template <bool STATS, bool LDS, bool CNT = false>
 #ifndef PT_RENDER_MIN_BLOCKS
 #define PT_RENDER_MIN_BLOCKS 5
 #endif
@@ -811,7 +844,7 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
   const int px = bx * 16 + q % 16;
   const int py = by * 16 + part * (16 / spl) + q / 16;
   const bool active = tile < P.blocks_total && px < P.width && py < P.height;   // :425-428
-  Ctr c = {0u, 0u, 0u};
+  Ctr c = {0u, 0u, 0u, 0u, 0u};
   const int W = P.width, H = P.height;
   // Per-pixel constants of main() (:430-432, :446-447, :457), hoisted out of
   // the sample loop — same values every sample.
@@ -914,10 +947,11 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
       // sphere 20K tris -9 %); on an LDS-staged scene the round trip is short
       // and the pair's registers cost more than it hides (box +11 %).
       v3 col;
+      if (CNT) c.prim++;
       if (STATS || LDS)
-        col = path_trace<STATS, !LDS>(P, origin, dir, seed, c, cand);
+        col = path_trace<STATS, !LDS, CNT>(P, origin, dir, seed, c, cand);
       else
-        col = path_trace_fused<PT_REC_PF != 0>(P, origin, dir, seed, cand);
+        col = path_trace_fused<PT_REC_PF != 0, CNT>(P, origin, dir, seed, cand, c);
       col4 = make_float4(col.x, col.y, col.z, 1.0f);                      // vec4(color, 1.0)
      }
      // hand the chunk's colours to the folding lanes of the same pixel
@@ -956,6 +990,7 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
       atomicAdd(&P.stats[3], smp);
     }
   }
+  if (CNT) flush_traced(P, c, lane);
 }
 
 __global__ __launch_bounds__(256) void setup_tris_kernel(const float* __restrict__ V, const uint32_t* __restrict__ I,
@@ -1487,7 +1522,7 @@ __global__ __launch_bounds__(256, PT_SM_MIN_BLOCKS) void render_sm_kernel(Render
     const float4 a = P.accum[pix];
     acc[0] = a.x; acc[1] = a.y; acc[2] = a.z; acc[3] = a.w;
   }
-  Ctr c = {0u, 0u, 0u};
+  Ctr c = {0u, 0u, 0u, 0u, 0u};
   PathSt S;
   S.s = 0;
   S.phase = PH_BEGIN;
@@ -1607,9 +1642,10 @@ __device__ __forceinline__ bool pixel_live(const RenderParams& P, float ndcX0, f
 }
 
 // Ray generation + shading up to the primary trace (path_step from PH_BEGIN).
+template <bool CNT>
 __global__ __launch_bounds__(256) void wf_gen_kernel(RenderParams P, WfBuffers B, long long n) {
   const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
-  bool need = false;
+  bool need = false, gen = false;
   Trav T;
   if (g < n) {
     const long long pp = g / (long long)P.n_batches;
@@ -1627,10 +1663,11 @@ __global__ __launch_bounds__(256) void wf_gen_kernel(RenderParams P, WfBuffers B
       F.tanFov = P.tan_fov;
       v3 col = mk(0.0f, 0.0f, 0.0f);
       if (pixel_live(P, F.ndcX0, F.ndcY0)) {
+        gen = true;
         PathSt S;
         S.s = (uint32_t)(g - pp * (long long)P.n_batches);
         S.phase = PH_BEGIN;
-        Ctr c = {0u, 0u, 0u};
+        Ctr c = {0u, 0u, 0u, 0u, 0u};
         need = path_step<false>(P, F, S, T, c, &col);
         if (need) wf_store_state(B.state + (size_t)g * kWfStateF4, S);
       }
@@ -1639,6 +1676,10 @@ __global__ __launch_bounds__(256) void wf_gen_kernel(RenderParams P, WfBuffers B
   }
   const int slot = wave_slot(&B.counters[0], need);
   if (need) wf_push(B, 0, slot, (int)g, T);
+  if (CNT) {
+    const unsigned long long m = __ballot(gen);
+    if (__lane_id() == 0 && m) atomicAdd(&P.stats[8], (unsigned long long)__popcll(m));
+  }
 }
 
 // Traversal state of one lane of the persistent traversal kernel: the ray,
@@ -1650,6 +1691,14 @@ struct WfLane {
   int k, nc, res, shadow;
   float lim;
 };
+
+// CNT: a ray handed to the traversal kernel -- closest (kind 0) or shadow
+// (kind 1) walk; a null shadow query (kind 2, trav_null) is no walk.
+__device__ __forceinline__ void count_start(const float4* __restrict__ ray, Ctr& c) {
+  const int kind = __float_as_int(ray[1].w);
+  c.rays += kind == 0 ? 1u : 0u;
+  c.srays += kind == 1 ? 1u : 0u;
+}
 
 __device__ __forceinline__ void wf_lane_start(const RenderParams& P, const float4* __restrict__ ray, float4 root_a,
                                               float4 root_b, WfLane& L) {
@@ -1669,12 +1718,13 @@ __device__ __forceinline__ void wf_lane_start(const RenderParams& P, const float
 
 // One node of trace_closest / occluded (same visit order and tests); true
 // when the ray is finished (L.lim / L.res hold the result).
-template <bool PF>
-__device__ __forceinline__ bool wf_lane_step(const RenderParams& P, WfLane& L, int* cand) {
+template <bool PF, bool CNT = false>
+__device__ __forceinline__ bool wf_lane_step(const RenderParams& P, WfLane& L, int* cand, Ctr& c) {
   if (L.k >= P.n_nodes) {
     if (!L.shadow) test_candidates(P, L.o, L.d, cand, L.nc, &L.lim, &L.res);
     return true;
   }
+  if (CNT) c.nodes++;
   float4 na, nb;
   if (PF) {
     na = P.nodes[2 * L.k + 2];
@@ -1684,6 +1734,7 @@ __device__ __forceinline__ bool wf_lane_step(const RenderParams& P, WfLane& L, i
   const bool h = slab(L.o, L.inv, L.a, L.b) || (raw < 0);
   const int tri = __float_as_int(L.b.w);
   const bool leaf_hit = h && tri >= 0;
+  if (CNT) c.leaves += leaf_hit ? 1u : 0u;
   if (L.shadow) {
     if (leaf_hit) {
       const float4* T = P.tris + 3 * tri;
@@ -1737,7 +1788,7 @@ constexpr unsigned long long group_lead() {
 #ifndef PT_WF_MIN_BLOCKS
 #define PT_WF_MIN_BLOCKS 7   // 72 VGPRs (11 spilled): sphere -7 %, 1M cloud -0.6 % vs 6; 8 spills 30 (+50 %)
 #endif
-template <bool LDS, int G>
+template <bool LDS, int G, bool CNT = false>
 __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderParams P, WfBuffers B, int cur) {
   const int tid = (int)threadIdx.x;
   if (blockIdx.x == 0 && tid == 0) B.counters[cur ^ 1] = 0;   // filled by the shading that follows
@@ -1769,6 +1820,7 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
   int p = -1;   // list slot this lane traces
   bool more = true;
   WfLane L;
+  Ctr c = {0u, 0u, 0u, 0u, 0u};
   for (;;) {
     const unsigned long long idle = __ballot(p < 0);
     // groups of G lanes refill together with consecutive list
@@ -1790,17 +1842,19 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
         if (slot < count) {
           p = slot;
           wf_lane_start(P, rays + 2 * (size_t)slot, root_a, root_b, L);
+          if (CNT) count_start(rays + 2 * (size_t)slot, c);
         }
       }
     }
     if (!more && __ballot(p >= 0) == 0ull) break;
     for (int it = 0; it < PT_WF_STEPS; ++it) {
-      if (p >= 0 && wf_lane_step<PT_WF_PF && !LDS>(P, L, cand)) {
+      if (p >= 0 && wf_lane_step<PT_WF_PF && !LDS, CNT>(P, L, cand, c)) {
         B.hits[p] = make_float2(L.lim, __int_as_float(L.res));
         p = -1;
       }
     }
   }
+  if (CNT) flush_traced(P, c, lane);
 }
 
 // Shading of every path in list `cur` (path_step on the returned hit);
@@ -1827,7 +1881,7 @@ __global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers
       T.res = __float_as_int(h.y);
       T.nc = 0;
       T.cn = T.cl = 0u;
-      Ctr c = {0u, 0u, 0u};
+      Ctr c = {0u, 0u, 0u, 0u, 0u};
       v3 col;
       need = path_step<false>(P, F, S, T, c, &col);
       if (need)
@@ -1934,7 +1988,9 @@ hipError_t launch_clear(float4* accum, int width, int height, const Part& part, 
   return hipGetLastError();
 }
 
-hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool state_machine, hipStream_t stream) {
+hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool state_machine, hipStream_t stream,
+                         bool cnt) {
+  if (cnt && (stats || state_machine)) return hipErrorInvalidValue;
   if (p.spl != 1 && p.spl != 2 && p.spl != 4 && p.spl != 8) return hipErrorInvalidValue;
   // owned tiles (part_tile); the recursive kernel splits each into spl workgroups
   const long long tiles = p.n_tiles;
@@ -1955,6 +2011,8 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool
   if (state_machine)
     kern = lds_scene ? (stats ? render_sm_kernel<true, true> : render_sm_kernel<false, true>)
                      : (stats ? render_sm_kernel<true, false> : render_sm_kernel<false, false>);
+  else if (cnt)
+    kern = lds_scene ? render_kernel<false, true, true> : render_kernel<false, false, true>;
   else
     kern = lds_scene ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
                      : (stats ? render_kernel<true, false> : render_kernel<false, false>);
@@ -1962,7 +2020,7 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool
   return hipGetLastError();
 }
 
-hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds_scene, hipStream_t stream) {
+hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds_scene, hipStream_t stream, bool cnt) {
   if (p0.spl != 1 && p0.spl != 2 && p0.spl != 4 && p0.spl != 8) return hipErrorInvalidValue;
   if (p0.n_batches == 0) return hipSuccess;
   const int per = 256 / p0.spl;
@@ -1982,8 +2040,10 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   const bool g2 = p0.n_tris < kWfGroup4Tris;
   void (*trace)(RenderParams, WfBuffers, int) =
-      lds_scene ? (g2 ? wf_trace_kernel<true, 2> : wf_trace_kernel<true, 4>)
-                : (g2 ? wf_trace_kernel<false, 2> : wf_trace_kernel<false, 4>);
+      cnt ? (lds_scene ? (g2 ? wf_trace_kernel<true, 2, true> : wf_trace_kernel<true, 4, true>)
+                       : (g2 ? wf_trace_kernel<false, 2, true> : wf_trace_kernel<false, 4, true>))
+          : (lds_scene ? (g2 ? wf_trace_kernel<true, 2> : wf_trace_kernel<true, 4>)
+                       : (g2 ? wf_trace_kernel<false, 2> : wf_trace_kernel<false, 4>));
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, trace, 256, lds);
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, wf_shade_kernel, 256, 0);
   if (e != hipSuccess) return e;
@@ -1998,7 +2058,10 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
     const long long n = px * p.n_batches;
     e = hipMemsetAsync(b.counters, 0, 3 * sizeof(int), stream);
     if (e != hipSuccess) return e;
-    wf_gen_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(p, b, n);
+    if (cnt)
+      wf_gen_kernel<true><<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(p, b, n);
+    else
+      wf_gen_kernel<false><<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(p, b, n);
     int cur = 0;
     for (int it = 0; it < iters; ++it) {
       hipLaunchKernelGGL(trace, dim3(grid_t), dim3(256), lds, stream, p, b, cur);

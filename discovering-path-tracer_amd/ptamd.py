@@ -26,6 +26,7 @@ PT_OPT_PRIMARY_CULL = 6
 PT_OPT_WF_PATHS = 7
 PT_OPT_ITEM_ORDER = 8
 PT_OPT_LAUNCH_TIMING = 9
+PT_OPT_COUNT_TRACED = 10
 KERNEL_AUTO, KERNEL_RECURSIVE, KERNEL_STATE_MACHINE, KERNEL_WAVEFRONT = 0, 1, 2, 3
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).
@@ -40,7 +41,7 @@ EXPORTS = [
     "pt_default_camera", "pt_primary_cull_rects", "pt_scene_save", "pt_scene_load_cache",
     "pt_progressive_camera", "pt_progressive_advance", "pt_readback_begin", "pt_readback_end", "pt_write_image",
     "pt_items_live", "pt_items_pack", "pt_items_unpack_all", "pt_render_packed", "pt_launch_span_ms",
-    "pt_set_partition_slots",
+    "pt_set_partition_slots", "pt_get_traced",
 ]
 
 
@@ -55,6 +56,11 @@ class Params(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [("rays", ctypes.c_uint64), ("nodes", ctypes.c_uint64), ("leaf_tests", ctypes.c_uint64),
                 ("samples", ctypes.c_uint64)]
+
+
+class Traced(ctypes.Structure):
+    _fields_ = [("closest_walks", ctypes.c_uint64), ("shadow_walks", ctypes.c_uint64), ("nodes", ctypes.c_uint64),
+                ("tri_tests", ctypes.c_uint64), ("primaries", ctypes.c_uint64)]
 
 
 _lib = None
@@ -84,7 +90,7 @@ def lib():
             "pt_set_stats_mode": ([vp, i32], i32), "pt_set_option": ([vp, i32, i32], i32), "pt_last_kernel": ([vp, ctypes.POINTER(ctypes.c_int)], i32),
             "pt_tiles_owned": ([vp, ctypes.POINTER(i32)], i32), "pt_tiles_pack": ([vp, vp], i32),
             "pt_tiles_unpack": ([vp, vp, i32, vp], i32), "pt_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
-            "pt_reset_stats": ([vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
+            "pt_reset_stats": ([vp], i32), "pt_get_traced": ([vp, ctypes.POINTER(Traced)], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
             "pt_launch_times_ms": ([vp, vp, sz, psz], i32), "pt_reset_launch_times": ([vp], i32),
             "pt_launch_span_ms": ([vp, ctypes.POINTER(ctypes.c_float), psz], i32),
             "pt_selftest_math": ([i32, i32, vp, vp, sz], i32),
@@ -429,6 +435,13 @@ class Renderer:
         s = Stats()
         _check(lib().pt_get_stats(self._c, ctypes.byref(s)), "pt_get_stats")
         return {"rays": s.rays, "nodes": s.nodes, "leaf_tests": s.leaf_tests, "samples": s.samples}
+
+    def traced(self):
+        """Work the fast kernels actually did while PT_OPT_COUNT_TRACED was on
+        (pt_get_traced), since the last reset_stats."""
+        t = Traced()
+        _check(lib().pt_get_traced(self._c, ctypes.byref(t)), "pt_get_traced")
+        return {k: int(getattr(t, k)) for k, _ in Traced._fields_}
 
     def last_launch_ms(self):
         ms = ctypes.c_float()

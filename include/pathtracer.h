@@ -74,6 +74,20 @@ typedef struct pt_stats {
   uint64_t samples;
 } pt_stats;
 
+/* Work the fast kernels actually did while PT_OPT_COUNT_TRACED is on (they
+ * skip work the reference does without changing a bit of the output: culled
+ * primary rays, shadow rays whose answer cannot change the image, the
+ * repeated light pre-pass ray, implied-hit nodes, leaf tests after an
+ * occluder): closest-hit and shadow walks started, BVH nodes visited,
+ * triangle tests, primary rays generated.  Reset by pt_reset_stats. */
+typedef struct pt_traced {
+  uint64_t closest_walks;
+  uint64_t shadow_walks;
+  uint64_t nodes;
+  uint64_t tri_tests;
+  uint64_t primaries;
+} pt_traced;
+
 typedef struct pt_context pt_context;
 
 /* upload flags */
@@ -242,6 +256,9 @@ int pt_render_packed(pt_context* ctx, uint32_t n_batches, void* dst_device, cons
  * launch (default 1; 0 = none) for pt_last_launch_ms / pt_launch_times_ms /
  * pt_launch_span_ms.  Output-invariant. */
 #define PT_OPT_LAUNCH_TIMING 9
+/* PT_OPT_COUNT_TRACED: 1 = run the fast kernels with counters of the work
+ * they actually do (pt_get_traced); slower, output identical.  Default 0. */
+#define PT_OPT_COUNT_TRACED 10
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */
@@ -266,6 +283,7 @@ int pt_primary_cull_rects(const float camera_ubo[16], int width, int height, con
 int pt_set_stats_mode(pt_context* ctx, int enabled);
 int pt_get_stats(pt_context* ctx, pt_stats* out);
 int pt_reset_stats(pt_context* ctx);
+int pt_get_traced(pt_context* ctx, pt_traced* out);
 /* Device time of the last pt_render/pt_dispatch launch, from HIP events
  * recorded on the launch stream. */
 int pt_last_launch_ms(pt_context* ctx, float* ms);

@@ -735,3 +735,52 @@ def test_reslotting_one_renderer_keeps_item_lists_right():
         rs[0].items_unpack_all(recv.data_ptr(), slot, frame.data_ptr())
         rs[0].synchronize()
         _assert_same(frame.cpu().numpy().reshape(-1), want, f"sparse exchange after re-slotting to {slots}")
+
+
+@pytest.mark.parametrize("scene", ["box", "sphere"])
+def test_count_traced_mode(scene):
+    """PT_OPT_COUNT_TRACED: the output is bit-identical, and the three fast
+    kernels (path-recursive with the scene in LDS, path-recursive walking
+    device memory with paired walks, wavefront pipeline) report the same
+    walks, node visits, triangle tests and primaries -- they do the same
+    work in different orders.  The counts sit below the reference's
+    exhaustive ones (stats mode) and the primaries equal the live samples."""
+    if scene == "box":
+        v, i, n = _box()
+        cam = scenes.DEFAULT_CAMERA
+    else:
+        sv, si = scenes.displaced_sphere(3)
+        v, i, n, _, _ = ptamd.Scene.from_arrays(sv, si).build_bvh().arrays()
+        cam = scenes.camera((0.0, 0.5, 3.0))
+    W, H, nb = 160, 96, 4
+    ref, ost = _oracle(v, i, n, W, H, nb=nb, cam=cam)
+    counts = {}
+    for name, lds, kernel in (("lds", 2, 1), ("dev", 0, 1), ("wf", 0, 3)):
+        if scene == "sphere" and lds == 2:
+            continue   # 5K triangles do not fit the LDS variant
+        r = _setup(v, i, n, cam=cam, lds=lds)
+        r.set_option(ptamd.PT_OPT_KERNEL, kernel)
+        r.set_option(ptamd.PT_OPT_COUNT_TRACED, 1)
+        r.resize_and_clear(W, H)
+        r.reset_stats()
+        r.render(0, nb)
+        _assert_same(r.read_accum(), ref, f"{scene} {name} counting")
+        assert r.last_kernel() == kernel
+        counts[name] = r.traced()
+    first = next(iter(counts.values()))
+    for name, c in counts.items():
+        assert c == first, (name, c, first)
+    walks = first["closest_walks"] + first["shadow_walks"]
+    assert 0 < walks < int(ost[0])
+    assert 0 < first["nodes"] < int(ost[1])
+    assert first["tri_tests"] <= int(ost[2])
+    assert 0 < first["primaries"] <= W * H * nb
+    # culling off: every sample generates its primary ray
+    r = _setup(v, i, n, cam=cam, lds=0)
+    r.set_option(ptamd.PT_OPT_PRIMARY_CULL, 0)
+    r.set_option(ptamd.PT_OPT_COUNT_TRACED, 1)
+    r.resize_and_clear(W, H)
+    r.reset_stats()
+    r.render(0, nb)
+    assert r.traced()["primaries"] == W * H * nb
+    _assert_same(r.read_accum(), ref, f"{scene} counting, culling off")

@@ -1,0 +1,31 @@
+#!/bin/bash
+# rocprofv3 evidence for one bench workload, per MI355X_MICROARCH.md §HBM:
+# a kernel-trace/stats pass, then FETCH_SIZE and WRITE_SIZE in passes of their
+# own (they cannot share one on gfx950), plus VALU/SALU instruction counts,
+# then tools/summarize_profile.py -> profiles/<TAG>/<WORKLOAD>_summary.json,
+# which bench.py prices its roofline from (matched by kernel SHA and workload).
+#   TAG=r02b WORKLOAD=box|sphere_1080p8|synthetic10M_1080p8 tools/profile_workload.sh
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${TAG:-x}
+WORKLOAD=${WORKLOAD:-box}
+case $WORKLOAD in
+  box) ARGS="--steps 20 --warmup 2"; STEPS=20; WARM=2 ;;
+  sphere_1080p8) ARGS="--scene sphere --steps 2 --warmup 1"; STEPS=2; WARM=1 ;;
+  synthetic10M_1080p8) ARGS="--scene synthetic:10000000 --steps 1 --warmup 1"; STEPS=1; WARM=1 ;;
+  *) echo "unknown WORKLOAD $WORKLOAD"; exit 2 ;;
+esac
+OUT=gpurun_out/prof_${TAG}_${WORKLOAD}
+mkdir -p $OUT
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
+  python3 bench.py $ARGS --profile-run > $OUT/bench_trace.log 2>&1 \
+  || { echo "trace rc=$?"; tail -20 $OUT/bench_trace.log; exit 1; }
+grep '^{' $OUT/bench_trace.log | tail -1 | cut -c1-300
+for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES"; do
+  n=${c%% *}
+  timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$n -o run -- \
+    python3 bench.py $ARGS --profile-run > $OUT/bench_$n.log 2>&1 \
+    || { echo "pmc $c rc=$?"; tail -20 $OUT/bench_$n.log; exit 1; }
+done
+python3 tools/summarize_profile.py "$TAG" "$WORKLOAD" $((STEPS + WARM))

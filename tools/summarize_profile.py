@@ -1,66 +1,88 @@
 #!/usr/bin/env python3
-"""Condense a tools/gpu_profile.sh run (gpurun_out/prof_<tag>/) into
-profiles/<tag>_summary.json + copies of the rocprofv3 stats CSV.
+"""Condense a tools/profile_workload.sh run (gpurun_out/prof_<tag>_<workload>/)
+into profiles/<tag>/<workload>_summary.json + the rocprofv3 stats CSV.
 
 HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
-WRITE_SIZE are in KiB, collected in separate passes; on gfx950 FETCH_SIZE
-reports half the bytes of a wide coalesced read, so it is doubled."""
+WRITE_SIZE are KiB, from separate passes; FETCH_SIZE is doubled (the guide's
+gfx950 correction for 16-B/lane streaming reads).  The raw readings are kept
+next to it, and, when profiles/<tag>/fetch_calibration.json exists (from
+tools/fetch_calib.hip), the calibrated ratios for 32-B and 48-B random
+gathers too.
+
+box: the dominant kernel is one render_kernel launch per frame (averaged over
+its dispatches).  sphere/synthetic: a frame is the wavefront pipeline
+(wf_gen, wf_trace x rays, wf_shade x rays, wf_fold, fill_culled): per-frame
+bytes = the sum over every dispatch of those kernels / frames."""
 import csv
+import hashlib
 import json
 import os
 import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BOX_KERNEL = "render_kernel<false, true, false>"
+WF_KERNELS = ("wf_gen_kernel", "wf_trace_kernel", "wf_shade_kernel", "wf_fold_kernel", "fill_culled_kernel")
 
 
-def main(tag, kernel_substr="render_kernel<false, "):
-    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
-    dst = os.path.join(ROOT, "profiles")
+def main(tag, workload, frames):
+    frames = int(frames)
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}_{workload}")
+    dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
     stats_csv = os.path.join(src, "trace", "run_kernel_stats.csv")
-    shutil.copy(stats_csv, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    shutil.copy(stats_csv, os.path.join(dst, f"{workload}_kernel_stats.csv"))
     kern = {}
     for row in csv.DictReader(open(stats_csv)):
         kern[row["Name"]] = {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
-                             "min_ns": float(row["MinNs"]), "max_ns": float(row["MaxNs"]),
-                             "percent": float(row["Percentage"])}
-    pmc = {}
-    for c in ("FETCH_SIZE", "WRITE_SIZE"):
-        path = os.path.join(src, f"pmc_{c}", "run_counter_collection.csv")
+                             "total_ns": float(row["TotalDurationNs"]), "percent": float(row["Percentage"])}
+    box = workload == "box"
+    match = (lambda k: BOX_KERNEL in k) if box else (lambda k: any(w in k for w in WF_KERNELS))
+
+    def per_launch(path, names):
         if not os.path.exists(path):
-            continue
-        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-                if kernel_substr in r["Kernel_Name"] and r["Counter_Name"] == c]
-        if vals:
-            pmc[c] = sum(vals) / len(vals)
-    sq = {}
-    path = os.path.join(src, "pmc_SQ_INSTS_VALU", "run_counter_collection.csv")
-    if os.path.exists(path):
-        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"):
-            vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-                    if kernel_substr in r["Kernel_Name"] and r["Counter_Name"] == c]
-            if vals:
-                sq[c] = sum(vals) / len(vals)
-    import hashlib
+            return {}
+        vals = {}
+        for r in csv.DictReader(open(path)):
+            if match(r["Kernel_Name"]) and r["Counter_Name"] in names:
+                vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
+        return {c: (sum(v) / len(v) if box else sum(v) / frames) for c, v in vals.items()}
+
+    pmc = {}
+    pmc.update(per_launch(os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv"), ("FETCH_SIZE",)))
+    pmc.update(per_launch(os.path.join(src, "pmc_WRITE_SIZE", "run_counter_collection.csv"), ("WRITE_SIZE",)))
+    sq = per_launch(os.path.join(src, "pmc_SQ_INSTS_VALU", "run_counter_collection.csv"),
+                    ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"))
     src_hash = hashlib.sha1(open(os.path.join(ROOT, "discovering-path-tracer_amd", "csrc", "pt_device.hip"),
                                  "rb").read()).hexdigest()
-    out = {"tag": tag, "kernels": kern, "kernel": kernel_substr, "pt_device_hip_sha1": src_hash}
+    if box:
+        ns = [v["avg_ns"] for k, v in kern.items() if BOX_KERNEL in k]
+        kernel_ms = ns[0] / 1e6 if ns else None
+    else:
+        kernel_ms = sum(v["total_ns"] for k, v in kern.items() if match(k)) / frames / 1e6
+    out = {"tag": tag, "workload": workload, "unit": "per launch" if box else f"per frame ({frames} frames)",
+           "kernel": BOX_KERNEL if box else "+".join(WF_KERNELS), "pt_device_hip_sha1": src_hash,
+           "kernel_ms_per_launch": kernel_ms, "kernels": kern}
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
-        fetch = pmc["FETCH_SIZE"] * 1024 * 2      # gfx950: FETCH_SIZE counts half of wide reads
+        fetch = pmc["FETCH_SIZE"] * 1024 * 2
         write = pmc["WRITE_SIZE"] * 1024
         out["hbm_bytes_per_launch"] = {"fetch_corrected": fetch, "write": write, "total": fetch + write,
                                        "raw_fetch_kib": pmc["FETCH_SIZE"], "raw_write_kib": pmc["WRITE_SIZE"]}
+        if kernel_ms:
+            out["hbm_GBps"] = {"x2_corrected": (fetch + write) / kernel_ms / 1e6,
+                               "raw": (pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024 / kernel_ms / 1e6}
+    cal = os.path.join(dst, "fetch_calibration.json")
+    if os.path.exists(cal):
+        out["fetch_calibration"] = json.load(open(cal))
     if sq:
         out["sq_per_launch"] = sq
-    for log in ("bench_trace.log",):
-        p = os.path.join(src, log)
-        if os.path.exists(p):
-            lines = [l for l in open(p) if l.startswith("{")]
-            if lines:
-                out["bench_line"] = json.loads(lines[-1])
-    json.dump(out, open(os.path.join(dst, f"{tag}_summary.json"), "w"), indent=1)
-    print(json.dumps(out, indent=1)[:3000])
+    p = os.path.join(src, "bench_trace.log")
+    if os.path.exists(p):
+        lines = [l for l in open(p) if l.startswith("{")]
+        if lines:
+            out["bench_line"] = json.loads(lines[-1])
+    json.dump(out, open(os.path.join(dst, f"{workload}_summary.json"), "w"), indent=1)
+    print(json.dumps({k: v for k, v in out.items() if k not in ("kernels", "bench_line")}, indent=1))
 
 
 if __name__ == "__main__":
