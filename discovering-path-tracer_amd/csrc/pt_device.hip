@@ -99,6 +99,12 @@ __device__ __forceinline__ bool tri_test(v3 o, v3 d, float4 A, float4 B, float4 
 #ifndef PT_KCAND
 #define PT_KCAND 8
 #endif
+#ifndef PT_WF_WAVEFLUSH
+#define PT_WF_WAVEFLUSH 1   // wf_trace_kernel: wave-wide candidate flush (see there)
+#endif
+#ifndef PT_WF_SHADOW_QUEUE
+#define PT_WF_SHADOW_QUEUE 1   // wf_trace_kernel: shadow rays queue their leaves too (see there)
+#endif
 constexpr int kCand = PT_KCAND;
 
 // PF (prefetch): load node k+1 while node k is being tested — it is the next
@@ -121,6 +127,19 @@ __device__ __forceinline__ void test_candidates(const RenderParams& P, v3 o, v3 
       *bt = tri;
     }
   }
+}
+
+// Shadow-ray candidates (PT_WF_SHADOW_QUEUE): the queued triangles in visit
+// order until the first one occluded() would stop at; true if any.
+__device__ __forceinline__ bool test_shadow_candidates(const RenderParams& P, v3 o, v3 d, float limit,
+                                                       const int* cand, int nc) {
+  for (int i = 0; i < nc; ++i) {
+    const int tri = cand[i * 64];
+    const float4* T = P.tris + 3 * tri;
+    float t;
+    if (tri_test(o, d, T[0], T[1], T[2], &t) && t < 1e30f && !(t >= limit)) return true;
+  }
+  return false;
 }
 
 // FLUSH_OUT: the candidate queue is tested when the walk ends or the queue is
@@ -1721,7 +1740,10 @@ __device__ __forceinline__ void wf_lane_start(const RenderParams& P, const float
 template <bool PF, bool CNT = false>
 __device__ __forceinline__ bool wf_lane_step(const RenderParams& P, WfLane& L, int* cand, Ctr& c) {
   if (L.k >= P.n_nodes) {
-    if (!L.shadow) test_candidates(P, L.o, L.d, cand, L.nc, &L.lim, &L.res);
+    if (!L.shadow)
+      test_candidates(P, L.o, L.d, cand, L.nc, &L.lim, &L.res);
+    else if (PT_WF_SHADOW_QUEUE && L.nc > 0)
+      L.res = test_shadow_candidates(P, L.o, L.d, L.lim, cand, L.nc) ? 1 : L.res;
     return true;
   }
   if (CNT) c.nodes++;
@@ -1735,7 +1757,7 @@ __device__ __forceinline__ bool wf_lane_step(const RenderParams& P, WfLane& L, i
   const int tri = __float_as_int(L.b.w);
   const bool leaf_hit = h && tri >= 0;
   if (CNT) c.leaves += leaf_hit ? 1u : 0u;
-  if (L.shadow) {
+  if (L.shadow && !PT_WF_SHADOW_QUEUE) {
     if (leaf_hit) {
       const float4* T = P.tris + 3 * tri;
       float t;
@@ -1747,7 +1769,7 @@ __device__ __forceinline__ bool wf_lane_step(const RenderParams& P, WfLane& L, i
   } else {
     cand[L.nc * 64] = tri;
     L.nc += leaf_hit ? 1 : 0;
-    if (L.nc == kCand) {
+    if (!PT_WF_WAVEFLUSH && !L.shadow && L.nc == kCand) {
       test_candidates(P, L.o, L.d, cand, L.nc, &L.lim, &L.res);
       L.nc = 0;
     }
@@ -1766,11 +1788,27 @@ __device__ __forceinline__ bool wf_lane_step(const RenderParams& P, WfLane& L, i
 
 // Persistent traversal over list `cur`: lanes pull list slots (one atomic per
 // wave) and refill once at least PT_WF_REFILL lanes are idle.
+//
+// PT_WF_WAVEFLUSH: closest-hit candidates are tested wave-wide -- as soon as
+// one lane's queue is full, every lane with queued candidates tests them in
+// the same loop -- instead of by each full lane alone while the other lanes
+// of the wave wait (round-1 counters on the sphere: ~10 of 64 lanes active
+// per VALU instruction in wf_trace_kernel).  Same candidates, same visit
+// order, same strict '<': the same hit.  1080p8 displaced sphere 378 -> 289
+// ms, 1M cloud +0.5 %.
+// PT_WF_SHADOW_QUEUE: shadow rays queue their hit leaves as well instead of
+// testing each at once in a branch the other lanes wait on; the wave-wide
+// flush tests them in visit order and ends the walk at the first occluder.
+// The answer ("some accepted triangle has !(t >= limit)") is the same; the
+// walk may visit a few nodes past that occluder before the flush finds it.
+// Sphere 288 -> 242 ms, 1M cloud 636 -> 602.  (With it, the counting mode's
+// triangle tests and nodes of shadow walks are the queued ones.)
 #ifndef PT_WF_STEPS
 #define PT_WF_STEPS 8
 #endif
+
 #ifndef PT_WF_REFILL
-#define PT_WF_REFILL 16
+#define PT_WF_REFILL 32   // 1080p8: sphere -3.3 %, 1M cloud -2.0 % vs 16 (with the shadow queue); 48: +1.3 % / -0.3 %
 #endif
 // Refill group: lanes refill in groups of G with consecutive list slots.  G
 // is chosen per launch (launch_wavefront): 2 for scenes under kWfGroup4Tris
@@ -1851,6 +1889,17 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
       if (p >= 0 && wf_lane_step<PT_WF_PF && !LDS, CNT>(P, L, cand, c)) {
         B.hits[p] = make_float2(L.lim, __int_as_float(L.res));
         p = -1;
+      }
+      if (PT_WF_WAVEFLUSH && __ballot(p >= 0 && L.nc == kCand)) {   // wave-uniform
+        if (p >= 0 && L.nc > 0) {
+          if (!L.shadow) {
+            test_candidates(P, L.o, L.d, cand, L.nc, &L.lim, &L.res);
+          } else if (test_shadow_candidates(P, L.o, L.d, L.lim, cand, L.nc)) {
+            L.res = 1;
+            L.k = P.n_nodes;   // occluded: the walk ends (its next step reports it)
+          }
+          L.nc = 0;
+        }
       }
     }
   }

@@ -741,9 +741,9 @@ def test_reslotting_one_renderer_keeps_item_lists_right():
 def test_count_traced_mode(scene):
     """PT_OPT_COUNT_TRACED: the output is bit-identical, and the three fast
     kernels (path-recursive with the scene in LDS, path-recursive walking
-    device memory with paired walks, wavefront pipeline) report the same
-    walks, node visits, triangle tests and primaries -- they do the same
-    work in different orders.  The counts sit below the reference's
+    device memory with paired walks, wavefront pipeline) start the same walks
+    and generate the same primaries; the two path-recursive ones also visit
+    the same nodes and run the same triangle tests.  The counts sit below the reference's
     exhaustive ones (stats mode) and the primaries equal the live samples."""
     if scene == "box":
         v, i, n = _box()
@@ -769,7 +769,15 @@ def test_count_traced_mode(scene):
         counts[name] = r.traced()
     first = next(iter(counts.values()))
     for name, c in counts.items():
-        assert c == first, (name, c, first)
+        # every kernel starts the same walks and generates the same primaries
+        for k in ("closest_walks", "shadow_walks", "primaries"):
+            assert c[k] == first[k], (name, k, c, first)
+    if "lds" in counts:   # the two path-recursive kernels do the same node visits and tests
+        assert counts["lds"] == counts["dev"]
+    # the wavefront kernel queues shadow leaves (PT_WF_SHADOW_QUEUE): a shadow
+    # walk may run a few nodes past its occluder before the queue is tested
+    assert counts["wf"]["nodes"] >= counts["dev"]["nodes"]
+    assert counts["wf"]["tri_tests"] >= counts["dev"]["tri_tests"]
     walks = first["closest_walks"] + first["shadow_walks"]
     assert 0 < walks < int(ost[0])
     assert 0 < first["nodes"] < int(ost[1])

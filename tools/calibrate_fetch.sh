@@ -1,4 +1,5 @@
 #!/bin/bash
+# (writes gpurun_out/calib_<TAG>/fetch_calibration.json; copy it to profiles/<TAG>/)
 # FETCH_SIZE calibration for the large-scene access patterns (tools/fetch_calib.hip,
 # built in the container: hipcc --offload-arch=gfx950 -O3 -o tools/fetch_calib tools/fetch_calib.hip).
 set -u
@@ -26,7 +27,6 @@ for f in glob.glob(out + "/pmc/**/*counter_collection.csv", recursive=True):
                           "ms": d["ms"], "GBps": d["bytes"] / d["ms"] / 1e6}
 for k, v in res.items():
     v["fetch_over_algorithmic"] = v["fetch_size_bytes"] / v["algorithmic_bytes"]
-os.makedirs(f"profiles/{tag}", exist_ok=True)
-json.dump(res, open(f"profiles/{tag}/fetch_calibration.json", "w"), indent=1)
+json.dump(res, open(os.path.join(out, "fetch_calibration.json"), "w"), indent=1)
 print(json.dumps(res, indent=1))
 PY

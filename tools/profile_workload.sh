@@ -28,4 +28,6 @@ for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES"; do
     python3 bench.py $ARGS --profile-run > $OUT/bench_$n.log 2>&1 \
     || { echo "pmc $c rc=$?"; tail -20 $OUT/bench_$n.log; exit 1; }
 done
-python3 tools/summarize_profile.py "$TAG" "$WORKLOAD" $((STEPS + WARM))
+echo "frames=$((STEPS + WARM))" > $OUT/frames.txt
+# summarize in the container (profiles/ written on the box does not come back):
+#   python3 tools/summarize_profile.py $TAG $WORKLOAD $((STEPS + WARM))
