@@ -505,6 +505,7 @@ def main():
     r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
     pending = []
     finish = None
+    ingest = None   # the emulated root's stand-in for the gather's receive traffic
     nparts = max(world, emu)
     if dist is None and emu == 1 and not args.packed:
         def step():
@@ -552,6 +553,17 @@ def main():
         out = outs[0] if root else None
         streams = [stream] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
         state = {"k": 0}
+        # Emulated root (PT_BENCH_EMULATE_RANKS): the other ranks' slots
+        # still have to arrive.  A high-priority side stream copies N-1 whole
+        # slots into the receive buffer after each render, in one copy as an
+        # RCCL gather is one call (device to device: a read and a write of
+        # them in this GPU's HBM, at least the write an RCCL receive costs),
+        # and the frame's assembly waits for it.
+        ingest = None
+        if dist is None and emu > 1 and root:
+            ingest = {"stream": torch.cuda.Stream(dev, priority=-1),
+                      "src": torch.zeros((nparts - 1) * slot, dtype=torch.float32, device=dev),
+                      "bytes": 4 * (nparts - 1) * slot}
 
         def finish(work, buf):   # separate assembly launch of one gathered frame
             if work is not None:
@@ -585,7 +597,13 @@ def main():
                 r.render_packed(SPP, dst.data_ptr(), *fused)
             else:
                 r.render_packed(SPP, dst.data_ptr())
-            if dist is None:
+            if dist is None and ingest is not None:
+                side = ingest["stream"]
+                side.wait_stream(streams[sid])
+                with torch.cuda.stream(side):
+                    recv_all[buf][1:].view(-1).copy_(ingest["src"])
+                work = _StreamWork(side)
+            elif dist is None:
                 work = _StreamWork(streams[sid])
             elif backend == "nccl":
                 work = dist.gather(send[buf], recv[buf] if root else None, dst=0, async_op=True)
@@ -666,7 +684,8 @@ def main():
         ref.resize_and_clear(W, H)
         ref.render(0, SPP)
         want = ref.read_accum()
-        frames = outs if args.collective == "gather" else [frame]
+        # --assemble 2 assembles frames into outs[stream]; 0 and 1 into outs[0]
+        frames = (outs if args.assemble == 2 else [out]) if args.collective == "gather" else [frame]
         for f in frames:
             got = f.cpu().numpy().reshape(-1)
             verified = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
@@ -727,6 +746,8 @@ def main():
         if emu > 1:
             out_line["metric"] = f"EMULATED (1 GPU, not a multi-GPU result): rank {emu_rank} of {emu}, " + out_line["metric"]
             out_line["emulated_ranks"] = emu
+            if ingest is not None:
+                out_line["emulated_ingest_bytes_per_step"] = int(ingest["bytes"])
             out_line["config"]["parallelism"] = f"emulated-tiles{emu}-sparse-gather"
         if no_cull is not None:
             out_line["primary_cull_off"] = no_cull

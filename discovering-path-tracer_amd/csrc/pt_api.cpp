@@ -455,10 +455,10 @@ static int pixels_in(int g0, int n, int res, float lo, float hi) {
 // Rank r's share of the slotted partition (pt_device.h Part): the period's
 // slots ordered by (k + 1/2) / slots[rank] for each rank's k-th slot (ties by
 // rank), so every rank's slots are spread evenly over the period.
-static ptd::Part part_of(const pt_context* c, int r) {
+static ptd::Part part_of_slots(const std::vector<int>& slots, int r) {
   std::vector<std::pair<double, int>> seq;
-  for (int i = 0; i < (int)c->slots.size(); ++i)
-    for (int k = 0; k < c->slots[i]; ++k) seq.push_back({(k + 0.5) / c->slots[i], i});
+  for (int i = 0; i < (int)slots.size(); ++i)
+    for (int k = 0; k < slots[i]; ++k) seq.push_back({(k + 0.5) / slots[i], i});
   std::stable_sort(seq.begin(), seq.end());
   ptd::Part pt{};
   pt.m = (int)seq.size();
@@ -466,6 +466,7 @@ static ptd::Part part_of(const pt_context* c, int r) {
     if (seq[v].second == r) pt.pos[pt.cnt++] = v;
   return pt;
 }
+static ptd::Part part_of(const pt_context* c, int r) { return part_of_slots(c->slots, r); }
 
 // Upload every rank's slot positions when the partition changed; the device
 // copy of rank r's starts at d_parts + r * kMaxSlots.
@@ -1810,6 +1811,60 @@ int pt_primary_cull_rects(const float cam[16], int w, int h, const float root_mi
     return fail(PT_ERR_INVALID, "null argument");
   if (max_rects < 1) return fail(PT_ERR_INVALID, "max_rects must be >= 1");
   *n_rects = cull_rects(cam, w, h, root_min, root_max, lights, n_lights, rects, max_rects);
+  return PT_OK;
+}
+
+int pt_partition_items(int w, int h, int spl, int nranks, int rank, const int* slots, const float* cull_rects,
+                       int n_cull, int item_order, int* live, size_t* n_live, int* culled, size_t* n_culled,
+                       int* pixel_of) {
+  if (!n_live || !n_culled) return fail(PT_ERR_INVALID, "null argument");
+  if (w <= 0 || h <= 0) return fail(PT_ERR_INVALID, "bad resolution");
+  if (spl != 1 && spl != 2 && spl != 4 && spl != 8) return fail(PT_ERR_INVALID, "sample lanes must be 1, 2, 4 or 8");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(PT_ERR_INVALID, "bad partition");
+  if (n_cull > ptd::kMaxCullRects || (n_cull > 0 && !cull_rects)) return fail(PT_ERR_INVALID, "bad cull rectangles");
+  std::vector<int> sl((size_t)nranks, 1);
+  if (slots) {
+    long long m = 0;
+    for (int r = 0; r < nranks; ++r) {
+      if (slots[r] < 1 || slots[r] > ptd::kMaxSlots) return fail(PT_ERR_INVALID, "partition slots must be 1..64");
+      sl[r] = slots[r];
+      m += slots[r];
+    }
+    if (m > 4096) return fail(PT_ERR_INVALID, "more than 4096 partition slots");
+  }
+  ptd::RenderParams p{};
+  p.width = w;
+  p.height = h;
+  p.spl = spl;
+  p.blocks_x = (w + 15) / 16;
+  p.blocks_total = p.blocks_x * ((h + 15) / 16);
+  p.n_cull = n_cull < 0 ? -1 : n_cull;
+  for (int r = 0; r < n_cull; ++r)
+    for (int k = 0; k < 4; ++k) p.cull[r][k] = cull_rects[4 * r + k];
+  p.item_order = item_order;
+  const ptd::Part pt = part_of_slots(sl, rank);
+  std::vector<int> lv, cu;
+  item_lists(p, pt, &lv, &cu);
+  if ((live && *n_live < lv.size()) || (culled && *n_culled < cu.size()))
+    return fail(PT_ERR_INVALID, "item buffers too small");
+  if (live) std::copy(lv.begin(), lv.end(), live);
+  if (culled) std::copy(cu.begin(), cu.end(), culled);
+  if (pixel_of) {   // the kernels' item -> pixel map (tile_pixel), live items first
+    const int per = 256 / spl;
+    size_t o = 0;
+    for (const std::vector<int>* v : {&lv, &cu})
+      for (int item : *v) {
+        const int tile = ptd::part_tile(pt, item / spl), part = item % spl;
+        int bx, by;
+        ptd::tile_block(tile, p.blocks_x, &bx, &by);
+        for (int q = 0; q < per; ++q, ++o) {
+          const int px = bx * 16 + q % 16, py = by * 16 + part * (16 / spl) + q / 16;
+          pixel_of[o] = (tile < p.blocks_total && px < w && py < h) ? py * w + px : -1;
+        }
+      }
+  }
+  *n_live = lv.size();
+  *n_culled = cu.size();
   return PT_OK;
 }
 

@@ -41,7 +41,7 @@ EXPORTS = [
     "pt_default_camera", "pt_primary_cull_rects", "pt_scene_save", "pt_scene_load_cache",
     "pt_progressive_camera", "pt_progressive_advance", "pt_readback_begin", "pt_readback_end", "pt_write_image",
     "pt_items_live", "pt_items_pack", "pt_items_unpack_all", "pt_render_packed", "pt_launch_span_ms",
-    "pt_set_partition_slots", "pt_get_traced",
+    "pt_set_partition_slots", "pt_get_traced", "pt_partition_items",
 ]
 
 
@@ -90,7 +90,8 @@ def lib():
             "pt_set_stats_mode": ([vp, i32], i32), "pt_set_option": ([vp, i32, i32], i32), "pt_last_kernel": ([vp, ctypes.POINTER(ctypes.c_int)], i32),
             "pt_tiles_owned": ([vp, ctypes.POINTER(i32)], i32), "pt_tiles_pack": ([vp, vp], i32),
             "pt_tiles_unpack": ([vp, vp, i32, vp], i32), "pt_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
-            "pt_reset_stats": ([vp], i32), "pt_get_traced": ([vp, ctypes.POINTER(Traced)], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
+            "pt_reset_stats": ([vp], i32), "pt_get_traced": ([vp, ctypes.POINTER(Traced)], i32),
+            "pt_partition_items": ([i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, psz, vp, psz, vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
             "pt_launch_times_ms": ([vp, vp, sz, psz], i32), "pt_reset_launch_times": ([vp], i32),
             "pt_launch_span_ms": ([vp, ctypes.POINTER(ctypes.c_float), psz], i32),
             "pt_selftest_math": ([i32, i32, vp, vp, sz], i32),
@@ -257,6 +258,30 @@ def partition_owned(width, height, nranks, rank, slots=None):
     ys, xs = np.mgrid[0:height, 0:width]
     by, bx = ys // 16, xs // 16
     return np.isin((by * nbx + (bx - by) % nbx) % m, pos)
+
+
+def partition_items(width, height, sample_lanes, nranks, rank, slots=None, cull_rects=None, item_order=1):
+    """pt_partition_items: the product's item tables for `rank` (host only).
+    Returns (live, culled, pixel_of) -- live and culled item ids in launch /
+    table order, and pixel_of[(len(live) + len(culled)), 256 // sample_lanes]
+    with the pixel index y*W+x of each item slot (-1 past the frame edge)."""
+    sl = None if slots is None else np.ascontiguousarray(slots, np.int32)
+    if cull_rects is None:
+        cr, nc = None, -1
+    else:
+        cr = np.ascontiguousarray(cull_rects, np.float32).reshape(-1, 4)
+        nc = cr.shape[0]
+    nl, nu = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    args = (width, height, sample_lanes, nranks, rank, None if sl is None else sl.ctypes.data,
+            None if cr is None else cr.ctypes.data, nc, item_order)
+    _check(lib().pt_partition_items(*args, None, ctypes.byref(nl), None, ctypes.byref(nu), None), "pt_partition_items")
+    live = np.zeros(max(nl.value, 1), np.int32)
+    culled = np.zeros(max(nu.value, 1), np.int32)
+    per = 256 // sample_lanes
+    pix = np.zeros(max((nl.value + nu.value) * per, 1), np.int32)
+    _check(lib().pt_partition_items(*args, live.ctypes.data, ctypes.byref(nl), culled.ctypes.data, ctypes.byref(nu),
+                                    pix.ctypes.data), "pt_partition_items")
+    return live[:nl.value], culled[:nu.value], pix[:(nl.value + nu.value) * per].reshape(-1, per)
 
 
 def primary_cull_rects(camera_ubo, width, height, root_min, root_max, lights16, max_rects=8):

@@ -210,6 +210,19 @@ int pt_items_unpack_all(pt_context* ctx, const void* src_device, size_t slot_flo
  * image readback (VulkanRayTracer.cpp:803-865). */
 int pt_render_packed(pt_context* ctx, uint32_t n_batches, void* dst_device, const void* gathered_device,
                      size_t slot_floats, void* frame_device);
+/* The item tables behind pt_items_live / pt_items_pack / pt_items_unpack_all
+ * and pt_render_packed, as a pure host function (no context, no GPU): rank's
+ * live items (tile parts that can hold a live pixel) in launch order, its
+ * culled items, and -- when pixel_of is not null -- for every listed item
+ * (live first, then culled) and each of its 256/sample_lanes slots q the
+ * pixel index y*W+x it carries, or -1 past the frame edge.  slots: null for
+ * one slot per rank, else as pt_set_partition_slots.  cull_rects / n_cull: as
+ * pt_primary_cull_rects returns them (n_cull < 0: no culling, every item is
+ * live).  item_order: PT_OPT_ITEM_ORDER.  Call with null live/culled to get
+ * the counts; *n_live / *n_culled give the buffer sizes on input. */
+int pt_partition_items(int width, int height, int sample_lanes, int nranks, int rank, const int* slots,
+                       const float* cull_rects, int n_cull, int item_order, int* live, size_t* n_live,
+                       int* culled, size_t* n_culled, int* pixel_of);
 
 /* ---- kernel options ---------------------------------------------------- */
 /* PT_OPT_SCENE_IN_LDS: stage the scene in LDS per workgroup — 0 never,

@@ -732,6 +732,57 @@ int oracle_render_ex(const float* verts, const uint32_t* idx, const float* nodes
   return 0;
 }
 
+// The pixels listed in pixels[0..n) (y*W+x; negative entries skipped), each
+// with n_batches sequential batches, threads over runs of 32 list entries.
+int oracle_render_pixels(const float* verts, const uint32_t* idx, const float* nodes, size_t n_nodes,
+                         const float* camera16, const float* lights16, size_t n_lights,
+                         int W, int H, uint32_t first_batch, uint32_t n_batches, int max_depth, int sss_bounces,
+                         const int32_t* pixels, size_t n, float* accum, uint64_t* stats, int nthreads,
+                         uint32_t flags) {
+  if (W <= 0 || H <= 0 || n_nodes == 0) return -1;
+  Scene S;
+  S.V = verts; S.I = idx; S.N = nodes; S.nn = n_nodes;
+  S.int_bits = (flags & ORACLE_INT_BITS) != 0;
+  S.cpos = V(camera16[0], camera16[1], camera16[2]);
+  S.cdir = V(camera16[4], camera16[5], camera16[6]);
+  S.cup = V(camera16[8], camera16[9], camera16[10]);
+  S.fov = camera16[12];
+  for (size_t i = 0; i < n_lights; ++i) {
+    const float* l = lights16 + i * 16;
+    Light L;
+    L.pos = V(l[0], l[1], l[2]);
+    L.nrm = V(l[4], l[5], l[6]);
+    L.inten = V(l[8], l[9], l[10]);
+    L.sx = l[12]; L.sy = l[13];
+    S.lights.push_back(L);
+  }
+  S.W = W; S.H = H; S.max_depth = max_depth; S.sss_bounces = sss_bounces;
+  if (nthreads <= 0) nthreads = (int)std::thread::hardware_concurrency();
+  if (nthreads <= 0) nthreads = 1;
+  std::atomic<size_t> next{0};
+  std::vector<Stats> per(nthreads);
+  auto work = [&](int tid) {
+    for (;;) {
+      const size_t j0 = next.fetch_add(32);
+      if (j0 >= n) break;
+      for (size_t j = j0; j < std::min(n, j0 + 32); ++j) {
+        const int32_t pix = pixels[j];
+        if (pix < 0 || pix >= W * H) continue;
+        float* a = accum + (size_t)pix * 4;
+        for (uint32_t b = 0; b < n_batches; ++b)
+          shade_pixel(S, (uint32_t)(pix % W), (uint32_t)(pix / W), first_batch + b, a, &per[tid]);
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int i = 0; i < nthreads; ++i) th.emplace_back(work, i);
+  for (auto& t : th) t.join();
+  if (stats) {
+    for (auto& s : per) { stats[0] += s.rays; stats[1] += s.nodes; stats[2] += s.leaves; }
+  }
+  return 0;
+}
+
 int oracle_render(const float* verts, const uint32_t* idx, const float* nodes, size_t n_nodes,
                   const float* camera16, const float* lights16, size_t n_lights,
                   int W, int H, uint32_t first_batch, uint32_t n_batches,

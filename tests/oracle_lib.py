@@ -35,6 +35,10 @@ def lib():
                                     ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                     F32P, U64P, ctypes.c_int]
         L.oracle_render_ex.argtypes = L.oracle_render.argtypes + [ctypes.c_uint32]
+        L.oracle_render_pixels.argtypes = [F32P, U32P, F32P, sz, F32P, F32P, sz, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_int,
+                                           np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS"), sz,
+                                           F32P, U64P, ctypes.c_int, ctypes.c_uint32]
         L.oracle_math.argtypes = [ctypes.c_int, F32P, F32P, sz]
         L.oracle_rng.argtypes = [ctypes.c_uint32, F32P, sz]
         L.oracle_trace.argtypes = [F32P, U32P, F32P, sz, F32P, F32P, F32P, U64P]
@@ -88,6 +92,24 @@ def render(verts, idx, nodes, camera16, lights16, W, H, first_batch=0, n_batches
                                 1 if int_bits else 0)
     if rc:
         raise ValueError(f"oracle_render rc={rc}")
+    return accum, stats
+
+
+def render_pixels(verts, idx, nodes, camera16, lights16, W, H, pixels, first_batch=0, n_batches=1, max_depth=4,
+                  sss_bounces=3, accum=None, nthreads=0, int_bits=False):
+    """Like render(), for the listed pixels (y*W+x, negatives skipped) only."""
+    if accum is None:
+        accum = np.zeros(W * H * 4, np.float32)
+    stats = np.zeros(3, np.uint64)
+    lights16 = np.ascontiguousarray(lights16, np.float32).reshape(-1)
+    nodes = np.ascontiguousarray(nodes, np.float32).reshape(-1)
+    pixels = np.ascontiguousarray(pixels, np.int32).reshape(-1)
+    rc = lib().oracle_render_pixels(np.ascontiguousarray(verts, np.float32), np.ascontiguousarray(idx, np.uint32),
+                                    nodes, nodes.size // 8, np.ascontiguousarray(camera16, np.float32), lights16,
+                                    lights16.size // 16, W, H, first_batch, n_batches, max_depth, sss_bounces,
+                                    pixels, pixels.size, accum, stats, nthreads, 1 if int_bits else 0)
+    if rc:
+        raise ValueError(f"oracle_render_pixels rc={rc}")
     return accum, stats
 
 

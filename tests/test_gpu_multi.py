@@ -1,0 +1,45 @@
+"""The product's N > 1 path on the GPU, in fresh processes.
+
+bench.py --gpus 2 under torch.distributed.run: two ranks, each driving
+libptamd on device 0 (a 1-GPU box; RCCL needs one GPU per rank, so the
+collectives run on gloo staged through the host), render their tile shares,
+exchange them -- the sparse live-item gather with pt_render_packed's fused
+assembly, or the -0/+0 SUM reduce -- and rank 0 checks the assembled frames
+bitwise against a single-GPU render (--verify).  The children are started as
+subprocesses, never exec'd over this (GPU-initialised) test process."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("collective,extra", [("gather", []), ("reduce", []), ("gather", ["--assemble", "0"])])
+def test_two_rank_bench_verifies_bitwise(collective, extra):
+    env = dict(os.environ, PT_BENCH_DEVICE="0", PT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2", "--verify",
+           "--collective", collective] + extra
+    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
+    lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
+    assert lines, res.stdout[-2000:]
+    out = json.loads(lines[-1])
+    assert out["n_gpus"] == 2
+    assert out["verified_bitwise_vs_single_gpu"] is True
+    assert out["config"]["rays_traced"] > 0

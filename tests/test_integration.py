@@ -1,0 +1,108 @@
+"""The documented drop-in binding, compiled and run.
+
+INTEGRATION.md §2 (initComputePipeline) and §3 (mainLoop, per batch and the
+progressive loop) are extracted verbatim and compiled inside
+tests/integration/snippet_harness.cpp against include/pathtracer.h, linked
+with libptamd.so (CPU test: the documentation cannot drift from the header
+or the exported symbols).  On the GPU the harness runs on box.obj and its
+accumulation buffer must equal the oracle's bit for bit; so must the PFM of
+the headless C++ driver pt_render (csrc/tools/pt_render.cpp), the C++ caller
+that replaces VulkanRayTracer's loop."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import ptamd
+import scenes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "discovering-path-tracer_amd")
+
+
+def _cpp_blocks(section):
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    start = text.index(f"## {section}.")
+    end = text.find("\n## ", start + 4)
+    return re.findall(r"```cpp\n(.*?)```", text[start:end if end > 0 else None], re.S)
+
+
+def build_harness(out_dir):
+    os.makedirs(out_dir, exist_ok=True)
+    init, = _cpp_blocks(2)
+    loop, progressive = _cpp_blocks(3)[:2]
+    for name, body in (("snippet_init.inc", init), ("snippet_loop.inc", loop),
+                       ("snippet_progressive.inc", progressive)):
+        with open(os.path.join(out_dir, name), "w") as f:
+            f.write(body)
+    exe = os.path.join(out_dir, "snippet_harness")
+    cmd = ["g++", "-std=c++17", "-O1", "-Wall", "-Wno-unused-variable", "-Wno-unused-but-set-variable",
+           "-I", os.path.join(ROOT, "include"), "-I", out_dir,
+           os.path.join(ROOT, "tests", "integration", "snippet_harness.cpp"), "-o", exe,
+           "-L", PKG, "-lptamd", f"-Wl,-rpath,{PKG}", "-L/opt/rocm/lib", "-Wl,-rpath,/opt/rocm/lib",
+           "-Wl,--allow-shlib-undefined"]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    assert res.returncode == 0, res.stderr[-4000:]
+    return exe
+
+
+def test_integration_snippets_compile_and_link(tmp_path):
+    exe = build_harness(str(tmp_path))
+    assert os.path.exists(exe)
+
+
+def test_integration_snippets_name_only_declared_symbols():
+    declared = set(re.findall(r"\b(pt_[a-z_]+)\s*\(", open(os.path.join(ROOT, "include", "pathtracer.h")).read()))
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    used = set(re.findall(r"\b(pt_[a-z_]+)\s*\(", "\n".join(re.findall(r"```cpp\n(.*?)```", text, re.S))))
+    assert used and used <= declared, used - declared
+    assert used <= set(ptamd.EXPORTS)
+
+
+def _oracle_box(W, H, spp):
+    s = ptamd.Scene.load_obj(scenes.BOX_OBJ).build_bvh()
+    v, i, n, _, _ = s.arrays()
+    ref, _ = O.render(v, i, n.reshape(-1), scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, W, H, n_batches=spp)
+    return ref
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["dispatch", "progressive"])
+def test_integration_snippets_render_the_oracle_frame(tmp_path, mode):
+    exe = build_harness(str(tmp_path))
+    W, H, spp = 64, 48, 8
+    out = str(tmp_path / "frame.raw")
+    res = subprocess.run([exe, mode, scenes.BOX_OBJ, str(W), str(H), str(spp), out], capture_output=True, text=True,
+                         timeout=120)
+    assert res.returncode == 0, res.stderr[-3000:]
+    got = np.fromfile(out, np.float32)
+    want = _oracle_box(W, H, spp)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def _read_pfm(path):
+    with open(path, "rb") as f:
+        assert f.readline().strip() == b"PF"
+        w, h = map(int, f.readline().split())
+        scale = float(f.readline())
+        assert scale < 0   # little-endian
+        return np.fromfile(f, "<f4").reshape(h, w, 3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [[], ["-fused"], ["-progressive", "8", "-chunk", "3"]])
+def test_pt_render_cpp_driver_matches_oracle(tmp_path, flags):
+    exe = os.path.join(PKG, "pt_render")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "-s", "-C", PKG, "pt_render"])
+    W, H, spp = 64, 48, 8
+    out = str(tmp_path / "box.pfm")
+    res = subprocess.run([exe, scenes.BOX_OBJ, "-w", str(W), "-h", str(H), "-spp", str(spp), "-o", out] + flags,
+                         capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr[-3000:]
+    got = _read_pfm(out)   # rows bottom-to-top: buffer row 0 first
+    want = _oracle_box(W, H, spp).reshape(H, W, 4)[..., :3]
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))

@@ -1,8 +1,17 @@
-"""Multi-rank path on CPU (gloo, world_size 2 and 4): each rank renders its
-screen tiles (pt_set_partition's block-interleaved ownership) with -0 in the
-pixels it does not own, exactly as the device clear kernel leaves them; a SUM
-reduction over ranks must reproduce the single-rank frame bit for bit.  This
-is the collective bench.py runs over RCCL for N > 1."""
+"""Multi-rank path on CPU (gloo, world_size 2 and 4), built from the
+product's own partition and exchange tables.
+
+Each rank takes its share from libptamd's host code -- pt_partition_items
+(the item lists pt_render_packed launches and pt_items_pack writes, with the
+kernels' item -> pixel map) and pt_primary_cull_rects -- renders exactly those
+pixels with the CPU oracle (the GPU's stand-in here; the GPU runs of the same
+exchange are tests/test_gpu_multi.py), packs its live items into the
+pt_items_pack slot layout, and gloo-gathers the slots to rank 0.  Rank 0
+assembles the frame as pt_items_unpack_all does: every rank's live items
+scattered by its table, culled items written as (0,0,0,1).  The frame must
+be the single-rank frame bit for bit.  A second test covers the reduce
+alternative: each rank's -0/+0 cleared share (partition_owned), SUM-reduced.
+This is the exchange bench.py runs over RCCL for N > 1."""
 import os
 import socket
 
@@ -16,7 +25,8 @@ import oracle_lib as O
 import ptamd
 import scenes
 
-W, H, SPP = 72, 40, 2
+W, H, SPP, SPL = 72, 40, 2, 4
+CAM = scenes.camera((3.0, 2.0, 4.0))   # the box off-centre: live and culled items on every rank
 
 
 def _scene():
@@ -25,21 +35,69 @@ def _scene():
     return v, ri, nodes
 
 
-def _rank_frame(rank, world):
+def _rects(nodes):
+    n = nodes.reshape(-1, 8)
+    return ptamd.primary_cull_rects(CAM, W, H, n[0, 0:3], n[0, 4:7], scenes.REFERENCE_LIGHT)
+
+
+def _pack_share(rank, world, slots, slot_items):
+    """This rank's live items rendered and packed as pt_items_pack lays them out."""
     v, ri, nodes = _scene()
-    owned = ptamd.partition_owned(W, H, world, rank)
-    acc = np.repeat(np.where(owned[..., None], np.float32(0.0), np.float32(-0.0)), 4, axis=2)
-    acc = np.ascontiguousarray(acc, np.float32).reshape(-1)
-    O.render(v, ri, nodes, scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, W, H, n_batches=SPP,
-             tile=16, nranks=world, rank=rank, accum=acc, nthreads=2)
-    return acc
+    live, culled, pix = ptamd.partition_items(W, H, SPL, world, rank, slots, _rects(nodes))
+    lp = pix[:len(live)].reshape(-1)
+    frame, _ = O.render_pixels(v, ri, nodes, CAM, scenes.REFERENCE_LIGHT, W, H, lp, n_batches=SPP, nthreads=2)
+    frame = frame.reshape(-1, 4)
+    send = np.zeros((slot_items * (256 // SPL), 4), np.float32)
+    ok = lp >= 0
+    send[:lp.size][ok] = frame[lp[ok]]   # pixels past the frame edge stay zero, as on the device
+    return send.reshape(-1)
 
 
-def _worker(rank, world, port, q):
+def _assemble(slots_data, world, slots):
+    """pt_items_unpack_all on the host: live items from each rank's slot,
+    culled items (0,0,0,1)."""
+    _, _, nodes = _scene()
+    frame = np.full((W * H, 4), np.nan, np.float32)
+    for r in range(world):
+        live, culled, pix = ptamd.partition_items(W, H, SPL, world, r, slots, _rects(nodes))
+        src = slots_data[r].reshape(-1, 4)
+        lp = pix[:len(live)].reshape(-1)
+        ok = lp >= 0
+        frame[lp[ok]] = src[:lp.size][ok]
+        cp = pix[len(live):].reshape(-1)
+        frame[cp[cp >= 0]] = (0.0, 0.0, 0.0, 1.0)
+    return frame.reshape(-1)
+
+
+def _slot_items(world, slots):
+    _, _, nodes = _scene()
+    return max(len(ptamd.partition_items(W, H, SPL, world, r, slots, _rects(nodes))[0]) for r in range(world))
+
+
+def _gather_worker(rank, world, port, slots, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    t = torch.from_numpy(_rank_frame(rank, world))
+    t = torch.from_numpy(_pack_share(rank, world, slots, _slot_items(world, slots)))
+    got = [torch.empty_like(t) for _ in range(world)] if rank == 0 else None
+    dist.gather(t, got, dst=0)
+    if rank == 0:
+        q.put(_assemble([g.numpy() for g in got], world, slots).tobytes())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _reduce_worker(rank, world, port, slots, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    v, ri, nodes = _scene()
+    owned = ptamd.partition_owned(W, H, world, rank, slots)
+    acc = np.repeat(np.where(owned[..., None], np.float32(0.0), np.float32(-0.0)), 4, axis=2)
+    acc = np.ascontiguousarray(acc, np.float32).reshape(-1)   # pt_clear_accum: +0 owned, -0 elsewhere
+    O.render_pixels(v, ri, nodes, CAM, scenes.REFERENCE_LIGHT, W, H, np.flatnonzero(owned.reshape(-1)),
+                    n_batches=SPP, accum=acc, nthreads=2)
+    t = torch.from_numpy(acc)
     dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
     if rank == 0:
         q.put(t.numpy().tobytes())
@@ -55,20 +113,52 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_tile_split_reduce_is_bit_exact(world):
+def _run(worker, world, slots):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=worker, args=(r, world, port, slots, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = np.frombuffer(q.get(timeout=240), np.float32)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
+    return got
+
+
+def _want():
     v, ri, nodes = _scene()
-    want, _ = O.render(v, ri, nodes, scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, W, H, n_batches=SPP)
+    want, _ = O.render(v, ri, nodes, CAM, scenes.REFERENCE_LIGHT, W, H, n_batches=SPP)
+    return want
+
+
+@pytest.mark.parametrize("world,slots", [(2, None), (4, None), (4, [2, 4, 4, 4])])
+def test_sparse_gather_with_product_tables_is_bit_exact(world, slots):
+    got = _run(_gather_worker, world, slots)
+    want = _want()
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+def test_culled_items_hold_exactly_the_fill_value():
+    """The premise of the sparse exchange: every pixel of a culled item is
+    (0,0,0,1) in a frame rendered from batch 0."""
+    _, _, nodes = _scene()
+    want = _want().reshape(-1, 4)
+    n_culled = 0
+    for r in range(3):
+        live, culled, pix = ptamd.partition_items(W, H, SPL, 3, r, None, _rects(nodes))
+        cp = pix[len(live):].reshape(-1)
+        cp = cp[cp >= 0]
+        n_culled += cp.size
+        assert np.all(want[cp] == np.array([0, 0, 0, 1], np.float32))
+    assert n_culled > 0
+
+
+@pytest.mark.parametrize("world,slots", [(2, None), (4, [3, 2, 2, 1])])
+def test_tile_split_reduce_is_bit_exact(world, slots):
+    got = _run(_reduce_worker, world, slots)
+    want = _want()
     assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
 
 
