@@ -52,6 +52,7 @@ sys.path.insert(0, os.path.join(ROOT, "discovering-path-tracer_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_ACHIEVABLE_GBS = 6300.0    # the guide's measured achievable HBM rate (MI355X_MICROARCH.md §HBM)
 # VALU issue peak: 1024 SIMDs x 2.4 GHz, one wave64 f32 instruction per 2
 # cycles per SIMD (MI355X_MICROARCH.md constants: v_fma_f32 2 cyc on SIMD-32)
 VALU_PEAK_GINST = 1024 * 2.4 / 2
@@ -217,7 +218,11 @@ def roofline_block(prof, time_ms, alg_bytes, kernel, kernel_ms, interval_ms, n_t
            "kernel": kernel, "kernel_ms": round(kernel_ms, 4), "launch_interval_ms": round(interval_ms, 4),
            "timed_launches": n_timed, "time_basis": time_basis,
            "algorithmic_bytes_per_launch": None if not alg_bytes else int(alg_bytes),
-           "effective_GBps": None if eff is None else round(eff, 2)}
+           "effective_GBps": None if eff is None else round(eff, 2),
+           "frac_of_achievable": None if achieved is None else round(achieved / HBM_ACHIEVABLE_GBS, 5),
+           "achievable_GBps": HBM_ACHIEVABLE_GBS,
+           "traffic_basis": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch (every gfx950 fabric read request is a "
+                            "128-B line tallied at 64 B: profiles/r02/fetch_calibration.json)"}
     if prof is not None:
         hb = prof[1]["hbm_bytes_per_launch"]
         if "raw_fetch_kib" in hb:

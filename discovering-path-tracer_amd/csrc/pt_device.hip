@@ -2087,7 +2087,11 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
   int dev = 0, cus = 0, per_cu_t = 0, per_cu_s = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+#ifdef PT_WF_FORCE_G
+  const bool g2 = PT_WF_FORCE_G == 2;
+#else
   const bool g2 = p0.n_tris < kWfGroup4Tris;
+#endif
   void (*trace)(RenderParams, WfBuffers, int) =
       cnt ? (lds_scene ? (g2 ? wf_trace_kernel<true, 2, true> : wf_trace_kernel<true, 4, true>)
                        : (g2 ? wf_trace_kernel<false, 2, true> : wf_trace_kernel<false, 4, true>))

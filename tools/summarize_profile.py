@@ -3,11 +3,11 @@
 into profiles/<tag>/<workload>_summary.json + the rocprofv3 stats CSV.
 
 HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and
-WRITE_SIZE are KiB, from separate passes; FETCH_SIZE is doubled (the guide's
-gfx950 correction for 16-B/lane streaming reads).  The raw readings are kept
-next to it, and, when profiles/<tag>/fetch_calibration.json exists (from
-tools/fetch_calib.hip), the calibrated ratios for 32-B and 48-B random
-gathers too.
+WRITE_SIZE are KiB, from separate passes; FETCH_SIZE is doubled.  The guide
+calibrates x2 for 16-B/lane streaming reads; profiles/r02/fetch_calibration.json
+(tools/fetch_calib.hip + request counters) shows it holds for the random
+32-B/48-B gathers of the traversal too: every fabric read request is a 128-B
+line and FETCH_SIZE tallies 64 B per request.  Raw readings are kept.
 
 box: the dominant kernel is one render_kernel launch per frame (averaged over
 its dispatches).  sphere/synthetic: a frame is the wavefront pipeline
@@ -50,6 +50,14 @@ def main(tag, workload, frames):
 
     pmc = {}
     pmc.update(per_launch(os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv"), ("FETCH_SIZE",)))
+    # per kernel family (FETCH_SIZE KiB per frame): where the reads come from
+    fam_fetch = {}
+    fpath = os.path.join(src, "pmc_FETCH_SIZE", "run_counter_collection.csv")
+    if os.path.exists(fpath) and not box:
+        for r in csv.DictReader(open(fpath)):
+            if match(r["Kernel_Name"]) and r["Counter_Name"] == "FETCH_SIZE":
+                f = next(w for w in WF_KERNELS if w in r["Kernel_Name"])
+                fam_fetch[f] = fam_fetch.get(f, 0.0) + float(r["Counter_Value"]) / frames
     pmc.update(per_launch(os.path.join(src, "pmc_WRITE_SIZE", "run_counter_collection.csv"), ("WRITE_SIZE",)))
     sq = per_launch(os.path.join(src, "pmc_SQ_INSTS_VALU", "run_counter_collection.csv"),
                     ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"))
@@ -68,12 +76,16 @@ def main(tag, workload, frames):
         write = pmc["WRITE_SIZE"] * 1024
         out["hbm_bytes_per_launch"] = {"fetch_corrected": fetch, "write": write, "total": fetch + write,
                                        "raw_fetch_kib": pmc["FETCH_SIZE"], "raw_write_kib": pmc["WRITE_SIZE"]}
+        if fam_fetch:
+            out["fetch_kib_by_kernel"] = fam_fetch
         if kernel_ms:
             out["hbm_GBps"] = {"x2_corrected": (fetch + write) / kernel_ms / 1e6,
                                "raw": (pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024 / kernel_ms / 1e6}
-    cal = os.path.join(dst, "fetch_calibration.json")
+    cal = os.path.join(ROOT, "profiles", "r02", "fetch_calibration.json")
     if os.path.exists(cal):
-        out["fetch_calibration"] = json.load(open(cal))
+        out["fetch_calibration"] = {k: v["fetch_over_algorithmic"] for k, v in json.load(open(cal)).items()
+                                    if isinstance(v, dict) and "fetch_over_algorithmic" in v}
+        out["fetch_calibration"]["source"] = "profiles/r02/fetch_calibration.json (x2 holds for 128-B line requests)"
     if sq:
         out["sq_per_launch"] = sq
     p = os.path.join(src, "bench_trace.log")
