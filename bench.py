@@ -234,8 +234,9 @@ def roofline_block(prof, time_ms, alg_bytes, kernel, kernel_ms, interval_ms, n_t
     if traffic is None:
         out["note"] = "no committed rocprofv3 summary of this kernel source and workload: traffic unmeasured"
     elif eff is not None and eff > HBM_PEAK_GBS:
-        out["note"] = ("effective_GBps exceeds the HBM peak because the algorithmic node/triangle bytes are "
-                       "served from LDS/L2, not HBM; frac is the measured HBM traffic over the kernel time")
+        out["note"] = ("effective_GBps counts the reference's exhaustive node/triangle bytes (SURVEY 8d) over the "
+                       "kernel time; the kernel serves them from LDS/L2/MALL and skips exact no-op work, so it can "
+                       "exceed the HBM peak.  frac is the measured HBM traffic over the kernel time")
     return out
 
 
