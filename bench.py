@@ -295,6 +295,58 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device):
     return out
 
 
+def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light, cam, depth, sss):
+    """RCCL communicator for pt_dist_run and a 4-frame bitwise self-check on
+    the root against a single-GPU render; None (every rank) if anything
+    fails, so the caller keeps the Python step."""
+    import ptamd
+    import torch
+    ok = 1
+    uid = bytes(128)
+    if rank == 0:
+        try:
+            uid = ptamd.Renderer.dist_unique_id()
+        except ptamd.PTError as e:
+            print(f"bench: native step loop unavailable: {e}", file=sys.stderr, flush=True)
+            ok = 0
+    t = torch.tensor([ok] + list(uid), dtype=torch.uint8, device=dev)
+    dist.broadcast(t, 0)   # the id, and whether rank 0 could make one
+    if int(t[0].item()) == 0:
+        return None
+    frames = None
+    try:
+        r.dist_init(bytes(t[1:].cpu().tolist()), world, rank)
+        frames = torch.full((2, H, W, 4), float("nan"), dtype=torch.float32, device=dev)
+        r.dist_run(spp, 4, frames.data_ptr(), 2)
+        r.synchronize()
+        if rank == 0:
+            ref = ptamd.Renderer(dev.index)
+            ref.upload_scene(v, i, n, int_bits=int_bits)
+            ref.upload_lights(light)
+            ref.set_camera(cam)
+            ref.set_params(depth, sss)
+            ref.resize_and_clear(W, H)
+            ref.render(0, spp)
+            want = ref.read_accum().view(np.uint32)
+            del ref
+            for f in range(2):
+                if not np.array_equal(frames[f].cpu().numpy().reshape(-1).view(np.uint32), want):
+                    ok = 0
+    except ptamd.PTError as e:
+        print(f"bench: native step loop unavailable: {e}", file=sys.stderr, flush=True)
+        ok = 0
+    flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 0:
+        print("bench: native step loop failed its self-check; using the Python step", file=sys.stderr, flush=True)
+        try:
+            r.dist_finalize()
+        except ptamd.PTError:
+            pass
+        return None
+    return {"frames": frames, "outs": [frames[0], frames[1]]}
+
+
 class _StreamWork:
     """Stand-in for an async collective's Work in the rank emulation: wait()
     orders the caller's current stream after what `stream` had queued when
@@ -626,8 +678,27 @@ def main():
         while pending:
             finish(*pending.pop(0))
 
-    for _ in range(args.warmup):
-        step()
+    # Native step loop (pt_dist_*): the same pipelined sparse gather with the
+    # RCCL send/recv issued from C++ -- no Python per frame.  Used for N > 1
+    # over RCCL (and PT_BENCH_FORCE_DIST=1 at N = 1) unless PT_BENCH_NATIVE=0.
+    # A 4-frame self-check against a single-GPU render runs first; if the root
+    # finds any bit different, every rank falls back to the Python step.
+    native = None
+    if (dist is not None and backend == "nccl" and args.collective == "gather" and args.assemble == 2
+            and os.environ.get("PT_BENCH_NATIVE", "1") != "0"):
+        native = setup_native(r, dist, dev, world, rank, W, H, SPP, v, i, n, int_bits, light, cam, DEPTH, SSS)
+        if native is not None:
+            outs = native["outs"]
+            out = outs[0]
+
+    def run_steps(k):
+        if native is not None:
+            r.dist_run(SPP, k, native["frames"].data_ptr(), 2)
+        else:
+            for _ in range(k):
+                step()
+
+    run_steps(args.warmup)
     drain()
     r.synchronize()
     torch.cuda.synchronize(dev)
@@ -635,8 +706,7 @@ def main():
         dist.barrier()
     r.reset_launch_times()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run_steps(args.steps)
     t_enq = time.perf_counter() - t0   # host time to issue the steps (no sync inside)
     drain()
     r.synchronize()
@@ -662,7 +732,8 @@ def main():
     no_cull = None
     default_cfg = args.scene == "box" and (W, H, SPP, DEPTH, SSS) == (1920, 1080, 8, 4, 3)
     if args.compare_no_cull is None:
-        args.compare_no_cull = int(world == 1 and emu == 1 and default_cfg and not args.packed and not args.profile_run)
+        args.compare_no_cull = int(world == 1 and emu == 1 and default_cfg and not args.packed and not args.profile_run
+                                   and dist is None)
     if world == 1 and args.compare_no_cull:
         # the same frames with primary-ray culling off (every pixel generated
         # and traced), for reference next to the default
@@ -730,6 +801,7 @@ def main():
                        "parallelism": (f"tiles{world}-" + ("sparse-gather" if args.collective == "gather" else "reduce"))
                        if world > 1 else ("single-packed" if args.packed else "single"),
                        "streams": args.streams,
+                       "step_loop": "native (pt_dist_run, RCCL from C++)" if native is not None else "python",
                        "rays_per_frame": None if rays_per_frame != rays_per_frame else int(rays_per_frame),
                        "primary_cull": True,
                        "msamples_per_s": round(W * H * SPP * args.steps / dt / 1e6, 3)},

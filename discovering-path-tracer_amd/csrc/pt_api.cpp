@@ -7,8 +7,10 @@
 // an explicit pt_synchronize / pt_read_accum.  Scene preparation that the
 // device layout needs (threading the BVH, building triangle records) happens
 // here once per upload.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <rccl/rccl.h>   // types only: the functions are resolved at run time (rccl_api)
 #include <string.h>
 
 #include <algorithm>
@@ -277,6 +279,22 @@ int cull_rects(const float cam[16], int W, int H, const float* lo, const float* 
 
 }  // namespace
 
+// Native multi-GPU step loop state (pt_dist_*): an RCCL communicator of its
+// own, a high-priority stream for the gathers, two render streams (frames
+// alternate), and double-buffered send / receive slots.
+struct DistState {
+  ncclComm_t comm = nullptr;
+  int nranks = 0, rank = 0;
+  hipStream_t comm_stream = nullptr;
+  hipStream_t streams[2] = {nullptr, nullptr};
+  hipEvent_t render_done[2] = {nullptr, nullptr}, gather_done[2] = {nullptr, nullptr};
+  float* send[2] = {nullptr, nullptr};
+  float* recv[2] = {nullptr, nullptr};   // root: nranks slots each
+  size_t slot_floats = 0, cap_floats = 0;
+  std::vector<float> layout_key;         // frame_key of the layout the slots were sized for
+  bool ready = false;
+};
+
 struct pt_context {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -300,6 +318,9 @@ struct pt_context {
   pt_params params{4, 3};
   int nranks = 1, rank = 0;
   std::vector<int> slots{1};    // partition slots per rank (pt_set_partition_slots)
+  std::vector<ptd::Part> parts;  // every rank's share, derived from slots (ensure_parts)
+  bool parts_valid = false;     // parts match slots
+  bool parts_synced = false;    // d_parts holds parts
   int* d_parts = nullptr;       // every rank's slot positions, kMaxSlots ints each (rank_tile)
   size_t parts_cap = 0;
   std::vector<int> parts_key;
@@ -333,6 +354,7 @@ struct pt_context {
   int n_unpack = 0;
   std::vector<float> unpack_key;
   std::vector<float> packed_key;   // frame parameters of the last pt_render_packed
+  std::vector<float> key_scratch, items_scratch;   // per-launch keys, built without reallocating
   float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};   // root AABB of the uploaded tree
   std::vector<pt_area_light> lights_host;
   // wavefront pipeline buffers (PT_OPT_KERNEL 3), grown on demand
@@ -378,6 +400,7 @@ struct pt_context {
   int opt_timing = 1;         // PT_OPT_LAUNCH_TIMING: event pair on every k-th launch, 0 = none
   long long launch_n = 0;     // render launches since pt_reset_launch_times
   long long ring_launch[kRing] = {};   // launch number of each recorded pair
+  DistState* dist = nullptr;           // pt_dist_init
 };
 
 struct pt_scene {
@@ -466,7 +489,28 @@ static ptd::Part part_of_slots(const std::vector<int>& slots, int r) {
     if (seq[v].second == r) pt.pos[pt.cnt++] = v;
   return pt;
 }
-static ptd::Part part_of(const pt_context* c, int r) { return part_of_slots(c->slots, r); }
+// Every rank's share, computed once per partition change (one sort of the
+// period for all ranks) -- not per launch: at 8 ranks the per-call derivation
+// cost ~10 us of host time per render launch.
+static void ensure_parts(pt_context* c) {
+  if (c->parts_valid && c->parts.size() == c->slots.size()) return;
+  std::vector<std::pair<double, int>> seq;
+  for (int i = 0; i < (int)c->slots.size(); ++i)
+    for (int k = 0; k < c->slots[i]; ++k) seq.push_back({(k + 0.5) / c->slots[i], i});
+  std::stable_sort(seq.begin(), seq.end());
+  c->parts.assign(c->slots.size(), ptd::Part{});
+  for (auto& pt : c->parts) pt.m = (int)seq.size();
+  for (int v = 0; v < (int)seq.size(); ++v) {
+    ptd::Part& pt = c->parts[seq[v].second];
+    pt.pos[pt.cnt++] = v;
+  }
+  c->parts_valid = true;
+  c->parts_synced = false;
+}
+static const ptd::Part& part_of(pt_context* c, int r) {
+  ensure_parts(c);
+  return c->parts[r];
+}
 
 // Upload every rank's slot positions when the partition changed; the device
 // copy of rank r's starts at d_parts + r * kMaxSlots.
@@ -481,16 +525,22 @@ static int upload_ints_(const std::vector<int>& h, int** d, size_t* cap) {
   return PT_OK;
 }
 static int sync_parts(pt_context* c) {
+  ensure_parts(c);
+  if (c->parts_synced && c->d_parts) return PT_OK;
   std::vector<int> all((size_t)c->nranks * ptd::kMaxSlots, 0);
   for (int r = 0; r < c->nranks; ++r) {
-    const ptd::Part pt = part_of(c, r);
+    const ptd::Part& pt = c->parts[r];
     for (int i = 0; i < pt.cnt; ++i) all[(size_t)r * ptd::kMaxSlots + i] = pt.pos[i];
   }
-  if (all == c->parts_key && c->d_parts) return PT_OK;
+  if (all == c->parts_key && c->d_parts) {
+    c->parts_synced = true;
+    return PT_OK;
+  }
   { const int rc_ = quiesce(c); if (rc_) return rc_; }
   const int rc = upload_ints_(all, &c->d_parts, &c->parts_cap);
   if (rc) return rc;
   c->parts_key = all;
+  c->parts_synced = true;
   return PT_OK;
 }
 
@@ -534,11 +584,12 @@ static void item_lists(const ptd::RenderParams& p, const ptd::Part& part, std::v
 }
 
 static int compact_items(pt_context* c, ptd::RenderParams* p) {
-  const ptd::Part pt = part_of(c, p->rank);
+  const ptd::Part& pt = part_of(c, p->rank);
   // every slot position of this rank's share: two slot sets with the same
   // period, count and first position still deal different tiles
-  std::vector<float> key = {(float)p->width, (float)p->height, (float)pt.m, (float)pt.cnt,
-                            (float)p->rank, (float)p->spl, (float)p->n_cull, (float)p->item_order};
+  std::vector<float>& key = c->items_scratch;
+  key.assign({(float)p->width, (float)p->height, (float)pt.m, (float)pt.cnt, (float)p->rank, (float)p->spl,
+              (float)p->n_cull, (float)p->item_order});
   for (int k = 0; k < pt.cnt; ++k) key.push_back((float)pt.pos[k]);
   for (int r = 0; r < p->n_cull; ++r) key.insert(key.end(), p->cull[r], p->cull[r] + 4);
   if (key.size() != c->items_key.size() || memcmp(key.data(), c->items_key.data(), key.size() * 4) != 0) {
@@ -567,12 +618,13 @@ static int compact_items(pt_context* c, ptd::RenderParams* p) {
 }
 
 namespace {
-std::vector<float> frame_key(const pt_context* c, const ptd::RenderParams& p) {
-  std::vector<float> key = {(float)p.width, (float)p.height, (float)p.nranks, (float)p.rank, (float)p.spl,
-                            (float)p.n_cull, (float)p.blocks_x, (float)p.blocks_total, (float)p.item_order};
-  for (int r = 0; r < p.n_cull; ++r) key.insert(key.end(), p.cull[r], p.cull[r] + 4);
-  for (int sl : c->slots) key.push_back((float)sl);   // every rank's share (the assembly table)
-  return key;
+// The frame parameters an item layout depends on, into *key (its capacity is
+// kept between launches: no allocation per launch).
+void frame_key(const pt_context* c, const ptd::RenderParams& p, std::vector<float>* key) {
+  key->assign({(float)p.width, (float)p.height, (float)p.nranks, (float)p.rank, (float)p.spl, (float)p.n_cull,
+               (float)p.blocks_x, (float)p.blocks_total, (float)p.item_order});
+  for (int r = 0; r < p.n_cull; ++r) key->insert(key->end(), p.cull[r], p.cull[r] + 4);
+  for (int sl : c->slots) key->push_back((float)sl);   // every rank's share (the assembly table)
 }
 int upload_ints(const std::vector<int>& h, int** d, size_t* cap) {
   if (h.size() > *cap) {
@@ -590,8 +642,7 @@ constexpr long long kWfMaxPaths = 1ll << 24;
 constexpr int kWfAutoTris = 32768;
 // The root's assembly table for frames rendered with params p: per rank its
 // live items {rank, tile*8 + part, slot} and its culled items {rank, tile*8 + part, -1}.
-int unpack_table(pt_context* c, const ptd::RenderParams& p) {
-  const std::vector<float> key = frame_key(c, p);
+int unpack_table(pt_context* c, const ptd::RenderParams& p, const std::vector<float>& key) {
   if (key == c->unpack_key) return PT_OK;
   std::vector<int> table, live, culled;
   for (int r = 0; r < p.nranks; ++r) {
@@ -689,7 +740,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.blocks_total = p.blocks_x * ((c->height + 15) / 16);
   p.nranks = c->nranks;
   p.rank = c->rank;
-  const ptd::Part hpart = part_of(c, c->rank);
+  const ptd::Part& hpart = part_of(c, c->rank);
   {
     const int rc = sync_parts(c);
     if (rc) return rc;
@@ -768,12 +819,15 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.n_unpack = 0;
   p.unpack_slot_f4 = 0;
   if (pack_out) {
-    const std::vector<float> key = frame_key(c, p);
+    frame_key(c, p, &c->key_scratch);
+    const std::vector<float>& key = c->key_scratch;
     if (as.src && key != c->packed_key)
       return fail(PT_ERR_INVALID, "pt_render_packed: the frame to assemble has another item layout (size, partition, lanes, culling)");
     if (wf || sm) {
       // these kernels render into the accumulation buffer: render, pack,
-      // then assemble the previous frame in a launch of its own
+      // then assemble the previous frame in a launch of its own (the calls
+      // below rebuild c->key_scratch: keep this frame's key)
+      const std::vector<float> frame_k = key;
       if (as.src) {
         const int rc = pt_items_unpack_all(c, as.src, as.slot_floats, as.frame);
         if (rc) return rc;
@@ -783,13 +837,13 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
       const int rc = render_impl(c, 0, n_batches, nullptr);
       c->opt_fresh = fresh;
       if (rc) return rc;
-      c->packed_key = key;
+      c->packed_key = frame_k;
       const int rp = pt_items_pack(c, pack_out);
       if (rp) return rp;
       return mark_shared(c);   // the pack read the accumulation buffer
     }
     if (as.src) {
-      const int rc = unpack_table(c, p);
+      const int rc = unpack_table(c, p, key);
       if (rc) return rc;
       p.unpack_src = (const float4*)as.src;
       p.unpack_frame = (float4*)as.frame;
@@ -877,10 +931,13 @@ int pt_create(int device_ordinal, pt_context** out) {
   return PT_OK;
 }
 
+int pt_dist_finalize(pt_context* c);
+
 int pt_destroy(pt_context* c) {
   if (!c) return PT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->dist) (void)pt_dist_finalize(c);
   (void)quiesce(c);
   for (auto& u : c->uses) (void)hipEventDestroy(u.ev);
   c->uses.clear();
@@ -922,6 +979,10 @@ int pt_synchronize(pt_context* c) {
   if (!c) return fail(PT_ERR_INVALID, "null context");
   PT_HIP(hipSetDevice(c->device));
   PT_HIP(hipStreamSynchronize(c->stream));
+  if (c->dist) {   // the native step loop's streams
+    for (hipStream_t s : {c->dist->streams[0], c->dist->streams[1], c->dist->comm_stream})
+      if (s) PT_HIP(hipStreamSynchronize(s));
+  }
   return PT_OK;
 }
 
@@ -1027,6 +1088,7 @@ int pt_set_partition(pt_context* c, int nranks, int rank) {
   c->nranks = nranks;
   c->rank = rank;
   c->slots.assign((size_t)nranks, 1);
+  c->parts_valid = false;
   c->items_key.clear();   // the cached item lists follow the partition
   return PT_OK;
 }
@@ -1043,6 +1105,7 @@ int pt_set_partition_slots(pt_context* c, int nranks, int rank, const int* slots
   c->nranks = nranks;
   c->rank = rank;
   c->slots.assign(slots, slots + nranks);
+  c->parts_valid = false;
   c->items_key.clear();
   return PT_OK;
 }
@@ -1337,7 +1400,8 @@ int pt_items_pack(pt_context* c, void* dst) {
   if (!c || !dst) return fail(PT_ERR_INVALID, "null argument");
   if (!c->last_valid || !c->d_accum) return fail(PT_ERR_INVALID, "no path-recursive pt_render yet");
   PT_HIP(hipSetDevice(c->device));
-  const std::vector<float> key = frame_key(c, c->last);
+  frame_key(c, c->last, &c->key_scratch);
+  const std::vector<float>& key = c->key_scratch;
   if (key != c->pack_key) {
     std::vector<int> live, culled;
     item_lists(c->last, part_of(c, c->last.rank), &live, &culled);
@@ -1361,7 +1425,8 @@ int pt_items_unpack_all(pt_context* c, const void* src, size_t slot_floats, void
   if ((((uintptr_t)src) & 15) || (((uintptr_t)frame) & 15) || (slot_floats & 3))
     return fail(PT_ERR_INVALID, "buffers must be 16-B aligned, slots whole float4s");
   PT_HIP(hipSetDevice(c->device));
-  const int rc = unpack_table(c, c->last);
+  frame_key(c, c->last, &c->key_scratch);
+  const int rc = unpack_table(c, c->last, c->key_scratch);
   if (rc) return rc;
   PT_HIP(ptd::launch_items_unpack(c->last, (float4*)frame, (const float4*)src, slot_floats / 4, c->d_unpack,
                                   c->n_unpack, c->stream));
@@ -1872,6 +1937,230 @@ int pt_default_camera(float ubo[16]) {
   if (!ubo) return fail(PT_ERR_INVALID, "null argument");
   pt::Camera cam;
   cam.toUBO(ubo);
+  return PT_OK;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// Native multi-GPU step loop: the tile split's frames with the
+// RCCL gather issued from C++, so a run of frames costs no Python per frame.
+// bench.py's Python step (render_packed + torch.distributed.gather + stream
+// switches) costs ~40-50 us of host time per frame, more than the ~40-us GPU
+// step of a 1/8 box.obj share; here one frame is a render_packed launch, two
+// event operations and one grouped send/recv.
+// ===========================================================================
+namespace {
+struct RcclApi {
+  void* h = nullptr;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*GroupStart)() = nullptr;
+  ncclResult_t (*GroupEnd)() = nullptr;
+  ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
+// RCCL is loaded only when the multi-GPU loop is used: the one already in
+// the process (torch's) if there is one, else the system's.
+const RcclApi* rccl_api() {
+  static RcclApi api;
+  static bool tried = false;
+  if (!tried) {
+    tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (h) {
+      api.GetUniqueId = (decltype(api.GetUniqueId))dlsym(h, "ncclGetUniqueId");
+      api.CommInitRank = (decltype(api.CommInitRank))dlsym(h, "ncclCommInitRank");
+      api.CommDestroy = (decltype(api.CommDestroy))dlsym(h, "ncclCommDestroy");
+      api.GroupStart = (decltype(api.GroupStart))dlsym(h, "ncclGroupStart");
+      api.GroupEnd = (decltype(api.GroupEnd))dlsym(h, "ncclGroupEnd");
+      api.Send = (decltype(api.Send))dlsym(h, "ncclSend");
+      api.Recv = (decltype(api.Recv))dlsym(h, "ncclRecv");
+      api.GetErrorString = (decltype(api.GetErrorString))dlsym(h, "ncclGetErrorString");
+      if (api.GetUniqueId && api.CommInitRank && api.CommDestroy && api.GroupStart && api.GroupEnd && api.Send &&
+          api.Recv && api.GetErrorString)
+        api.h = h;
+    }
+  }
+  return api.h ? &api : nullptr;
+}
+#define PT_NCCL(call)                                                                                   \
+  do {                                                                                                  \
+    ncclResult_t r_ = (call);                                                                           \
+    if (r_ != ncclSuccess) return fail(PT_ERR_HIP, std::string(#call ": ") + R->GetErrorString(r_));    \
+  } while (0)
+
+// Slot size and buffers for the layout of the last rendered frame (c->last).
+int dist_layout(pt_context* c) {
+  DistState* d = c->dist;
+  std::vector<float> key;
+  frame_key(c, c->last, &key);
+  if (key == d->layout_key && d->send[0]) return PT_OK;
+  size_t live_max = 0;
+  std::vector<int> live, culled;
+  for (int r = 0; r < c->nranks; ++r) {
+    item_lists(c->last, part_of(c, r), &live, &culled);
+    live_max = std::max(live_max, live.size());
+  }
+  const size_t slot = std::max<size_t>(4, live_max * (size_t)(256 / c->last.spl) * 4);
+  if (slot > d->cap_floats) {
+    for (int b = 0; b < 2; ++b)
+      for (hipStream_t s : {d->streams[b], d->comm_stream}) PT_HIP(hipStreamSynchronize(s));
+    for (int b = 0; b < 2; ++b) {
+      dev_free(d->send[b]);
+      dev_free(d->recv[b]);
+    }
+    d->cap_floats = 0;
+    for (int b = 0; b < 2; ++b) {
+      PT_HIP(hipMalloc((void**)&d->send[b], slot * sizeof(float)));
+      PT_HIP(hipMemset(d->send[b], 0, slot * sizeof(float)));
+      if (d->rank == 0) {
+        PT_HIP(hipMalloc((void**)&d->recv[b], (size_t)d->nranks * slot * sizeof(float)));
+        PT_HIP(hipMemset(d->recv[b], 0, (size_t)d->nranks * slot * sizeof(float)));
+      }
+    }
+    d->cap_floats = slot;
+  }
+  d->slot_floats = slot;
+  d->layout_key = key;
+  return PT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int pt_dist_unique_id(void* id, size_t id_bytes) {
+  if (!id || id_bytes < sizeof(ncclUniqueId)) return fail(PT_ERR_INVALID, "id buffer must hold 128 bytes");
+  const RcclApi* R = rccl_api();
+  if (!R) return fail(PT_ERR_UNSUPPORTED, "RCCL (librccl.so.1) could not be loaded");
+  ncclUniqueId u;
+  PT_NCCL(R->GetUniqueId(&u));
+  memcpy(id, &u, sizeof u);
+  return PT_OK;
+}
+
+int pt_dist_init(pt_context* c, const void* id, int nranks, int rank) {
+  if (!c || !id) return fail(PT_ERR_INVALID, "null argument");
+  if (nranks != c->nranks || rank != c->rank)
+    return fail(PT_ERR_INVALID, "pt_dist_init: set the same partition first (pt_set_partition / _slots)");
+  const RcclApi* R = rccl_api();
+  if (!R) return fail(PT_ERR_UNSUPPORTED, "RCCL (librccl.so.1) could not be loaded");
+  if (c->dist) pt_dist_finalize(c);
+  PT_HIP(hipSetDevice(c->device));
+  DistState* d = new DistState();
+  c->dist = d;
+  d->nranks = nranks;
+  d->rank = rank;
+  int lo = 0, hi = 0;
+  PT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  PT_HIP(hipStreamCreateWithPriority(&d->comm_stream, hipStreamNonBlocking, hi));   // gathers take CUs first
+  for (int b = 0; b < 2; ++b) {
+    PT_HIP(hipStreamCreateWithFlags(&d->streams[b], hipStreamNonBlocking));
+    PT_HIP(hipEventCreateWithFlags(&d->render_done[b], hipEventDisableTiming));
+    PT_HIP(hipEventCreateWithFlags(&d->gather_done[b], hipEventDisableTiming));
+  }
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  PT_NCCL(R->CommInitRank(&d->comm, nranks, u, rank));
+  d->ready = true;
+  return PT_OK;
+}
+
+int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, void* frames, int n_frame_bufs) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  DistState* d = c->dist;
+  if (!d || !d->ready) return fail(PT_ERR_INVALID, "pt_dist_run: no communicator (pt_dist_init)");
+  if (n_frames < 0 || n_batches == 0) return fail(PT_ERR_INVALID, "pt_dist_run: bad frame or batch count");
+  if (d->rank == 0 && (!frames || n_frame_bufs < 1 || (((uintptr_t)frames) & 15)))
+    return fail(PT_ERR_INVALID, "pt_dist_run: the root needs 16-B aligned frame buffers");
+  if (d->nranks != c->nranks || d->rank != c->rank) return fail(PT_ERR_INVALID, "partition changed since pt_dist_init");
+  if (!c->last_valid) return fail(PT_ERR_INVALID, "pt_dist_run: render one frame with pt_render first (item layout)");
+  const RcclApi* R = rccl_api();
+  PT_HIP(hipSetDevice(c->device));
+  {
+    const int rc = dist_layout(c);
+    if (rc) return rc;
+  }
+  const size_t slot = d->slot_floats;
+  const size_t frame_f = (size_t)c->width * c->height * 4;
+  hipStream_t saved = c->stream;
+  int rc = PT_OK;
+  // frame k: stream and buffer set k % 2.  Frame k's launch (pt_render_packed)
+  // also assembles frame k-2 on the root, whose gather ran during frame k-1;
+  // frame k's own gather overwrites that receive set after the launch that
+  // read it.  Frame k first waits for the gather of frame k-2, which read the
+  // send slot it is about to overwrite.
+  for (int k = 0; k < n_frames && rc == PT_OK; ++k) {
+    const int b = k & 1;
+    c->stream = d->streams[b];
+    Assembly as;
+    if (k >= 2) {
+      PT_HIP(hipStreamWaitEvent(c->stream, d->gather_done[b], 0));
+      if (d->rank == 0) {
+        as.src = d->recv[b];
+        as.slot_floats = slot;
+        as.frame = (float*)frames + (size_t)((k - 2) % n_frame_bufs) * frame_f;
+      }
+    }
+    rc = render_impl(c, 0, n_batches, (float4*)d->send[b], as);
+    if (rc) break;
+    PT_HIP(hipEventRecord(d->render_done[b], c->stream));
+    PT_HIP(hipStreamWaitEvent(d->comm_stream, d->render_done[b], 0));
+    PT_NCCL(R->GroupStart());
+    if (d->rank == 0)
+      for (int r = 0; r < d->nranks; ++r) PT_NCCL(R->Recv(d->recv[b] + (size_t)r * slot, slot, ncclFloat32, r, d->comm, d->comm_stream));
+    PT_NCCL(R->Send(d->send[b], slot, ncclFloat32, 0, d->comm, d->comm_stream));
+    PT_NCCL(R->GroupEnd());
+    PT_HIP(hipEventRecord(d->gather_done[b], d->comm_stream));
+  }
+  // the root assembles the last (up to) two frames in launches of their own
+  if (rc == PT_OK && d->rank == 0) {
+    frame_key(c, c->last, &c->key_scratch);
+    rc = unpack_table(c, c->last, c->key_scratch);
+    for (int k = std::max(0, n_frames - 2); k < n_frames && rc == PT_OK; ++k) {
+      const int b = k & 1;
+      c->stream = d->streams[b];
+      PT_HIP(hipStreamWaitEvent(c->stream, d->gather_done[b], 0));
+      float4* out = (float4*)((float*)frames + (size_t)(k % n_frame_bufs) * frame_f);
+      PT_HIP(ptd::launch_items_unpack(c->last, out, (const float4*)d->recv[b], slot / 4, c->d_unpack, c->n_unpack,
+                                      c->stream));
+      rc = note_use(c);
+    }
+  }
+  c->stream = saved;
+  return rc;
+}
+
+int pt_dist_slot_floats(pt_context* c, size_t* slot_floats) {
+  if (!c || !slot_floats) return fail(PT_ERR_INVALID, "null argument");
+  if (!c->dist || !c->dist->slot_floats) return fail(PT_ERR_INVALID, "no pt_dist_run yet");
+  *slot_floats = c->dist->slot_floats;
+  return PT_OK;
+}
+
+int pt_dist_finalize(pt_context* c) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  DistState* d = c->dist;
+  if (!d) return PT_OK;
+  (void)hipSetDevice(c->device);
+  for (hipStream_t s : {d->streams[0], d->streams[1], d->comm_stream})
+    if (s) (void)hipStreamSynchronize(s);
+  const RcclApi* R = rccl_api();
+  if (d->comm && R) (void)R->CommDestroy(d->comm);
+  for (int b = 0; b < 2; ++b) {
+    dev_free(d->send[b]);
+    dev_free(d->recv[b]);
+    if (d->render_done[b]) (void)hipEventDestroy(d->render_done[b]);
+    if (d->gather_done[b]) (void)hipEventDestroy(d->gather_done[b]);
+    if (d->streams[b]) (void)hipStreamDestroy(d->streams[b]);
+  }
+  if (d->comm_stream) (void)hipStreamDestroy(d->comm_stream);
+  delete d;
+  c->dist = nullptr;
   return PT_OK;
 }
 

@@ -42,6 +42,7 @@ EXPORTS = [
     "pt_progressive_camera", "pt_progressive_advance", "pt_readback_begin", "pt_readback_end", "pt_write_image",
     "pt_items_live", "pt_items_pack", "pt_items_unpack_all", "pt_render_packed", "pt_launch_span_ms",
     "pt_set_partition_slots", "pt_get_traced", "pt_partition_items",
+    "pt_dist_unique_id", "pt_dist_init", "pt_dist_run", "pt_dist_slot_floats", "pt_dist_finalize",
 ]
 
 
@@ -91,7 +92,10 @@ def lib():
             "pt_tiles_owned": ([vp, ctypes.POINTER(i32)], i32), "pt_tiles_pack": ([vp, vp], i32),
             "pt_tiles_unpack": ([vp, vp, i32, vp], i32), "pt_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
             "pt_reset_stats": ([vp], i32), "pt_get_traced": ([vp, ctypes.POINTER(Traced)], i32),
-            "pt_partition_items": ([i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, psz, vp, psz, vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
+            "pt_partition_items": ([i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, psz, vp, psz, vp], i32),
+            "pt_dist_unique_id": ([vp, sz], i32), "pt_dist_init": ([vp, vp, i32, i32], i32),
+            "pt_dist_run": ([vp, u32, i32, vp, i32], i32), "pt_dist_slot_floats": ([vp, psz], i32),
+            "pt_dist_finalize": ([vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
             "pt_launch_times_ms": ([vp, vp, sz, psz], i32), "pt_reset_launch_times": ([vp], i32),
             "pt_launch_span_ms": ([vp, ctypes.POINTER(ctypes.c_float), psz], i32),
             "pt_selftest_math": ([i32, i32, vp, vp, sz], i32),
@@ -460,6 +464,29 @@ class Renderer:
         s = Stats()
         _check(lib().pt_get_stats(self._c, ctypes.byref(s)), "pt_get_stats")
         return {"rays": s.rays, "nodes": s.nodes, "leaf_tests": s.leaf_tests, "samples": s.samples}
+
+    # ---- native multi-GPU step loop (pt_dist_*) ----
+    @staticmethod
+    def dist_unique_id():
+        """128-byte RCCL communicator id (rank 0 makes it, every rank gets a copy)."""
+        buf = (ctypes.c_char * 128)()
+        _check(lib().pt_dist_unique_id(buf, 128), "pt_dist_unique_id")
+        return bytes(buf)
+
+    def dist_init(self, uid, nranks, rank):
+        b = (ctypes.c_char * 128).from_buffer_copy(uid)
+        _check(lib().pt_dist_init(self._c, b, nranks, rank), "pt_dist_init")
+
+    def dist_run(self, n_batches, n_frames, frames_ptr=None, n_frame_bufs=1):
+        _check(lib().pt_dist_run(self._c, n_batches, n_frames, frames_ptr, n_frame_bufs), "pt_dist_run")
+
+    def dist_slot_floats(self):
+        n = ctypes.c_size_t(0)
+        _check(lib().pt_dist_slot_floats(self._c, ctypes.byref(n)), "pt_dist_slot_floats")
+        return n.value
+
+    def dist_finalize(self):
+        _check(lib().pt_dist_finalize(self._c), "pt_dist_finalize")
 
     def traced(self):
         """Work the fast kernels actually did while PT_OPT_COUNT_TRACED was on

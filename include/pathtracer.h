@@ -224,6 +224,31 @@ int pt_partition_items(int width, int height, int sample_lanes, int nranks, int 
                        const float* cull_rects, int n_cull, int item_order, int* live, size_t* n_live,
                        int* culled, size_t* n_culled, int* pixel_of);
 
+/* ---- native multi-GPU step loop (RCCL) ------------------ */
+/* The tile split's pipelined sparse gather with the collective issued from
+ * C++: frames alternate between two internal streams; frame k's launch
+ * renders this rank's live items into a send slot and, on the root, assembles
+ * frame k-2 (pt_render_packed); a grouped RCCL send/recv on a high-priority
+ * stream gathers every rank's slot on rank 0.  RCCL (librccl.so.1) is loaded
+ * at run time -- the copy already in the process if there is one -- so the
+ * single-GPU library needs none.
+ * pt_dist_unique_id: rank 0 makes the communicator id (128 bytes), which the
+ * caller broadcasts (e.g. over torch.distributed); pt_dist_init: every rank,
+ * collectively, after setting the same partition; pt_dist_run: n_frames
+ * frames of n_batches samples (batch 0..n-1, fresh); the root writes frame j
+ * to frames + (j % n_frame_bufs) * W*H*4 floats (device memory; ignored on
+ * other ranks).  Every rank must have rendered the frame's configuration once
+ * with pt_render (it fixes the item layout).  Work is enqueued; the frames
+ * are complete after pt_synchronize.  pt_dist_finalize frees it (also done
+ * by pt_destroy).  Replaces, for the tile split, the reference's
+ * dispatch-and-readback per frame (VulkanRayTracer.cpp:803-865). */
+#define PT_DIST_ID_BYTES 128
+int pt_dist_unique_id(void* id, size_t id_bytes);
+int pt_dist_init(pt_context* ctx, const void* id, int nranks, int rank);
+int pt_dist_run(pt_context* ctx, uint32_t n_batches, int n_frames, void* frames_device, int n_frame_bufs);
+int pt_dist_slot_floats(pt_context* ctx, size_t* slot_floats);
+int pt_dist_finalize(pt_context* ctx);
+
 /* ---- kernel options ---------------------------------------------------- */
 /* PT_OPT_SCENE_IN_LDS: stage the scene in LDS per workgroup — 0 never,
  * 1 when it fits in 48 KB (default), 2 always (error if it does not fit).

@@ -43,3 +43,19 @@ def test_two_rank_bench_verifies_bitwise(collective, extra):
     assert out["n_gpus"] == 2
     assert out["verified_bitwise_vs_single_gpu"] is True
     assert out["config"]["rays_traced"] > 0
+
+
+def test_native_step_loop_single_rank_rccl():
+    """pt_dist_run (RCCL driven from C++) at N = 1 on the box: a real RCCL
+    communicator of one rank, the grouped self send/recv, the two-stream
+    pipeline, the fused and the trailing assemblies -- checked bitwise by
+    bench.py's self-check and by --verify over every assembled frame."""
+    env = dict(os.environ, PT_BENCH_FORCE_DIST="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "7", "--warmup", "3", "--verify",
+           "--no-scene-legs", "--no-cpu-baseline"]
+    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
+    out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["config"]["step_loop"].startswith("native"), res.stderr[-2000:]
+    assert out["verified_bitwise_vs_single_gpu"] is True
