@@ -317,7 +317,7 @@ def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light,
     try:
         r.dist_init(bytes(t[1:].cpu().tolist()), world, rank)
         frames = torch.full((2, H, W, 4), float("nan"), dtype=torch.float32, device=dev)
-        r.dist_run(spp, 4, frames.data_ptr(), 2)
+        r.dist_run(spp, 4, frames.data_ptr(), 2, n_streams=1)
         r.synchronize()
         if rank == 0:
             ref = ptamd.Renderer(dev.index)
@@ -690,16 +690,37 @@ def main():
         if native is not None:
             outs = native["outs"]
             out = outs[0]
+    elif (dist is None and emu > 1 and emu_rank == 0 and args.collective == "gather" and args.assemble == 2
+          and os.environ.get("PT_BENCH_NATIVE", "1") != "0"):
+        # the emulated root on the native loop: a 1-rank communicator with the
+        # N-way partition; the other ranks' slots arrive as a device copy of
+        # the same bytes on the high-priority stream (pt_dist_init, emulation)
+        r.dist_init(ptamd.Renderer.dist_unique_id(), 1, 0)
+        frames_t = torch.empty((2, H, W, 4), dtype=torch.float32, device=dev)
+        native = {"frames": frames_t, "outs": [frames_t[0], frames_t[1]], "emulated": True}
 
     def run_steps(k):
         if native is not None:
-            r.dist_run(SPP, k, native["frames"].data_ptr(), 2)
+            r.dist_run(SPP, k, native["frames"].data_ptr(), 2, n_streams=min(2, args.streams))
         else:
             for _ in range(k):
                 step()
 
+    if native is not None and os.environ.get("PT_BENCH_NATIVE_TORCH_STREAMS", "1") == "1":
+        # the native loop on torch's streams (the Python step's, whose frames
+        # measured to overlap), the gather on a high-priority one
+        gs = torch.cuda.Stream(dev, priority=-1)
+        native["gather_stream"] = gs
+        r.dist_set_streams(streams[0].cuda_stream, streams[-1].cuda_stream, gs.cuda_stream)
+    if native is not None:
+        # an event pair around every 4th launch: the native loop's host cost is
+        # a handful of HIP calls per frame, and each event record is one of them
+        args.timing_every = max(args.timing_every, 4)
+        r.set_option(ptamd.PT_OPT_LAUNCH_TIMING, args.timing_every)
     run_steps(args.warmup)
     drain()
+    if native is not None and native.get("emulated"):
+        ingest = {"bytes": 4 * (emu - 1) * r.dist_slot_floats()}
     r.synchronize()
     torch.cuda.synchronize(dev)
     if dist is not None:

@@ -282,14 +282,17 @@ int cull_rects(const float cam[16], int W, int H, const float* lo, const float* 
 // Native multi-GPU step loop state (pt_dist_*): an RCCL communicator of its
 // own, a high-priority stream for the gathers, two render streams (frames
 // alternate), and double-buffered send / receive slots.
+constexpr int kDistSets = 4;   // frame k uses buffer set k % 4 (see pt_dist_run)
 struct DistState {
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0;
   hipStream_t comm_stream = nullptr;
   hipStream_t streams[2] = {nullptr, nullptr};
-  hipEvent_t render_done[2] = {nullptr, nullptr}, gather_done[2] = {nullptr, nullptr};
-  float* send[2] = {nullptr, nullptr};
-  float* recv[2] = {nullptr, nullptr};   // root: nranks slots each
+  hipStream_t own[3] = {nullptr, nullptr, nullptr};   // created here (pt_dist_set_streams may override)
+  hipEvent_t render_done[kDistSets] = {}, gather_done[kDistSets] = {};
+  float* send[2] = {nullptr, nullptr};   // non-root ranks: frame k's live items (k % 2)
+  float* recv[kDistSets] = {};           // root: one slot per rank of the partition; slot 0 its own
+  float* ingest = nullptr;               // emulated root: stand-in for the other ranks' slots
   size_t slot_floats = 0, cap_floats = 0;
   std::vector<float> layout_key;         // frame_key of the layout the slots were sized for
   bool ready = false;
@@ -401,6 +404,7 @@ struct pt_context {
   long long launch_n = 0;     // render launches since pt_reset_launch_times
   long long ring_launch[kRing] = {};   // launch number of each recorded pair
   DistState* dist = nullptr;           // pt_dist_init
+  bool in_dist = false;                // inside pt_dist_run: it records the use events itself
 };
 
 struct pt_scene {
@@ -877,7 +881,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   if (shared) {
     const int rm = mark_shared(c);
     if (rm) return rm;
-  } else {
+  } else if (!c->in_dist) {
     const int ru = note_use(c);   // render_packed reads the scene and item tables
     if (ru) return ru;
   }
@@ -2007,21 +2011,25 @@ int dist_layout(pt_context* c) {
     live_max = std::max(live_max, live.size());
   }
   const size_t slot = std::max<size_t>(4, live_max * (size_t)(256 / c->last.spl) * 4);
+  const size_t nslots = (size_t)c->nranks;   // the partition's ranks (emulation: > d->nranks)
   if (slot > d->cap_floats) {
     for (int b = 0; b < 2; ++b)
       for (hipStream_t s : {d->streams[b], d->comm_stream}) PT_HIP(hipStreamSynchronize(s));
-    for (int b = 0; b < 2; ++b) {
-      dev_free(d->send[b]);
-      dev_free(d->recv[b]);
-    }
+    for (int b = 0; b < 2; ++b) dev_free(d->send[b]);
+    for (int b = 0; b < kDistSets; ++b) dev_free(d->recv[b]);
+    dev_free(d->ingest);
     d->cap_floats = 0;
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < 2 && d->rank != 0; ++b) {
       PT_HIP(hipMalloc((void**)&d->send[b], slot * sizeof(float)));
       PT_HIP(hipMemset(d->send[b], 0, slot * sizeof(float)));
-      if (d->rank == 0) {
-        PT_HIP(hipMalloc((void**)&d->recv[b], (size_t)d->nranks * slot * sizeof(float)));
-        PT_HIP(hipMemset(d->recv[b], 0, (size_t)d->nranks * slot * sizeof(float)));
-      }
+    }
+    for (int b = 0; b < kDistSets && d->rank == 0; ++b) {
+      PT_HIP(hipMalloc((void**)&d->recv[b], nslots * slot * sizeof(float)));
+      PT_HIP(hipMemset(d->recv[b], 0, nslots * slot * sizeof(float)));
+    }
+    if (d->nranks == 1 && nslots > 1) {
+      PT_HIP(hipMalloc((void**)&d->ingest, (nslots - 1) * slot * sizeof(float)));
+      PT_HIP(hipMemset(d->ingest, 0, (nslots - 1) * slot * sizeof(float)));
     }
     d->cap_floats = slot;
   }
@@ -2045,7 +2053,8 @@ int pt_dist_unique_id(void* id, size_t id_bytes) {
 
 int pt_dist_init(pt_context* c, const void* id, int nranks, int rank) {
   if (!c || !id) return fail(PT_ERR_INVALID, "null argument");
-  if (nranks != c->nranks || rank != c->rank)
+  const bool emulated = nranks == 1 && rank == 0 && c->rank == 0 && c->nranks > 1;
+  if (!emulated && (nranks != c->nranks || rank != c->rank))
     return fail(PT_ERR_INVALID, "pt_dist_init: set the same partition first (pt_set_partition / _slots)");
   const RcclApi* R = rccl_api();
   if (!R) return fail(PT_ERR_UNSUPPORTED, "RCCL (librccl.so.1) could not be loaded");
@@ -2057,9 +2066,12 @@ int pt_dist_init(pt_context* c, const void* id, int nranks, int rank) {
   d->rank = rank;
   int lo = 0, hi = 0;
   PT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  PT_HIP(hipStreamCreateWithPriority(&d->comm_stream, hipStreamNonBlocking, hi));   // gathers take CUs first
-  for (int b = 0; b < 2; ++b) {
-    PT_HIP(hipStreamCreateWithFlags(&d->streams[b], hipStreamNonBlocking));
+  PT_HIP(hipStreamCreateWithPriority(&d->own[2], hipStreamNonBlocking, hi));   // gathers take CUs first
+  for (int b = 0; b < 2; ++b) PT_HIP(hipStreamCreateWithFlags(&d->own[b], hipStreamNonBlocking));
+  d->streams[0] = d->own[0];
+  d->streams[1] = d->own[1];
+  d->comm_stream = d->own[2];
+  for (int b = 0; b < kDistSets; ++b) {
     PT_HIP(hipEventCreateWithFlags(&d->render_done[b], hipEventDisableTiming));
     PT_HIP(hipEventCreateWithFlags(&d->gather_done[b], hipEventDisableTiming));
   }
@@ -2070,14 +2082,17 @@ int pt_dist_init(pt_context* c, const void* id, int nranks, int rank) {
   return PT_OK;
 }
 
-int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, void* frames, int n_frame_bufs) {
+int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, void* frames, int n_frame_bufs) {
   if (!c) return fail(PT_ERR_INVALID, "null context");
   DistState* d = c->dist;
   if (!d || !d->ready) return fail(PT_ERR_INVALID, "pt_dist_run: no communicator (pt_dist_init)");
   if (n_frames < 0 || n_batches == 0) return fail(PT_ERR_INVALID, "pt_dist_run: bad frame or batch count");
   if (d->rank == 0 && (!frames || n_frame_bufs < 1 || (((uintptr_t)frames) & 15)))
     return fail(PT_ERR_INVALID, "pt_dist_run: the root needs 16-B aligned frame buffers");
-  if (d->nranks != c->nranks || d->rank != c->rank) return fail(PT_ERR_INVALID, "partition changed since pt_dist_init");
+  if (n_streams != 1 && n_streams != 2) return fail(PT_ERR_INVALID, "pt_dist_run: 1 or 2 streams");
+  const bool emulated = d->nranks == 1 && c->nranks > 1;
+  if ((d->nranks != c->nranks && !emulated) || d->rank != c->rank)
+    return fail(PT_ERR_INVALID, "partition changed since pt_dist_init");
   if (!c->last_valid) return fail(PT_ERR_INVALID, "pt_dist_run: render one frame with pt_render first (item layout)");
   const RcclApi* R = rccl_api();
   PT_HIP(hipSetDevice(c->device));
@@ -2089,50 +2104,78 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, void* frames, i
   const size_t frame_f = (size_t)c->width * c->height * 4;
   hipStream_t saved = c->stream;
   int rc = PT_OK;
-  // frame k: stream and buffer set k % 2.  Frame k's launch (pt_render_packed)
-  // also assembles frame k-2 on the root, whose gather ran during frame k-1;
-  // frame k's own gather overwrites that receive set after the launch that
-  // read it.  Frame k first waits for the gather of frame k-2, which read the
-  // send slot it is about to overwrite.
+  // Frame k runs on stream k % 2 (or the one stream) with buffer set k % 4.
+  // Its launch (pt_render_packed) writes this rank's live items -- on the root
+  // straight into its own slot of receive set k % 4, elsewhere into send
+  // slot k % 2 -- and, on the root, assembles frame k-2 from receive set
+  // (k-2) % 4, after waiting for that frame's gather.  Hazards: the gather of
+  // frame k (comm stream, after frame k's launch) overwrites set k % 4, which
+  // frame k-2's launch read -- earlier on frame k's own stream; a send slot
+  // is read by the gather of frame k-2, which frame k's launch waits for.
+  c->in_dist = true;
   for (int k = 0; k < n_frames && rc == PT_OK; ++k) {
-    const int b = k & 1;
-    c->stream = d->streams[b];
+    const int b = k % kDistSets;
+    c->stream = d->streams[n_streams == 2 ? (k & 1) : 0];
     Assembly as;
     if (k >= 2) {
-      PT_HIP(hipStreamWaitEvent(c->stream, d->gather_done[b], 0));
+      const int pb = (k - 2) % kDistSets;
+      PT_HIP(hipStreamWaitEvent(c->stream, d->gather_done[pb], 0));
       if (d->rank == 0) {
-        as.src = d->recv[b];
+        as.src = d->recv[pb];
         as.slot_floats = slot;
         as.frame = (float*)frames + (size_t)((k - 2) % n_frame_bufs) * frame_f;
       }
     }
-    rc = render_impl(c, 0, n_batches, (float4*)d->send[b], as);
+    rc = render_impl(c, 0, n_batches, (float4*)(d->rank == 0 ? d->recv[b] : d->send[k & 1]), as);
     if (rc) break;
     PT_HIP(hipEventRecord(d->render_done[b], c->stream));
     PT_HIP(hipStreamWaitEvent(d->comm_stream, d->render_done[b], 0));
-    PT_NCCL(R->GroupStart());
-    if (d->rank == 0)
-      for (int r = 0; r < d->nranks; ++r) PT_NCCL(R->Recv(d->recv[b] + (size_t)r * slot, slot, ncclFloat32, r, d->comm, d->comm_stream));
-    PT_NCCL(R->Send(d->send[b], slot, ncclFloat32, 0, d->comm, d->comm_stream));
-    PT_NCCL(R->GroupEnd());
+    if (emulated)   // the other ranks' slots: the bytes a real gather would write here
+      PT_HIP(hipMemcpyAsync(d->recv[b] + slot, d->ingest, (size_t)(c->nranks - 1) * slot * sizeof(float),
+                            hipMemcpyDeviceToDevice, d->comm_stream));
+    if (d->nranks > 1) {
+      PT_NCCL(R->GroupStart());
+      if (d->rank == 0)
+        for (int r = 1; r < d->nranks; ++r)
+          PT_NCCL(R->Recv(d->recv[b] + (size_t)r * slot, slot, ncclFloat32, r, d->comm, d->comm_stream));
+      else
+        PT_NCCL(R->Send(d->send[k & 1], slot, ncclFloat32, 0, d->comm, d->comm_stream));
+      PT_NCCL(R->GroupEnd());
+    }
     PT_HIP(hipEventRecord(d->gather_done[b], d->comm_stream));
   }
+  c->in_dist = false;
   // the root assembles the last (up to) two frames in launches of their own
   if (rc == PT_OK && d->rank == 0) {
     frame_key(c, c->last, &c->key_scratch);
     rc = unpack_table(c, c->last, c->key_scratch);
     for (int k = std::max(0, n_frames - 2); k < n_frames && rc == PT_OK; ++k) {
-      const int b = k & 1;
-      c->stream = d->streams[b];
+      const int b = k % kDistSets;
+      c->stream = d->streams[n_streams == 2 ? (k & 1) : 0];
       PT_HIP(hipStreamWaitEvent(c->stream, d->gather_done[b], 0));
       float4* out = (float4*)((float*)frames + (size_t)(k % n_frame_bufs) * frame_f);
       PT_HIP(ptd::launch_items_unpack(c->last, out, (const float4*)d->recv[b], slot / 4, c->d_unpack, c->n_unpack,
                                       c->stream));
-      rc = note_use(c);
     }
+  }
+  // one use event per stream for the whole run (the launches above skip theirs)
+  for (int sidx = 0; sidx < n_streams && rc == PT_OK; ++sidx) {
+    c->stream = d->streams[sidx];
+    rc = note_use(c);
   }
   c->stream = saved;
   return rc;
+}
+
+int pt_dist_set_streams(pt_context* c, void* render0, void* render1, void* comm) {
+  if (!c || !c->dist) return fail(PT_ERR_INVALID, "pt_dist_set_streams: no communicator (pt_dist_init)");
+  DistState* d = c->dist;
+  PT_HIP(hipSetDevice(c->device));
+  for (hipStream_t s : {d->streams[0], d->streams[1], d->comm_stream}) PT_HIP(hipStreamSynchronize(s));
+  d->streams[0] = render0 ? (hipStream_t)render0 : d->own[0];
+  d->streams[1] = render1 ? (hipStream_t)render1 : d->own[1];
+  d->comm_stream = comm ? (hipStream_t)comm : d->own[2];
+  return PT_OK;
 }
 
 int pt_dist_slot_floats(pt_context* c, size_t* slot_floats) {
@@ -2151,14 +2194,15 @@ int pt_dist_finalize(pt_context* c) {
     if (s) (void)hipStreamSynchronize(s);
   const RcclApi* R = rccl_api();
   if (d->comm && R) (void)R->CommDestroy(d->comm);
-  for (int b = 0; b < 2; ++b) {
-    dev_free(d->send[b]);
+  dev_free(d->ingest);
+  for (int b = 0; b < 2; ++b) dev_free(d->send[b]);
+  for (hipStream_t s : d->own)
+    if (s) (void)hipStreamDestroy(s);
+  for (int b = 0; b < kDistSets; ++b) {
     dev_free(d->recv[b]);
     if (d->render_done[b]) (void)hipEventDestroy(d->render_done[b]);
     if (d->gather_done[b]) (void)hipEventDestroy(d->gather_done[b]);
-    if (d->streams[b]) (void)hipStreamDestroy(d->streams[b]);
   }
-  if (d->comm_stream) (void)hipStreamDestroy(d->comm_stream);
   delete d;
   c->dist = nullptr;
   return PT_OK;

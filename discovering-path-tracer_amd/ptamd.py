@@ -43,6 +43,7 @@ EXPORTS = [
     "pt_items_live", "pt_items_pack", "pt_items_unpack_all", "pt_render_packed", "pt_launch_span_ms",
     "pt_set_partition_slots", "pt_get_traced", "pt_partition_items",
     "pt_dist_unique_id", "pt_dist_init", "pt_dist_run", "pt_dist_slot_floats", "pt_dist_finalize",
+    "pt_dist_set_streams",
 ]
 
 
@@ -94,8 +95,8 @@ def lib():
             "pt_reset_stats": ([vp], i32), "pt_get_traced": ([vp, ctypes.POINTER(Traced)], i32),
             "pt_partition_items": ([i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, psz, vp, psz, vp], i32),
             "pt_dist_unique_id": ([vp, sz], i32), "pt_dist_init": ([vp, vp, i32, i32], i32),
-            "pt_dist_run": ([vp, u32, i32, vp, i32], i32), "pt_dist_slot_floats": ([vp, psz], i32),
-            "pt_dist_finalize": ([vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
+            "pt_dist_run": ([vp, u32, i32, i32, vp, i32], i32), "pt_dist_slot_floats": ([vp, psz], i32),
+            "pt_dist_finalize": ([vp], i32), "pt_dist_set_streams": ([vp, vp, vp, vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
             "pt_launch_times_ms": ([vp, vp, sz, psz], i32), "pt_reset_launch_times": ([vp], i32),
             "pt_launch_span_ms": ([vp, ctypes.POINTER(ctypes.c_float), psz], i32),
             "pt_selftest_math": ([i32, i32, vp, vp, sz], i32),
@@ -477,8 +478,11 @@ class Renderer:
         b = (ctypes.c_char * 128).from_buffer_copy(uid)
         _check(lib().pt_dist_init(self._c, b, nranks, rank), "pt_dist_init")
 
-    def dist_run(self, n_batches, n_frames, frames_ptr=None, n_frame_bufs=1):
-        _check(lib().pt_dist_run(self._c, n_batches, n_frames, frames_ptr, n_frame_bufs), "pt_dist_run")
+    def dist_run(self, n_batches, n_frames, frames_ptr=None, n_frame_bufs=1, n_streams=2):
+        _check(lib().pt_dist_run(self._c, n_batches, n_frames, n_streams, frames_ptr, n_frame_bufs), "pt_dist_run")
+
+    def dist_set_streams(self, render0=None, render1=None, gather=None):
+        _check(lib().pt_dist_set_streams(self._c, render0, render1, gather), "pt_dist_set_streams")
 
     def dist_slot_floats(self):
         n = ctypes.c_size_t(0)
