@@ -318,6 +318,11 @@ def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light,
         r.dist_init(bytes(t[1:].cpu().tolist()), world, rank)
         frames = torch.full((2, H, W, 4), float("nan"), dtype=torch.float32, device=dev)
         r.dist_run(spp, 4, frames.data_ptr(), 2, n_streams=1)
+        try:
+            r.dist_wait(30000)   # a hung gather must not hang the bench: abort and fall back
+        except ptamd.PTError:
+            r.dist_abort()
+            raise
         r.synchronize()
         if rank == 0:
             ref = ptamd.Renderer(dev.index)
@@ -340,7 +345,7 @@ def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light,
     if int(flag.item()) == 0:
         print("bench: native step loop failed its self-check; using the Python step", file=sys.stderr, flush=True)
         try:
-            r.dist_finalize()
+            r.dist_abort()
         except ptamd.PTError:
             pass
         return None

@@ -14,7 +14,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/pathtracer.h"
@@ -1960,6 +1962,7 @@ struct RcclApi {
   ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
   ncclResult_t (*GroupEnd)() = nullptr;
   ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
@@ -1980,12 +1983,13 @@ const RcclApi* rccl_api() {
       api.GetUniqueId = (decltype(api.GetUniqueId))dlsym(h, "ncclGetUniqueId");
       api.CommInitRank = (decltype(api.CommInitRank))dlsym(h, "ncclCommInitRank");
       api.CommDestroy = (decltype(api.CommDestroy))dlsym(h, "ncclCommDestroy");
+      api.CommAbort = (decltype(api.CommAbort))dlsym(h, "ncclCommAbort");
       api.GroupStart = (decltype(api.GroupStart))dlsym(h, "ncclGroupStart");
       api.GroupEnd = (decltype(api.GroupEnd))dlsym(h, "ncclGroupEnd");
       api.Send = (decltype(api.Send))dlsym(h, "ncclSend");
       api.Recv = (decltype(api.Recv))dlsym(h, "ncclRecv");
       api.GetErrorString = (decltype(api.GetErrorString))dlsym(h, "ncclGetErrorString");
-      if (api.GetUniqueId && api.CommInitRank && api.CommDestroy && api.GroupStart && api.GroupEnd && api.Send &&
+      if (api.GetUniqueId && api.CommInitRank && api.CommDestroy && api.CommAbort && api.GroupStart && api.GroupEnd && api.Send &&
           api.Recv && api.GetErrorString)
         api.h = h;
     }
@@ -2183,6 +2187,33 @@ int pt_dist_slot_floats(pt_context* c, size_t* slot_floats) {
   if (!c->dist || !c->dist->slot_floats) return fail(PT_ERR_INVALID, "no pt_dist_run yet");
   *slot_floats = c->dist->slot_floats;
   return PT_OK;
+}
+
+int pt_dist_wait(pt_context* c, int timeout_ms) {
+  if (!c || !c->dist) return fail(PT_ERR_INVALID, "pt_dist_wait: no communicator");
+  DistState* d = c->dist;
+  PT_HIP(hipSetDevice(c->device));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    bool done = true;
+    for (hipStream_t s : {d->streams[0], d->streams[1], d->comm_stream}) {
+      const hipError_t q = hipStreamQuery(s);
+      if (q == hipErrorNotReady) done = false;
+      else if (q != hipSuccess) return fail(PT_ERR_HIP, std::string("pt_dist_wait: ") + hipGetErrorString(q));
+    }
+    if (done) return PT_OK;
+    const long long ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (timeout_ms >= 0 && ms > timeout_ms) return fail(PT_ERR_HIP, "pt_dist_wait: timed out (gather not complete)");
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+}
+
+int pt_dist_abort(pt_context* c) {
+  if (!c || !c->dist) return PT_OK;
+  const RcclApi* R = rccl_api();
+  if (c->dist->comm && R) (void)R->CommAbort(c->dist->comm);   // ends outstanding transfers
+  c->dist->comm = nullptr;
+  return pt_dist_finalize(c);
 }
 
 int pt_dist_finalize(pt_context* c) {

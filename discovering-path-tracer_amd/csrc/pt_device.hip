@@ -102,6 +102,9 @@ __device__ __forceinline__ bool tri_test(v3 o, v3 d, float4 A, float4 B, float4 
 #ifndef PT_WF_WAVEFLUSH
 #define PT_WF_WAVEFLUSH 1   // wf_trace_kernel: wave-wide candidate flush (see there)
 #endif
+#ifndef PT_WF_SORT
+#define PT_WF_SORT 0   // wf_shade_kernel: bin each workgroup's next rays by kind and octant (see there)
+#endif
 #ifndef PT_WF_SHADOW_QUEUE
 #define PT_WF_SHADOW_QUEUE 1   // wf_trace_kernel: shadow rays queue their leaves too (see there)
 #endif
@@ -1908,10 +1911,23 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
 
 // Shading of every path in list `cur` (path_step on the returned hit);
 // paths that need another ray go to list cur^1, finished ones store colour.
+//
+// PT_WF_SORT: a workgroup appends its next rays binned by kind (closest-hit
+// / shadow) and direction octant -- one atomic per workgroup, a counting sort
+// in LDS -- so the traversal kernel's waves, which take consecutive list
+// slots, get rays of one kind heading the same way: fewer divergent branches
+// and more shared nodes per wave.  A ray's result does not depend on where
+// it sits in the list, so the image is unchanged.  Measured at 1080p 8 spp:
+// sphere -0.5 %, 1M cloud +0.5 %, 10M cloud +3.5 % -- off by default.
+__device__ __forceinline__ int ray_bin(const Trav& T) {
+  const int oct = (T.d.x < 0.0f ? 1 : 0) | (T.d.y < 0.0f ? 2 : 0) | (T.d.z < 0.0f ? 4 : 0);
+  return (T.shadow ? 8 : 0) | oct;
+}
 __global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers B, int cur) {
   if (blockIdx.x == 0 && threadIdx.x == 0) B.counters[2] = 0;   // the next traversal's cursor
   const int count = B.counters[cur];
   CamFrame F = {};   // camera frame: used by PH_BEGIN only
+  __shared__ int bin_cnt[16], bin_base[16], wg_base;
   for (int base = (int)blockIdx.x * 256; base < count; base += (int)gridDim.x * 256) {
     const int i = base + (int)threadIdx.x;
     bool need = false;
@@ -1938,8 +1954,28 @@ __global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers
       else
         B.colors[p] = make_float4(col.x, col.y, col.z, 1.0f);
     }
-    const int slot = wave_slot(&B.counters[cur ^ 1], need);
-    if (need) wf_push(B, cur ^ 1, slot, p, T);
+    if (PT_WF_SORT) {   // uniform: every thread of the workgroup runs each iteration
+      const int tid = (int)threadIdx.x;
+      if (tid < 16) bin_cnt[tid] = 0;
+      __syncthreads();
+      const int bin = need ? ray_bin(T) : 0;
+      const int rank = need ? atomicAdd(&bin_cnt[bin], 1) : 0;
+      __syncthreads();
+      if (tid == 0) {
+        int acc = 0;
+        for (int k = 0; k < 16; ++k) {
+          bin_base[k] = acc;
+          acc += bin_cnt[k];
+        }
+        wg_base = acc ? atomicAdd(&B.counters[cur ^ 1], acc) : 0;
+      }
+      __syncthreads();
+      if (need) wf_push(B, cur ^ 1, wg_base + bin_base[bin] + rank, p, T);
+      __syncthreads();   // the bins are reused by the next iteration
+    } else {
+      const int slot = wave_slot(&B.counters[cur ^ 1], need);
+      if (need) wf_push(B, cur ^ 1, slot, p, T);
+    }
   }
 }
 

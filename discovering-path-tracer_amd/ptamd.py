@@ -43,7 +43,7 @@ EXPORTS = [
     "pt_items_live", "pt_items_pack", "pt_items_unpack_all", "pt_render_packed", "pt_launch_span_ms",
     "pt_set_partition_slots", "pt_get_traced", "pt_partition_items",
     "pt_dist_unique_id", "pt_dist_init", "pt_dist_run", "pt_dist_slot_floats", "pt_dist_finalize",
-    "pt_dist_set_streams",
+    "pt_dist_set_streams", "pt_dist_wait", "pt_dist_abort",
 ]
 
 
@@ -96,7 +96,8 @@ def lib():
             "pt_partition_items": ([i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, psz, vp, psz, vp], i32),
             "pt_dist_unique_id": ([vp, sz], i32), "pt_dist_init": ([vp, vp, i32, i32], i32),
             "pt_dist_run": ([vp, u32, i32, i32, vp, i32], i32), "pt_dist_slot_floats": ([vp, psz], i32),
-            "pt_dist_finalize": ([vp], i32), "pt_dist_set_streams": ([vp, vp, vp, vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
+            "pt_dist_finalize": ([vp], i32), "pt_dist_set_streams": ([vp, vp, vp, vp], i32),
+            "pt_dist_wait": ([vp, i32], i32), "pt_dist_abort": ([vp], i32), "pt_last_launch_ms": ([vp, ctypes.POINTER(ctypes.c_float)], i32),
             "pt_launch_times_ms": ([vp, vp, sz, psz], i32), "pt_reset_launch_times": ([vp], i32),
             "pt_launch_span_ms": ([vp, ctypes.POINTER(ctypes.c_float), psz], i32),
             "pt_selftest_math": ([i32, i32, vp, vp, sz], i32),
@@ -488,6 +489,12 @@ class Renderer:
         n = ctypes.c_size_t(0)
         _check(lib().pt_dist_slot_floats(self._c, ctypes.byref(n)), "pt_dist_slot_floats")
         return n.value
+
+    def dist_wait(self, timeout_ms):
+        _check(lib().pt_dist_wait(self._c, timeout_ms), "pt_dist_wait")
+
+    def dist_abort(self):
+        _check(lib().pt_dist_abort(self._c), "pt_dist_abort")
 
     def dist_finalize(self):
         _check(lib().pt_dist_finalize(self._c), "pt_dist_finalize")

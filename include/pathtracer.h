@@ -258,6 +258,10 @@ int pt_dist_run(pt_context* ctx, uint32_t n_batches, int n_frames, int n_streams
  * which ones overlap. */
 int pt_dist_set_streams(pt_context* ctx, void* render_stream0, void* render_stream1, void* gather_stream);
 int pt_dist_slot_floats(pt_context* ctx, size_t* slot_floats);
+/* Wait (polling) up to timeout_ms for the loop's streams; PT_ERR_HIP on
+ * timeout.  pt_dist_abort: ncclCommAbort + free, after such a timeout. */
+int pt_dist_wait(pt_context* ctx, int timeout_ms);
+int pt_dist_abort(pt_context* ctx);
 int pt_dist_finalize(pt_context* ctx);
 
 /* ---- kernel options ---------------------------------------------------- */
