@@ -159,6 +159,60 @@ void collapse_implied(const std::vector<float4>& full, std::vector<float4>* out)
   }
 }
 
+// Child-pair records (pt_device.h): one 64-B record per internal node in DFS
+// order, right child first, plus record 0, a virtual parent of the root.
+// Links are validated by thread_bvh first.  *depth = the tree's depth.
+void build_pairs(const pt_bvh_node* nodes, size_t n, bool int_bits, std::vector<float4>* out, int* depth) {
+  auto link = [&](int32_t i, int which) {
+    const float f = which ? nodes[i].max_bounds[3] : nodes[i].min_bounds[3];
+    int32_t v;
+    if (int_bits) memcpy(&v, &f, 4);
+    else v = (int32_t)f;
+    return v;
+  };
+  auto is_leaf = [&](int32_t i) { return link(i, 0) == -1; };
+  std::vector<int32_t> rec(n, -1), order;
+  std::vector<std::pair<int32_t, int>> st{{0, 1}};
+  int maxd = 0;
+  int32_t next = 1;
+  while (!st.empty()) {
+    const auto [v, d] = st.back();
+    st.pop_back();
+    maxd = std::max(maxd, d);
+    if (is_leaf(v)) continue;
+    rec[v] = next++;
+    order.push_back(v);
+    st.push_back({link(v, 0), d + 1});   // left, walked second
+    st.push_back({link(v, 1), d + 1});   // right, walked first
+  }
+  auto child_link = [&](int32_t ch) { return is_leaf(ch) ? ~link(ch, 1) : rec[ch]; };
+  auto same = [&](int32_t a, int32_t b) {
+    return memcmp(nodes[a].min_bounds, nodes[b].min_bounds, 12) == 0 &&
+           memcmp(nodes[a].max_bounds, nodes[b].max_bounds, 12) == 0;
+  };
+  auto bits = [](int32_t v) { float f; memcpy(&f, &v, 4); return f; };
+  out->assign(4 * (size_t)next, make_float4(0, 0, 0, 0));
+  auto put = [&](size_t r, int32_t R, int32_t L, int32_t flags) {
+    const pt_bvh_node& a = nodes[R];
+    (*out)[4 * r + 0] = make_float4(a.min_bounds[0], a.min_bounds[1], a.min_bounds[2], bits(child_link(R)));
+    if (L >= 0) {
+      const pt_bvh_node& b = nodes[L];
+      (*out)[4 * r + 1] = make_float4(a.max_bounds[0], a.max_bounds[1], a.max_bounds[2], bits(child_link(L)));
+      (*out)[4 * r + 2] = make_float4(b.min_bounds[0], b.min_bounds[1], b.min_bounds[2], bits(flags));
+      (*out)[4 * r + 3] = make_float4(b.max_bounds[0], b.max_bounds[1], b.max_bounds[2], 0.0f);
+    } else {
+      (*out)[4 * r + 1] = make_float4(a.max_bounds[0], a.max_bounds[1], a.max_bounds[2], bits(-1));
+      (*out)[4 * r + 2] = make_float4(0.0f, 0.0f, 0.0f, bits(flags | 4));
+    }
+  };
+  put(0, 0, -1, 0);   // virtual parent: the root is tested like any node
+  for (int32_t v : order) {
+    const int32_t R = link(v, 1), L = link(v, 0);
+    put((size_t)rec[v], R, L, (same(R, v) ? 1 : 0) | (same(L, v) ? 2 : 0));
+  }
+  *depth = maxd;
+}
+
 // ---- primary-ray bundle culling -----------------------------
 // Camera model of raytrace_comp.comp:430-460 in the orthonormal camera frame
 // (right, up, ez = dir/|dir|) centred on the camera position, with the
@@ -307,6 +361,8 @@ struct pt_context {
   float4* d_nodes = nullptr;        // threaded, implied internal nodes collapsed (fast kernel)
   int n_nodes = 0;
   float4* d_nodes_full = nullptr;   // threaded, every reference node (stats mode)
+  float4* d_pairs = nullptr;        // child-pair records (wavefront walk of device-memory scenes)
+  int pair_depth = 0;               // tree depth (the pair walk's stack holds at most this)
   int n_nodes_full = 0;
   float4* d_tris = nullptr;
   int n_tris = 0;
@@ -339,6 +395,7 @@ struct pt_context {
   int opt_cull = 1;           // PT_OPT_PRIMARY_CULL
   int opt_wf_paths = 0;       // PT_OPT_WF_PATHS (0 = 2^24)
   int opt_count = 0;          // PT_OPT_COUNT_TRACED
+  int opt_pairs = 0;          // PT_OPT_PAIRS
   int last_kernel = 0;        // kernel of the last render (1 recursive, 2 state machine, 3 wavefront)
   // compact-launch item lists (live items, then culled ones), rebuilt when
   // the frame, partition, sample lanes or cull rectangles change
@@ -712,6 +769,8 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   if (!c->has_camera) return fail(PT_ERR_INVALID, "no camera set");
   if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
   ptd::RenderParams p;
+  p.pairs = nullptr;   // set below for the wavefront walk
+  p.pair_depth = 0;
   p.nodes = c->stats_mode ? c->d_nodes_full : c->d_nodes;
   p.tris = c->d_tris;
   p.lights = c->d_lights_dev;
@@ -876,6 +935,10 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     if (rc) return rc;
     ptd::WfBuffers b = c->wf;
     b.cap = chunk_paths;   // paths per chunk (the allocation may be larger)
+    if (c->opt_pairs && c->d_pairs && c->pair_depth <= 32) {
+      p.pairs = c->d_pairs;
+      p.pair_depth = std::max(1, c->pair_depth);
+    }
     PT_HIP(ptd::launch_wavefront(p, b, lds, c->stream, cnt));
   } else {
     PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream, cnt));
@@ -949,6 +1012,7 @@ int pt_destroy(pt_context* c) {
   c->uses.clear();
   dev_free(c->d_nodes);
   dev_free(c->d_nodes_full);
+  dev_free(c->d_pairs);
   dev_free(c->d_tris);
   dev_free(c->d_lights);
   dev_free(c->d_lights_dev);
@@ -1011,12 +1075,16 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   int rc = thread_bvh(nodes, n_nodes, (flags & PT_NODES_INT_BITS) != 0, n_indices / 3, &threaded);
   if (rc) return rc;
   collapse_implied(threaded, &collapsed);
+  std::vector<float4> pairs;
+  int pair_depth = 0;
+  build_pairs(nodes, n_nodes, (flags & PT_NODES_INT_BITS) != 0, &pairs, &pair_depth);
   float lo[3] = {threaded[0].x, threaded[0].y, threaded[0].z};   // node 0 is the root
   float hi[3] = {threaded[1].x, threaded[1].y, threaded[1].z};
   PT_HIP(hipSetDevice(c->device));
   { const int rc_ = quiesce(c); if (rc_) return rc_; }
   dev_free(c->d_nodes);
   dev_free(c->d_nodes_full);
+  dev_free(c->d_pairs);
   dev_free(c->d_tris);
   c->has_scene = false;
   const int T = (int)(n_indices / 3);
@@ -1034,6 +1102,8 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   PT_HIP(hipMalloc((void**)&c->d_nodes, collapsed.size() * sizeof(float4)));
   PT_HIP(hipMalloc((void**)&c->d_nodes_full, threaded.size() * sizeof(float4)));
   PT_HIP(hipMalloc((void**)&c->d_tris, (size_t)T * 3 * sizeof(float4)));
+  PT_HIP(hipMalloc((void**)&c->d_pairs, pairs.size() * sizeof(float4)));
+  PT_HIP(hipMemcpyAsync(c->d_pairs, pairs.data(), pairs.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
   PT_HIP(hipMalloc((void**)&st.v, n_vertex_floats * sizeof(float) + 16));
   PT_HIP(hipMalloc((void**)&st.i, n_indices * sizeof(uint32_t)));
   PT_HIP(hipMemcpyAsync(c->d_nodes, collapsed.data(), collapsed.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
@@ -1044,6 +1114,7 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   PT_HIP(hipStreamSynchronize(c->stream));
   c->n_nodes = (int)(collapsed.size() / 2) - 1;
   c->n_nodes_full = (int)(threaded.size() / 2) - 1;
+  c->pair_depth = pair_depth;
   c->n_tris = T;
   memcpy(c->root_lo, lo, sizeof lo);
   memcpy(c->root_hi, hi, sizeof hi);
@@ -1309,6 +1380,10 @@ int pt_set_option(pt_context* c, int key, int value) {
     case PT_OPT_KERNEL:
       if (value < 0 || value > 3) return fail(PT_ERR_INVALID, "PT_OPT_KERNEL takes 0, 1, 2 or 3");
       c->opt_kernel = value;
+      return PT_OK;
+    case PT_OPT_PAIRS:
+      if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_PAIRS takes 0 or 1");
+      c->opt_pairs = value;
       return PT_OK;
     case PT_OPT_COUNT_TRACED:
       if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_COUNT_TRACED takes 0 or 1");

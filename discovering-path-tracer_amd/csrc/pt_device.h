@@ -74,7 +74,16 @@ __host__ __device__ inline bool part_owns(const Part& p, int b) {
   return own;
 }
 
+// Child-pair record (wavefront traversal of device-memory scenes): one per
+// internal node, in DFS order (right child first), 64 B:
+//   [0] = {R.min.xyz, R link}   [1] = {R.max.xyz, L link}
+//   [2] = {L.min.xyz, flags}    [3] = {L.max.xyz, 0}
+// link: the child's record index if internal, ~triangle slot if a leaf;
+// flags: 1 R implied hit, 2 L implied hit (bounds bitwise the parent's),
+// 4 L absent.  Record 0 is a virtual parent: R = the root, L absent.
 struct RenderParams {
+  const float4* pairs;      // child-pair records, or null (threaded walk)
+  int pair_depth;           // tree depth: entries of the pair walk's stack
   const float4* nodes;
   const float4* tris;
   const LightDev* lights;

@@ -1826,6 +1826,9 @@ constexpr unsigned long long group_lead() {
   return G == 1 ? ~0ull : G == 2 ? 0x5555555555555555ull : G == 4 ? 0x1111111111111111ull
                                     : G == 8 ? 0x0101010101010101ull : 0x0001000100010001ull;
 }
+#ifndef PT_WF_PAIR_MIN_BLOCKS
+#define PT_WF_PAIR_MIN_BLOCKS 7
+#endif
 #ifndef PT_WF_MIN_BLOCKS
 #define PT_WF_MIN_BLOCKS 7   // 72 VGPRs (11 spilled): sphere -7 %, 1M cloud -0.6 % vs 6; 8 spills 30 (+50 %)
 #endif
@@ -1900,6 +1903,168 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
           } else if (test_shadow_candidates(P, L.o, L.d, L.lim, cand, L.nc)) {
             L.res = 1;
             L.k = P.n_nodes;   // occluded: the walk ends (its next step reports it)
+          }
+          L.nc = 0;
+        }
+      }
+    }
+  }
+  if (CNT) flush_traced(P, c, lane);
+}
+
+// ---------------------------------------------------------------------------
+// Child-pair traversal for scenes in device memory (PT_OPT_PAIRS, off by
+// default: measured at 1080p 8 spp, sphere 234 -> 249 ms, 1M cloud 590 -> 574,
+// 10M cloud 2827 -> 3526; the stack's LDS cuts occupancy to 4-6 waves/SIMD
+// and L2 requests fell only 21 %, not the simulated half).
+//
+// The reference's exhaustive DFS tests both children of every internal node
+// whose box is hit (raytrace_comp.comp:196-200), so both child boxes are
+// stored together in one 64-B record per internal node (pt_device.h
+// PairRec): one fetch serves two box tests, where the threaded layout
+// fetched each child's 32-B node separately.  The right child is walked
+// first; a hit left child waits on a per-lane stack of pending subtrees and
+// hit leaves in that order, so the candidate sequence -- every hit leaf in
+// the reference's visit order -- and hence every result is the reference's.
+// Implied-hit children (bounds bitwise the parent's) skip their slab test.
+// Record 0 is a virtual parent whose right child is the root.
+// ---------------------------------------------------------------------------
+
+struct PairLane {
+  v3 o, d, inv;
+  int rec;     // record to fetch next, or -1: take the next pending entry
+  int sp;      // pending entries on the stack
+  int nc, res, shadow;
+  float lim;
+};
+
+__device__ __forceinline__ void pair_lane_start(const float4* __restrict__ ray, PairLane& L) {
+  const float4 r0 = ray[0], r1 = ray[1];
+  L.o = mk(r0.x, r0.y, r0.z);
+  L.d = mk(r1.x, r1.y, r1.z);
+  L.inv = mk(rcp_(L.d.x), rcp_(L.d.y), rcp_(L.d.z));
+  const int kind = __float_as_int(r1.w);   // 0 closest, 1 shadow, 2 null shadow (trav_null)
+  L.shadow = kind ? 1 : 0;
+  L.lim = L.shadow ? r0.w : 1e30f;
+  L.res = L.shadow ? 0 : -1;
+  L.rec = kind == 2 ? -1 : 0;
+  L.sp = 0;
+  L.nc = 0;
+}
+
+// One record (two box tests) and the pending entries it frees; true when the
+// walk is finished, with its remaining candidates tested.  Enqueues at most
+// two candidates before the pops, which stop when the queue is full: the
+// caller flushes wave-wide once a lane holds more than kCand - 2.
+template <bool CNT, int SS>
+__device__ __forceinline__ bool pair_step(const RenderParams& P, PairLane& L, int* stk, int* cand, Ctr& c) {
+  if (L.rec >= 0) {
+    const float4* rp = P.pairs + 4 * (size_t)L.rec;
+    const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
+    const int flags = __float_as_int(r2.w);
+    const bool hR = slab(L.o, L.inv, r0, r1) || (flags & 1);
+    const bool hL = (slab(L.o, L.inv, r2, r3) || (flags & 2)) && !(flags & 4);
+    if (CNT) c.nodes += (flags & 4) ? 1u : 2u;
+    const int lr = __float_as_int(r0.w), ll = __float_as_int(r1.w);
+    int next = -1;
+    if (hR) {
+      if (lr < 0) {
+        cand[L.nc * 64] = ~lr;
+        ++L.nc;
+      } else {
+        next = lr;
+      }
+    }
+    if (hL) {
+      if (next >= 0) {
+        stk[SS * L.sp++] = ll;   // after the right subtree (a leaf stays a leaf marker)
+      } else if (ll < 0) {
+        cand[L.nc * 64] = ~ll;
+        ++L.nc;
+      } else {
+        next = ll;
+      }
+    }
+    if (CNT) c.leaves += (hR && lr < 0 ? 1u : 0u) + (hL && ll < 0 ? 1u : 0u);
+    L.rec = next;
+  }
+  while (L.rec < 0 && L.sp > 0 && L.nc < kCand) {
+    const int e = stk[SS * --L.sp];
+    if (e < 0) {
+      cand[L.nc * 64] = ~e;
+      ++L.nc;
+    } else {
+      L.rec = e;
+    }
+  }
+  if (L.rec >= 0 || L.sp > 0) return false;
+  if (!L.shadow)
+    test_candidates(P, L.o, L.d, cand, L.nc, &L.lim, &L.res);
+  else if (L.nc > 0 && test_shadow_candidates(P, L.o, L.d, L.lim, cand, L.nc))
+    L.res = 1;
+  L.nc = 0;
+  return true;
+}
+
+template <int G, bool CNT = false>
+__global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_kernel(RenderParams P, WfBuffers B,
+                                                                                   int cur) {
+  const int tid = (int)threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0) B.counters[cur ^ 1] = 0;   // filled by the shading that follows
+  const int count = B.counters[cur];
+  if (count == 0) return;
+  const int wave = tid >> 6, lane = tid & 63;
+  __shared__ int cand_buf[4][kCand][64];
+  int* cand = &cand_buf[wave][0][lane];
+  // per-lane pending entries: in LDS, [depth][lane] per wave (P.pair_depth
+  // entries, sized by the host); private memory is written through to L2 on
+  // CDNA, and a stack there made every pop an L2 round trip
+  extern __shared__ int stk_lds[];
+  int* stk = stk_lds + wave * 64 * P.pair_depth + lane;
+  const float4* __restrict__ rays = B.rays[cur];
+  int p = -1;   // list slot this lane traces
+  bool more = true;
+  PairLane L;
+  L.rec = -1;
+  L.sp = 0;
+  L.nc = 0;
+  Ctr c = {0u, 0u, 0u, 0u, 0u};
+  for (;;) {
+    const unsigned long long idle = __ballot(p < 0);
+    unsigned long long gm = idle;
+#pragma unroll
+    for (int sh = 1; sh < G; sh <<= 1) gm &= gm >> sh;
+    gm &= group_lead<G>();
+    const int ng = (int)__popcll(gm);
+    if (more && ng * G >= PT_WF_REFILL) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&B.counters[2], ng * G);
+      base = __shfl(base, 0);
+      if (base + ng * G >= count) more = false;
+      const int lead = lane & ~(G - 1);
+      if ((gm >> lead) & 1ull) {
+        const int slot = base + (int)__popcll(gm & ((1ull << lead) - 1ull)) * G + (lane - lead);
+        if (slot < count) {
+          p = slot;
+          pair_lane_start(rays + 2 * (size_t)slot, L);
+          if (CNT) count_start(rays + 2 * (size_t)slot, c);
+        }
+      }
+    }
+    if (!more && __ballot(p >= 0) == 0ull) break;
+    for (int it = 0; it < PT_WF_STEPS; ++it) {
+      if (p >= 0 && pair_step<CNT, 64>(P, L, stk, cand, c)) {
+        B.hits[p] = make_float2(L.lim, __int_as_float(L.res));
+        p = -1;
+      }
+      if (__ballot(p >= 0 && L.nc > kCand - 2)) {   // wave-uniform flush
+        if (p >= 0 && L.nc > 0) {
+          if (!L.shadow) {
+            test_candidates(P, L.o, L.d, cand, L.nc, &L.lim, &L.res);
+          } else if (test_shadow_candidates(P, L.o, L.d, L.lim, cand, L.nc)) {
+            L.res = 1;
+            L.rec = -1;   // occluded: the walk ends (its next step reports it)
+            L.sp = 0;
           }
           L.nc = 0;
         }
@@ -2133,7 +2298,12 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
                        : (g2 ? wf_trace_kernel<false, 2, true> : wf_trace_kernel<false, 4, true>))
           : (lds_scene ? (g2 ? wf_trace_kernel<true, 2> : wf_trace_kernel<true, 4>)
                        : (g2 ? wf_trace_kernel<false, 2> : wf_trace_kernel<false, 4>));
-  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, trace, 256, lds);
+  if (p0.pairs && !lds_scene)   // child-pair records (PT_OPT_PAIRS)
+    trace = cnt ? (g2 ? wf_trace_pairs_kernel<2, true> : wf_trace_pairs_kernel<4, true>)
+                : (g2 ? wf_trace_pairs_kernel<2> : wf_trace_pairs_kernel<4>);
+  size_t lds_t = lds;
+  if (p0.pairs && !lds_scene) lds_t = (size_t)4 * 64 * p0.pair_depth * sizeof(int);   // the walk stacks
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, trace, 256, lds_t);
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, wf_shade_kernel, 256, 0);
   if (e != hipSuccess) return e;
   const unsigned grid_t = (unsigned)(cus * (per_cu_t > 0 ? per_cu_t : 1));
@@ -2153,7 +2323,7 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
       wf_gen_kernel<false><<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(p, b, n);
     int cur = 0;
     for (int it = 0; it < iters; ++it) {
-      hipLaunchKernelGGL(trace, dim3(grid_t), dim3(256), lds, stream, p, b, cur);
+      hipLaunchKernelGGL(trace, dim3(grid_t), dim3(256), lds_t, stream, p, b, cur);
       wf_shade_kernel<<<grid_s, 256, 0, stream>>>(p, b, cur);
       cur ^= 1;
     }

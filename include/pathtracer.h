@@ -312,6 +312,12 @@ int pt_dist_finalize(pt_context* ctx);
 /* PT_OPT_COUNT_TRACED: 1 = run the fast kernels with counters of the work
  * they actually do (pt_get_traced); slower, output identical.  Default 0. */
 #define PT_OPT_COUNT_TRACED 10
+/* PT_OPT_PAIRS: 1 = the wavefront pipeline walks device-memory scenes over
+ * child-pair records (both child boxes of an internal node in one 64-B
+ * record, the right subtree first, pending siblings on a per-lane LDS
+ * stack); 0 (default) = the threaded node walk, faster on the BASELINE
+ * scenes.  Output is identical. */
+#define PT_OPT_PAIRS 11
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */

@@ -792,3 +792,31 @@ def test_count_traced_mode(scene):
     r.render(0, nb)
     assert r.traced()["primaries"] == W * H * nb
     _assert_same(r.read_accum(), ref, f"{scene} counting, culling off")
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_wavefront_pair_records(case):
+    """PT_OPT_PAIRS: the wavefront walk over child-pair records (right subtree
+    first, pending siblings and hit leaves on a per-lane stack) gives the
+    oracle's frame: a displaced sphere, a 20K int-encoded cloud, and the
+    tie-heavy grid with two lights (implied-hit children, leaf markers on the
+    stack)."""
+    if case == 0:
+        sv, si = scenes.displaced_sphere(3)
+        cam, lights, int_bits = scenes.camera((0.0, 0.5, 3.0)), scenes.REFERENCE_LIGHT, False
+    elif case == 1:
+        sv, si = scenes.random_triangles(20000, seed=7)
+        cam, lights, int_bits = scenes.camera((0.3, 0.2, 2.2)), scenes.REFERENCE_LIGHT, True
+    else:
+        sv, si = scenes.grid_mesh(6)
+        cam, int_bits = scenes.camera((0.0, 0.0, 3.0)), False
+        lights = np.concatenate([scenes.REFERENCE_LIGHT,
+                                 ptamd.pack_light([0.5, 0.5, 1.5], [0, 0, -1], [2, 4, 8], [0.5, 1.0])])
+    v, i, n, _, _ = ptamd.Scene.from_arrays(sv, si).build_bvh(int_bits=int_bits).arrays()
+    r = _setup(v, i, n, cam=cam, lights=lights, int_bits=int_bits, lds=0)
+    r.set_option(ptamd.PT_OPT_KERNEL, 3)
+    r.set_option(ptamd.PT_OPT_PAIRS, 1)
+    r.resize_and_clear(72, 56)
+    r.render(1, 3)
+    ref, _ = _oracle(v, i, n, 72, 56, first=1, nb=3, cam=cam, lights=lights, int_bits=int_bits)
+    _assert_same(r.read_accum(), ref, f"pair records case {case}")
