@@ -26,6 +26,7 @@
 #include "scene/camera.h"
 #include "scene/light.h"
 #include "scene/obj_loader.h"
+#include "scene/wide_bvh.h"
 
 namespace {
 
@@ -363,6 +364,16 @@ struct pt_context {
   float4* d_nodes_full = nullptr;   // threaded, every reference node (stats mode)
   float4* d_pairs = nullptr;        // child-pair records (wavefront walk of device-memory scenes)
   int pair_depth = 0;               // tree depth (the pair walk's stack holds at most this)
+  // culled wide walk (wide_walk.h): nodes, triangle records by rank, rank ->
+  // slot, per-lane stack overflow areas (grown on demand)
+  float4* d_wide = nullptr;
+  float4* d_wide_tris = nullptr;
+  int* d_wide_tri_of = nullptr;
+  int2* d_wide_ovf = nullptr;
+  long long wide_ovf_lanes = 0;
+  int n_wide = 0, wide_stack = 0;
+  std::string wide_reason = "no scene";
+  int opt_wide = 1;           // PT_OPT_WIDE
   int n_nodes_full = 0;
   float4* d_tris = nullptr;
   int n_tris = 0;
@@ -771,6 +782,13 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   ptd::RenderParams p;
   p.pairs = nullptr;   // set below for the wavefront walk
   p.pair_depth = 0;
+  p.wide = nullptr;
+  p.wide_tris = nullptr;
+  p.wide_tri_of = nullptr;
+  p.wide_ovf = nullptr;
+  p.wide_ovf_lanes = 0;
+  p.wide_stack = 0;
+  p.wide_handback = 0;
   p.nodes = c->stats_mode ? c->d_nodes_full : c->d_nodes;
   p.tris = c->d_tris;
   p.lights = c->d_lights_dev;
@@ -938,6 +956,23 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     if (c->opt_pairs && c->d_pairs && c->pair_depth <= 32) {
       p.pairs = c->d_pairs;
       p.pair_depth = std::max(1, c->pair_depth);
+    } else if (c->opt_wide && c->n_wide > 0 && !lds) {
+      const long long lanes = ptd::wide_trace_lanes();
+      if (lanes <= 0) return fail(PT_ERR_HIP, "wide walk: occupancy query failed");
+      if (lanes > c->wide_ovf_lanes) {   // every lane of the persistent grid gets its overflow area
+        { const int rc_ = quiesce(c); if (rc_) return rc_; }
+        dev_free(c->d_wide_ovf);
+        c->wide_ovf_lanes = 0;
+        PT_HIP(hipMalloc((void**)&c->d_wide_ovf, (size_t)lanes * (size_t)c->wide_stack * sizeof(int2)));
+        c->wide_ovf_lanes = lanes;
+      }
+      p.wide = c->d_wide;
+      p.wide_tris = c->d_wide_tris;
+      p.wide_tri_of = c->d_wide_tri_of;
+      p.wide_ovf = c->d_wide_ovf;
+      p.wide_ovf_lanes = c->wide_ovf_lanes;
+      p.wide_stack = c->wide_stack;
+      p.wide_handback = c->opt_wide == 2 ? 1 : 0;
     }
     PT_HIP(ptd::launch_wavefront(p, b, lds, c->stream, cnt));
   } else {
@@ -1013,6 +1048,10 @@ int pt_destroy(pt_context* c) {
   dev_free(c->d_nodes);
   dev_free(c->d_nodes_full);
   dev_free(c->d_pairs);
+  dev_free(c->d_wide);
+  dev_free(c->d_wide_tris);
+  dev_free(c->d_wide_tri_of);
+  dev_free(c->d_wide_ovf);
   dev_free(c->d_tris);
   dev_free(c->d_lights);
   dev_free(c->d_lights_dev);
@@ -1078,6 +1117,10 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   std::vector<float4> pairs;
   int pair_depth = 0;
   build_pairs(nodes, n_nodes, (flags & PT_NODES_INT_BITS) != 0, &pairs, &pair_depth);
+  pt::WideBVH wide;
+  const std::string wide_reason =
+      pt::build_wide_bvh((const float*)nodes, n_nodes, (flags & PT_NODES_INT_BITS) != 0, vertices, n_vertex_floats,
+                         indices, n_indices / 3, &wide);
   float lo[3] = {threaded[0].x, threaded[0].y, threaded[0].z};   // node 0 is the root
   float hi[3] = {threaded[1].x, threaded[1].y, threaded[1].z};
   PT_HIP(hipSetDevice(c->device));
@@ -1085,7 +1128,10 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   dev_free(c->d_nodes);
   dev_free(c->d_nodes_full);
   dev_free(c->d_pairs);
-  dev_free(c->d_tris);
+  dev_free(c->d_wide);
+  dev_free(c->d_wide_tris);
+  dev_free(c->d_wide_tri_of);
+  c->n_wide = 0;
   c->has_scene = false;
   const int T = (int)(n_indices / 3);
   struct Staging {   // vertex/index copies live only until the triangle records are built
@@ -1111,7 +1157,20 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   PT_HIP(hipMemcpyAsync(st.v, vertices, n_vertex_floats * sizeof(float), hipMemcpyHostToDevice, c->stream));
   PT_HIP(hipMemcpyAsync(st.i, indices, n_indices * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
   PT_HIP(ptd::launch_setup_tris(st.v, st.i, T, c->d_tris, c->stream));
+  if (wide_reason.empty()) {
+    PT_HIP(hipMalloc((void**)&c->d_wide, wide.nodes.size() * sizeof(float)));
+    PT_HIP(hipMalloc((void**)&c->d_wide_tri_of, (size_t)T * sizeof(int)));
+    PT_HIP(hipMalloc((void**)&c->d_wide_tris, (size_t)T * 3 * sizeof(float4)));
+    PT_HIP(hipMemcpyAsync(c->d_wide, wide.nodes.data(), wide.nodes.size() * sizeof(float), hipMemcpyHostToDevice,
+                          c->stream));
+    PT_HIP(hipMemcpyAsync(c->d_wide_tri_of, wide.rank_tri.data(), (size_t)T * sizeof(int), hipMemcpyHostToDevice,
+                          c->stream));
+    PT_HIP(ptd::launch_gather_tris(c->d_tris, c->d_wide_tri_of, T, c->d_wide_tris, c->stream));
+  }
   PT_HIP(hipStreamSynchronize(c->stream));
+  c->n_wide = wide_reason.empty() ? wide.n_nodes : 0;
+  c->wide_stack = wide.stack_cap;
+  c->wide_reason = wide_reason;
   c->n_nodes = (int)(collapsed.size() / 2) - 1;
   c->n_nodes_full = (int)(threaded.size() / 2) - 1;
   c->pair_depth = pair_depth;
@@ -1381,6 +1440,10 @@ int pt_set_option(pt_context* c, int key, int value) {
       if (value < 0 || value > 3) return fail(PT_ERR_INVALID, "PT_OPT_KERNEL takes 0, 1, 2 or 3");
       c->opt_kernel = value;
       return PT_OK;
+    case PT_OPT_WIDE:
+      if (value < 0 || value > 2) return fail(PT_ERR_INVALID, "PT_OPT_WIDE takes 0, 1 or 2");
+      c->opt_wide = value;
+      return PT_OK;
     case PT_OPT_PAIRS:
       if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_PAIRS takes 0 or 1");
       c->opt_pairs = value;
@@ -1530,6 +1593,14 @@ int pt_get_stats(pt_context* c, pt_stats* out) {
   out->nodes = h[1];
   out->leaf_tests = h[2];
   out->samples = h[3];
+  return PT_OK;
+}
+
+int pt_wide_info(pt_context* c, int info[2]) {
+  if (!c || !info) return fail(PT_ERR_INVALID, "null argument");
+  info[0] = c->n_wide;
+  info[1] = c->n_wide ? c->wide_stack : 0;
+  if (!c->n_wide) g_err = c->wide_reason;
   return PT_OK;
 }
 

@@ -84,6 +84,16 @@ __host__ __device__ inline bool part_owns(const Part& p, int b) {
 struct RenderParams {
   const float4* pairs;      // child-pair records, or null (threaded walk)
   int pair_depth;           // tree depth: entries of the pair walk's stack
+  // culled wide walk (wide_walk.h), or null: 4-wide nodes, triangle records
+  // by leaf rank, rank -> triangle slot, per-lane stack overflow areas
+  // (wide_ovf_lanes lanes of wide_stack entries, lane-strided)
+  const float4* wide;
+  const float4* wide_tris;
+  const int* wide_tri_of;
+  int2* wide_ovf;
+  long long wide_ovf_lanes;
+  int wide_stack;
+  int wide_handback;        // test: hand every odd list slot to the exact walk (PT_OPT_WIDE 2)
   const float4* nodes;
   const float4* tris;
   const LightDev* lights;
@@ -185,6 +195,10 @@ inline int wf_max_rays(const RenderParams& p) {
 }
 hipError_t launch_wavefront(const RenderParams& p, const WfBuffers& b, bool lds_scene, hipStream_t stream,
                             bool cnt = false);
+// lanes of the wide walk's persistent grid on this device (overflow areas to allocate)
+long long wide_trace_lanes();
+// triangle records by rank: dst[r] = tris[tri_of[r]]
+hipError_t launch_gather_tris(const float4* tris, const int* tri_of, int n, float4* dst, hipStream_t stream);
 hipError_t launch_math(int fn, const float* x, float* y, size_t n, hipStream_t stream);
 hipError_t launch_exhaustive(int fn, unsigned long long* bad, uint32_t* first_bad, hipStream_t stream);
 

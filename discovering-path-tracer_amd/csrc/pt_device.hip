@@ -25,6 +25,8 @@
 #include <algorithm>
 
 #include "pt_device.h"
+#include "pt_isect.h"
+#include "wide_walk.h"
 #include "pt_math.h"
 
 #pragma clang fp contract(off)
@@ -53,37 +55,6 @@ struct Hit {
   float t;
   int tri;   // -1 = miss
 };
-
-// intersectAABB (:102-112) with invDir hoisted (same value every node).
-__device__ __forceinline__ bool slab(v3 o, v3 inv, float4 a, float4 b) {
-  const float t0x = (a.x - o.x) * inv.x, t0y = (a.y - o.y) * inv.y, t0z = (a.z - o.z) * inv.z;
-  const float t1x = (b.x - o.x) * inv.x, t1y = (b.y - o.y) * inv.y, t1z = (b.z - o.z) * inv.z;
-  const float tmin = fmax_(fmax_(fmin_(t0x, t1x), fmin_(t0y, t1y)), fmin_(t0z, t1z));
-  const float tmax = fmin_(fmin_(fmax_(t0x, t1x), fmax_(t0y, t1y)), fmax_(t0z, t1z));
-  return tmin <= tmax && tmax >= 0.0f;
-}
-
-// intersectTriangle (:114-157), edges precomputed; UV tail is dead code.
-__device__ __forceinline__ bool tri_test(v3 o, v3 d, float4 A, float4 B, float4 C, float* tout) {
-  const float EPS = 0.000001f;
-  const v3 v0 = mk(A.x, A.y, A.z);
-  const v3 e1 = mk(A.w, B.x, B.y);
-  const v3 e2 = mk(B.z, B.w, C.x);
-  const v3 p = cross(d, e2);
-  const float det = dot(e1, p);
-  if (fabs_(det) < EPS) return false;
-  const float inv = rcp_(det);
-  const v3 s = sub(o, v0);
-  const float u = inv * dot(s, p);
-  if (u < 0.0f || u > 1.0f) return false;
-  const v3 q = cross(s, e1);
-  const float v = inv * dot(d, q);
-  if (v < 0.0f || u + v > 1.0f) return false;
-  const float t = inv * dot(e2, q);
-  if (t <= EPS) return false;
-  *tout = t;
-  return true;
-}
 
 // Leaf candidates are queued per lane (in LDS, [slot][lane] so a wave's
 // stores hit 64 distinct banks) and their triangles tested after the walk:
@@ -1032,6 +1003,16 @@ __global__ __launch_bounds__(256) void setup_tris_kernel(const float* __restrict
 
 // Per-light constants of sampleAreaLight / intersectAreaLight (:261-264,
 // :284-287, :295-296), computed with the shader's ops.
+// Triangle records in leaf-rank order for the wide walk.
+__global__ __launch_bounds__(256) void gather_tris_kernel(const float4* __restrict__ tris,
+                                                          const int* __restrict__ tri_of, int n,
+                                                          float4* __restrict__ dst) {
+  const int i = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (i >= 3 * n) return;
+  const int r = i / 3, k = i - 3 * r;
+  dst[i] = tris[3 * (size_t)tri_of[r] + k];
+}
+
 __global__ __launch_bounds__(64) void setup_lights_kernel(const LightRec* __restrict__ in, int n,
                                                           LightDev* __restrict__ out) {
   const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -2074,6 +2055,89 @@ __global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_ker
   if (CNT) flush_traced(P, c, lane);
 }
 
+// ---------------------------------------------------------------------------
+// Culled wide walk (wide_walk.h) for scenes in device memory: 4-wide nodes of
+// the reference's own boxes, nearest child first, children culled once no
+// triangle in them can beat (or tie) the best hit -- the same answer as the
+// exhaustive DFS, far fewer node fetches (CPU harness, 1M-triangle cloud,
+// camera rays: 42 wide nodes and 4.3 triangle tests per ray against 1022
+// nodes and 31 leaf tests).  Per lane: the ray, the node to expand, and a
+// stack of pending (node, cull threshold) entries -- the top kWideLds in LDS
+// ([entry][lane], conflict-free), older ones in a per-lane global overflow
+// area (P.wide_ovf, strided by lane so neighbouring lanes' spills coalesce).
+// Rays the walk does not take (zero / subnormal direction components) return
+// kNeedExact* and wf_shade_kernel walks them exactly (trace_closest /
+// occluded).
+// ---------------------------------------------------------------------------
+#ifndef PT_WIDE_MIN_BLOCKS
+#define PT_WIDE_MIN_BLOCKS 6
+#endif
+template <int G, bool CNT = false>
+__global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(RenderParams P, WfBuffers B,
+                                                                                int cur) {
+  const int tid = (int)threadIdx.x;
+  if (blockIdx.x == 0 && tid == 0) B.counters[cur ^ 1] = 0;   // filled by the shading that follows
+  const int count = B.counters[cur];
+  if (count == 0) return;
+  const int wave = tid >> 6, lane = tid & 63;
+  __shared__ int2 stk[4][kWideLds][64];
+  int2* lds = &stk[wave][0][lane];
+  const long long os = (long long)gridDim.x * 256;
+  int2* ovf = P.wide_ovf + ((long long)blockIdx.x * 256 + tid);
+  const float4* __restrict__ rays = B.rays[cur];
+  int p = -1;   // list slot this lane traces
+  bool more = true;
+  WideRay R;
+  R.cur = -1;
+  R.sp = R.lo = 0;
+  Ctr c = {0u, 0u, 0u, 0u, 0u};
+  for (;;) {
+    const unsigned long long idle = __ballot(p < 0);
+    unsigned long long gm = idle;
+#pragma unroll
+    for (int sh = 1; sh < G; sh <<= 1) gm &= gm >> sh;
+    gm &= group_lead<G>();
+    const int ng = (int)__popcll(gm);
+    if (more && ng * G >= PT_WF_REFILL) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&B.counters[2], ng * G);
+      base = __shfl(base, 0);
+      if (base + ng * G >= count) more = false;
+      const int lead = lane & ~(G - 1);
+      if ((gm >> lead) & 1ull) {
+        const int slot = base + (int)__popcll(gm & ((1ull << lead) - 1ull)) * G + (lane - lead);
+        if (slot < count) {
+          const float4 r0 = rays[2 * (size_t)slot], r1 = rays[2 * (size_t)slot + 1];
+          const int kind = __float_as_int(r1.w);   // 0 closest, 1 shadow, 2 null shadow (trav_null)
+          if (CNT) count_start(rays + 2 * (size_t)slot, c);
+          wide_start(R, mk(r0.x, r0.y, r0.z), mk(r1.x, r1.y, r1.z), kind != 0, r0.w);
+          if (kind == 2) {
+            B.hits[slot] = make_float2(R.lim, __int_as_float(0));
+          } else if (!wide_ray_ok(R.o, R.d, R.inv) || (P.wide_handback && (slot & 1))) {
+            B.hits[slot] = make_float2(R.lim, __int_as_float(kind ? kNeedExactShadow : kNeedExactClosest));
+          } else {
+            p = slot;
+          }
+        }
+      }
+    }
+    if (!more && __ballot(p >= 0) == 0ull) break;
+    for (int it = 0; it < PT_WF_STEPS; ++it) {
+      bool exact = false;
+      if (p >= 0 && wide_step<CNT>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
+                                   &c.leaves)) {
+        int res;
+        if (exact) res = R.shadow ? kNeedExactShadow : kNeedExactClosest;
+        else if (R.shadow) res = R.best;
+        else res = R.best >= 0 ? P.wide_tri_of[R.best] : -1;
+        B.hits[p] = make_float2(R.lim, __int_as_float(res));
+        p = -1;
+      }
+    }
+  }
+  if (CNT) flush_traced(P, c, lane);
+}
+
 // Shading of every path in list `cur` (path_step on the returned hit);
 // paths that need another ray go to list cur^1, finished ones store colour.
 //
@@ -2093,6 +2157,8 @@ __global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers
   const int count = B.counters[cur];
   CamFrame F = {};   // camera frame: used by PH_BEGIN only
   __shared__ int bin_cnt[16], bin_base[16], wg_base;
+  __shared__ int cand_buf[4][kCand][64];   // exact walks of handed-back rays
+  int* cand = &cand_buf[threadIdx.x >> 6][0][threadIdx.x & 63];
   for (int base = (int)blockIdx.x * 256; base < count; base += (int)gridDim.x * 256) {
     const int i = base + (int)threadIdx.x;
     bool need = false;
@@ -2112,6 +2178,13 @@ __global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers
       T.nc = 0;
       T.cn = T.cl = 0u;
       Ctr c = {0u, 0u, 0u, 0u, 0u};
+      if (T.shadow == 0 && T.res == kNeedExactClosest) {   // handed back by wf_trace_wide_kernel
+        const Hit e = trace_closest<false, false, true, false>(P, T.o, T.d, c, cand);
+        T.lim = e.t;
+        T.res = e.tri;
+      } else if (T.shadow == 1 && T.res == kNeedExactShadow) {
+        T.res = occluded<false, false>(P, T.o, T.d, T.lim, c) ? 1 : 0;
+      }
       v3 col;
       need = path_step<false>(P, F, S, T, c, &col);
       if (need)
@@ -2193,6 +2266,12 @@ hipError_t launch_setup_tris(const float* d_vertices, const uint32_t* d_indices,
   return hipGetLastError();
 }
 
+hipError_t launch_gather_tris(const float4* tris, const int* tri_of, int n, float4* dst, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  gather_tris_kernel<<<(unsigned)((3ll * n + 255) / 256), 256, 0, stream>>>(tris, tri_of, n, dst);
+  return hipGetLastError();
+}
+
 hipError_t launch_setup_lights(const LightRec* d_in, int n, LightDev* d_out, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
   setup_lights_kernel<<<(n + 63) / 64, 64, 0, stream>>>(d_in, n, d_out);
@@ -2270,6 +2349,19 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool
   return hipGetLastError();
 }
 
+long long wide_trace_lanes() {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  int most = 0;
+  for (auto k : {wf_trace_wide_kernel<2>, wf_trace_wide_kernel<4>, wf_trace_wide_kernel<2, true>,
+                 wf_trace_wide_kernel<4, true>}) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess) return 0;
+    most = std::max(most, per_cu);
+  }
+  return (long long)cus * std::max(most, 1) * 256;
+}
+
 hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds_scene, hipStream_t stream, bool cnt) {
   if (p0.spl != 1 && p0.spl != 2 && p0.spl != 4 && p0.spl != 8) return hipErrorInvalidValue;
   if (p0.n_batches == 0) return hipSuccess;
@@ -2301,12 +2393,21 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
   if (p0.pairs && !lds_scene)   // child-pair records (PT_OPT_PAIRS)
     trace = cnt ? (g2 ? wf_trace_pairs_kernel<2, true> : wf_trace_pairs_kernel<4, true>)
                 : (g2 ? wf_trace_pairs_kernel<2> : wf_trace_pairs_kernel<4>);
+  const bool wide = p0.wide && !lds_scene && !p0.pairs;
+  if (wide)   // culled wide walk (PT_OPT_WIDE, default)
+    trace = cnt ? (g2 ? wf_trace_wide_kernel<2, true> : wf_trace_wide_kernel<4, true>)
+                : (g2 ? wf_trace_wide_kernel<2> : wf_trace_wide_kernel<4>);
   size_t lds_t = lds;
   if (p0.pairs && !lds_scene) lds_t = (size_t)4 * 64 * p0.pair_depth * sizeof(int);   // the walk stacks
+  if (wide) lds_t = 0;
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, trace, 256, lds_t);
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, wf_shade_kernel, 256, 0);
   if (e != hipSuccess) return e;
-  const unsigned grid_t = (unsigned)(cus * (per_cu_t > 0 ? per_cu_t : 1));
+  unsigned grid_t = (unsigned)(cus * (per_cu_t > 0 ? per_cu_t : 1));
+  if (wide) {   // every lane needs its overflow stack area
+    if (p0.wide_ovf_lanes < 256) return hipErrorInvalidValue;
+    grid_t = std::min<unsigned>(grid_t, (unsigned)(p0.wide_ovf_lanes / 256));
+  }
   const unsigned grid_s = (unsigned)(cus * (per_cu_s > 0 ? per_cu_s : 1));
   const uint32_t chunk = (uint32_t)std::min<long long>((long long)p0.n_batches, b.cap / px);
   const int iters = wf_max_rays(p0);

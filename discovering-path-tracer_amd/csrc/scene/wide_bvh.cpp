@@ -1,0 +1,258 @@
+// Wide BVH builder and the cull bound of the culled walk (wide_bvh.h,
+// csrc/wide_walk.h).
+#include "wide_bvh.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+
+namespace pt {
+
+namespace {
+
+constexpr int32_t kEmpty = (int32_t)0x80000000;   // wide_walk.h kWideEmpty
+constexpr double kMaxCoord = 1e15;                 // wide_walk.h kWideMaxCoord
+constexpr double kU = 0x1p-24;                      // unit roundoff of fp32
+double gam(int k) { return k * kU / (1.0 - k * kU); }
+
+float up_f(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = nextafterf(f, INFINITY);
+  return f;
+}
+float down_f(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = nextafterf(f, -INFINITY);
+  return f;
+}
+
+}  // namespace
+
+// Error bound of intersectTriangle (raytrace_comp.comp:114-157) as the
+// kernels evaluate it (tri_test: edges e1, e2 precomputed, no contraction,
+// IEEE reciprocal).  Notation: u = 2^-24, g_k = k u / (1 - k u), |x|_1 and
+// |x|_inf vector norms, s = fl(o - v0), S = |s|_inf, p = fl(cross(d, e2)),
+// det = fl(dot(e1, p)), q = fl(cross(s, e1)).  Let o'' = v0 + s (exact), so
+// |o'' - o|_inf <= u |o - v0|_inf.  In exact arithmetic on these float
+// inputs, Cramer's rule gives o'' + T d = v0 + u* e1 + v* e2 =: X with
+// T = dot(e2, q*)/det*, u* = dot(s, p*)/det*, v* = dot(d, q*)/det* (starred:
+// exact cross/dot).  Standard bounds (cross component g2, dot of 3 terms g3):
+//   |det - det*|         <= g6 Dd,  Dd <= |d|inf D0,  D0 = sum_i |e1_i|(|e2|_1 - |e2_i|)
+//   |fl(s.p) - s.p*|     <= g6 S |d|inf 2|e2|_1
+//   |fl(d.q) - d.q*|     <= g6 S |d|inf 2|e1|_1
+//   |fl(e2.q) - e2.q*|   <= g6 S D0
+// and with the acceptance |det| >= 1e-6 (EPSILON, :127), g = g6 / 0.999e-6:
+//   du = |u_b - u*| <= (2 g dm |e2|_1 S + g dm D0 + g3) / (1 - g dm D0)   (u_b in [0,1])
+//   dv = |v_b - v*| <= (2 g dm |e1|_1 S + g dm D0 + g3) / (1 - g dm D0)
+//   |t_b - T| <= g D0 (S + dm |T|) + g3 t_b
+// (dm >= |d|_2, |d|_inf: the walk takes only rays with fl(d.d) <= 1.00002).
+// X lies within rho (inf-norm) of conv(v0, v0+e1, v0+e2) -- hence of the
+// triangle (|e1 - (v1 - v0)| <= u|e1|) and of any box B containing it:
+//   rho = u max(|e1|inf, |e2|inf) + du |e1|inf + dv |e2|inf.
+// An accepted triangle with t_b <= b then has |T| <= (b (1+g3) + g D0 S) /
+// (1 - g dm D0), and dist(o, B) <= |o - o''| + |o'' - X| + sqrt3 rho
+//   <= dm |T| + sqrt3 (rho + u S / (1-u)).
+// Every term is linear in S, and S <= (1+u)(dist(o, B) + ext(B)) (v0 is in
+// B; ext = the box's largest extent), so dist(o,B) <= a b + b' (dist + ext) + c
+// and, for b' < 1: dist(o,B) <= (a b + b' ext + c) / (1 - b').
+bool wide_tri_coeffs(const float e1f[3], const float e2f[3], double* A, double* Bc, double* C) {
+  const double dm = 1.0000102;   // sqrt(1.00002 (1 + g3)) rounded up
+  const double g = gam(6) / 0.999e-6;
+  double n1 = 0, n2 = 0, m1 = 0, m2 = 0, D0 = 0;
+  double a1[3], a2[3];
+  for (int i = 0; i < 3; ++i) {
+    a1[i] = fabs((double)e1f[i]);
+    a2[i] = fabs((double)e2f[i]);
+    n1 += a1[i];
+    n2 += a2[i];
+    m1 = std::max(m1, a1[i]);
+    m2 = std::max(m2, a2[i]);
+  }
+  for (int i = 0; i < 3; ++i) D0 += a1[i] * (n2 - a2[i]);
+  if (!(n1 < 1e30 && n2 < 1e30)) return false;
+  const double den = 1.0 - g * dm * D0;
+  if (!(den >= 0.5)) return false;
+  const double alpha_u = 2.0 * g * dm * n2 / den, alpha_v = 2.0 * g * dm * n1 / den;
+  const double beta = (g * dm * D0 + gam(3)) / den;
+  const double rhoS = alpha_u * m1 + alpha_v * m2;
+  const double rho0 = 1.01 * kU * std::max(m1, m2) + beta * (m1 + m2);
+  const double s3 = 1.7320508075688774;
+  const double a = dm * (1.0 + gam(3)) / den;
+  const double b = dm * g * D0 / den + s3 * (rhoS + kU / (1.0 - kU));
+  const double c = s3 * rho0;
+  const double bp = b * (1.0 + kU);
+  if (!(bp < 0.5)) return false;
+  *A = a / (1.0 - bp);
+  *Bc = bp / (1.0 - bp);
+  *C = c / (1.0 - bp);
+  return true;
+}
+
+std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float* V, size_t n_vf,
+                           const uint32_t* I, size_t n_tris, WideBVH* out) {
+  *out = WideBVH();
+  if (n == 0) return "no nodes";
+  auto link = [&](size_t i, int which) -> int32_t {
+    const float f = N[8 * i + (which ? 7 : 3)];
+    int32_t v;
+    if (int_bits) memcpy(&v, &f, 4);
+    else v = (int32_t)f;
+    return v;
+  };
+  auto leaf = [&](size_t i) { return link(i, 0) == -1; };
+  auto lo = [&](size_t i, int a) { return N[8 * i + a]; };
+  auto hi = [&](size_t i, int a) { return N[8 * i + 4 + a]; };
+  // pre-order (right child first: the reference's visit order) and leaf ranks
+  std::vector<int32_t> order, rank(n, -1);
+  order.reserve(n);
+  {
+    std::vector<int32_t> st{0};
+    while (!st.empty()) {
+      const int32_t v = st.back();
+      st.pop_back();
+      order.push_back(v);
+      if (leaf(v)) {
+        rank[v] = (int32_t)out->rank_tri.size();
+        out->rank_tri.push_back(link(v, 1));
+      } else {
+        st.push_back(link(v, 0));
+        st.push_back(link(v, 1));
+      }
+    }
+  }
+  if (out->rank_tri.size() != n_tris) return "tree leaves do not cover the triangles once";
+  // the walk's premises on the uploaded arrays: finite, bounded coordinates;
+  // parent boxes contain their children's; leaf boxes contain their triangle
+  for (size_t i = 0; i < n; ++i)
+    for (int a = 0; a < 3; ++a)
+      if (!(fabs((double)lo(i, a)) <= kMaxCoord && fabs((double)hi(i, a)) <= kMaxCoord))
+        return "node coordinates not finite or beyond 1e15";
+  std::vector<double> mA(n), mB(n), mC(n);   // max cull coefficients over each subtree
+  for (size_t k = order.size(); k-- > 0;) {
+    const int32_t v = order[k];
+    if (leaf(v)) {
+      const uint32_t t = (uint32_t)link(v, 1);
+      float p[3][3];
+      for (int c = 0; c < 3; ++c) {
+        const uint32_t vi = I[3 * (size_t)t + c];
+        if ((size_t)vi * 3 + 2 >= n_vf) return "vertex index out of range";
+        for (int a = 0; a < 3; ++a) {
+          p[c][a] = V[3 * (size_t)vi + a];
+          if (!(p[c][a] >= lo(v, a) && p[c][a] <= hi(v, a))) return "leaf box does not contain its triangle";
+        }
+      }
+      float e1[3], e2[3];
+      for (int a = 0; a < 3; ++a) {
+        e1[a] = p[1][a] - p[0][a];   // fl(v1 - v0), as setup_tris_kernel
+        e2[a] = p[2][a] - p[0][a];
+      }
+      double A, B, C;
+      if (wide_tri_coeffs(e1, e2, &A, &B, &C)) {
+        mA[v] = A;
+        mB[v] = B;
+        mC[v] = C;
+      } else {
+        mA[v] = INFINITY;
+        mB[v] = mC[v] = 0;
+      }
+    } else {
+      const int32_t l = link(v, 0), r = link(v, 1);
+      for (int32_t ch : {l, r})
+        for (int a = 0; a < 3; ++a)
+          if (!(lo(v, a) <= lo(ch, a) && hi(v, a) >= hi(ch, a))) return "a parent box does not contain its child's";
+      mA[v] = std::max(mA[l], mA[r]);
+      mB[v] = std::max(mB[l], mB[r]);
+      mC[v] = std::max(mC[l], mC[r]);
+    }
+  }
+  // wide nodes: expand the reference node's children, largest box first,
+  // until four entries or all leaves
+  auto area = [&](int32_t v) {
+    const double dx = (double)hi(v, 0) - lo(v, 0), dy = (double)hi(v, 1) - lo(v, 1), dz = (double)hi(v, 2) - lo(v, 2);
+    return dx * dy + dy * dz + dz * dx;
+  };
+  std::vector<float>& W = out->nodes;
+  std::vector<int32_t> n_inner;              // per wide node: inner children
+  std::vector<std::vector<int32_t>> kids;    // per wide node: its inner children's wide indices
+  auto alloc = [&]() {
+    W.resize(W.size() + 32, 0.0f);
+    n_inner.push_back(0);
+    kids.emplace_back();
+    return (int32_t)(n_inner.size() - 1);
+  };
+  std::vector<std::pair<int32_t, int32_t>> st;   // (reference node, wide node)
+  st.push_back({0, alloc()});
+  while (!st.empty()) {
+    const auto [v, w] = st.back();
+    st.pop_back();
+    std::vector<int32_t> list;
+    if (leaf(v)) {
+      list.push_back(v);   // a one-triangle tree: the root leaf is the only child
+    } else {
+      list = {link(v, 1), link(v, 0)};
+      while (list.size() < 4) {
+        int best = -1;
+        double ba = -1.0;
+        for (size_t j = 0; j < list.size(); ++j)
+          if (!leaf(list[j]) && area(list[j]) > ba) {
+            ba = area(list[j]);
+            best = (int)j;
+          }
+        if (best < 0) break;
+        const int32_t x = list[best];
+        list[best] = link(x, 1);
+        list.insert(list.begin() + best + 1, link(x, 0));
+      }
+    }
+    double A = 0.0, C = 0.0;
+    float* rec = &W[32 * (size_t)w];
+    for (int j = 0; j < 4; ++j) {
+      int32_t ref = kEmpty;
+      if (j < (int)list.size()) {
+        const int32_t c = list[j];
+        for (int a = 0; a < 3; ++a) {
+          rec[8 * a + j] = lo(c, a);
+          rec[8 * a + 4 + j] = hi(c, a);
+        }
+        const double ext = std::max({(double)hi(c, 0) - lo(c, 0), (double)hi(c, 1) - lo(c, 1),
+                                     (double)hi(c, 2) - lo(c, 2)});
+        A = std::max(A, mA[c]);
+        C = std::max(C, ext * mB[c] + mC[c]);
+        if (leaf(c)) {
+          ref = ~rank[c];
+        } else {
+          ref = alloc();
+          rec = &W[32 * (size_t)w];   // alloc may move W
+          n_inner[w]++;
+          kids[w].push_back(ref);
+          st.push_back({c, ref});
+        }
+      }
+      memcpy(&rec[24 + j], &ref, 4);
+    }
+    if (A == INFINITY || !(C < 1e30)) {
+      rec[28] = 0.0f;   // 1/A = 0: th = 0, nothing is culled (lim < 0 culls nothing that could win)
+      rec[29] = 0.0f;
+    } else {
+      rec[28] = down_f(1.0 / (A * (1.0 + 1e-6)));
+      rec[29] = up_f(C * (1.0 + 1e-6));
+    }
+    rec[30] = rec[31] = 0.0f;
+  }
+  // stack bound: a node pushes at most (inner children - 1) entries, which
+  // stay until its subtree is done: the most along any root-to-node path
+  const size_t nw = n_inner.size();
+  std::vector<int32_t> bound(nw, 0);
+  for (size_t w = nw; w-- > 0;) {   // children are allocated after their parent
+    int32_t m = 0;
+    for (int32_t k : kids[w]) m = std::max(m, bound[k]);
+    bound[w] = std::max(0, n_inner[w] - 1) + m;
+  }
+  if (bound[0] > 4096) return "tree too deep for the wide walk's stack";
+  out->n_nodes = (int)nw;
+  out->stack_cap = bound[0] + 1;
+  return "";
+}
+
+}  // namespace pt

@@ -1,0 +1,40 @@
+// Wide (4-ary) BVH for the culled walk of device-memory scenes
+// (csrc/wide_walk.h explains why the walk returns the reference's hits).
+//
+// Built from the uploaded reference tree (BoundingVolumeHierarchy.cpp layout,
+// already validated as a tree by thread_bvh): every wide node holds up to four
+// of the reference's own nodes (their boxes bitwise), obtained by expanding a
+// reference internal node's children until four or all leaves; leaves are
+// numbered by the rank the reference's right-first DFS (raytrace_comp.comp
+// :196-200) visits them in.  Each node also stores the cull coefficients of
+// the triangles below it.
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+namespace pt {
+
+struct WideBVH {
+  std::vector<float> nodes;        // 32 floats per node, the wide_walk.h layout
+  std::vector<int32_t> rank_tri;   // leaf rank -> triangle slot (the reference's triIdx)
+  int n_nodes = 0;
+  int stack_cap = 0;               // most stack entries a walk can hold
+};
+
+// nodes: n reference nodes, 8 floats each ({min.xyz, left}, {max.xyz, right};
+// links float- or int-encoded).  Returns "" on success, else the reason the
+// culled walk cannot take this scene (the caller keeps the exact walk): a
+// parent box not containing a child's, a leaf box not containing its
+// triangle, non-finite or huge coordinates, or a degenerate depth.
+std::string build_wide_bvh(const float* nodes, size_t n, bool int_bits, const float* verts, size_t n_vertex_floats,
+                           const uint32_t* idx, size_t n_tris, WideBVH* out);
+
+// The cull coefficients of one triangle (edges e1 = fl(v1-v0), e2 = fl(v2-v0)):
+// accepted with t <= b implies dist(o, B) <= A*b + Bc*ext(B) + C for every box
+// B containing it.  false: the bound does not apply (no culling).
+bool wide_tri_coeffs(const float e1[3], const float e2[3], double* A, double* Bc, double* C);
+
+}  // namespace pt

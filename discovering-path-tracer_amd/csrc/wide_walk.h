@@ -1,0 +1,240 @@
+// wide_walk.h — culled closest-hit / any-hit walk over a 4-wide BVH built
+// from the reference's tree, for scenes in device memory.
+//
+// Why it returns the reference's hit.  traceRay (raytrace_comp.comp:159-204)
+// is an exhaustive DFS: a leaf's triangle is tested iff the leaf's box and
+// every ancestor's box pass intersectAABB, and the hit is the accepted
+// triangle of least t, ties going to the first visited.  For a ray whose
+// invDir = 1/dir is finite on all three axes (and a finite origin and
+// scene), every slab quantity (lo - o) * inv is NaN-free and monotone in lo,
+// so a box B' containing B bitwise gives t_near' <= t_near and t_far' >=
+// t_far, hence "B hit => B' hit".  The reference builder makes every parent
+// box the componentwise min/max over its subtree (BoundingVolumeHierarchy.cpp
+// :84-100), so a leaf passes its own test only if all its ancestors pass
+// theirs: the triangles the reference tests are exactly those whose LEAF box
+// passes.  The result is then the least t over those triangles with ties to
+// the least visit rank (the leaf's position in the right-first DFS order,
+// :198-199), and any walk that tests every such triangle that could still
+// win -- in any order, over any grouping of the boxes -- returns it bit for
+// bit.  Rays with an infinite/NaN invDir component (a zero or subnormal
+// direction component), or a direction longer than the cull bound assumes,
+// are handed back for the exact threaded walk (kNeedExact*); the host builds
+// the wide tree only after checking the containment on the uploaded arrays.
+//
+// The walk visits 4-wide nodes nearest child first and skips (culls) a child
+// box B when no triangle inside it can have t <= the current best t (closest
+// rays) or t < limit (shadow rays).  The cull test must be exact-safe, i.e.
+// hold for the t the reference's float Moller-Trumbore computes, not the
+// real intersection.  wide_bvh.cpp derives, per triangle, a bound of the
+// form
+//     tri accepted with t_comp <= b   =>   dist(o, B) <= A*b + C
+// from IEEE error bounds of every op of intersectTriangle (:114-157) under its
+// |det| >= 1e-6 acceptance test, with dist the Euclidean distance from the
+// origin to the box (the intersection point lies within rho of the triangle,
+// rho from the barycentric errors, and |X - o| = |T| |d|).  A node stores,
+// for its children, 1/A rounded down and C rounded up; a child is culled iff
+//     b < th,   th = (sqrt(0.999 * dist^2) - C) * (1/A)
+// with dist^2 computed from the slab test's own (lo - o), (hi - o).  The
+// 0.999 covers every rounding of this evaluation (hardware sqrt <= 1 ulp).
+// Culling never removes a triangle that could win or tie, so the answer is
+// the reference's.  tests/wide_check.cpp checks it against the exhaustive
+// walk on millions of rays (grazing, axis-aligned, inside-box origins).
+#pragma once
+#include "pt_isect.h"
+
+namespace ptd {
+
+// Node: 128 B = 8 float4 (one cache line):
+//   [0] lo.x[4] [1] hi.x[4] [2] lo.y[4] [3] hi.y[4] [4] lo.z[4] [5] hi.z[4]
+//   [6] child refs (int bits): >= 0 node index, < 0 ~rank of a leaf,
+//       kWideEmpty unused slot
+//   [7] {1/A (rounded down), C (rounded up), 0, 0}
+// Leaf boxes are the reference's leaf boxes bitwise.  Triangle records are
+// stored by rank (the reference tris layout, 3 float4), with rank -> slot.
+constexpr int kWideNodeF4 = 8;
+constexpr int32_t kWideEmpty = (int32_t)0x80000000;
+#ifndef PT_WIDE_LDS_STACK
+#define PT_WIDE_LDS_STACK 8
+#endif
+constexpr int kWideLds = PT_WIDE_LDS_STACK;   // stack entries per lane kept in LDS (power of two)
+static_assert((kWideLds & (kWideLds - 1)) == 0, "LDS stack entries: power of two");
+// hits[] markers: the ray needs the exact threaded walk (wide_ray_ok false,
+// or a stack bound violation, which the builder rules out)
+constexpr int kNeedExactClosest = -2;
+constexpr int kNeedExactShadow = 2;
+// direction-length guard of the cull bound: |d|^2 <= 1 + 2e-5 (computed)
+constexpr float kWideMaxD2 = 1.00002f;
+
+struct WideRay {
+  v3 o, d, inv;
+  float lim;    // closest: best t (1e30 = none yet); shadow: occlusion limit
+  int best;     // closest: rank of the best triangle (-1 none); shadow: 1 once occluded
+  int shadow;
+  int cur;      // node to expand next, -1 = take one from the stack
+  int sp, lo;   // entries on the stack; entries below lo live in the overflow area
+};
+
+PT_FN bool finite_(float x) { return fabs_(x) <= 3.40282347e38f; }
+
+// |coordinate| bound of origins and scene (the builder checks the scene):
+// keeps dist^2 finite in wide_child
+constexpr float kWideMaxCoord = 1e15f;
+
+PT_FN bool wide_ray_ok(v3 o, v3 d, v3 inv) {
+  return finite_(inv.x) && finite_(inv.y) && finite_(inv.z) && fabs_(o.x) <= kWideMaxCoord &&
+         fabs_(o.y) <= kWideMaxCoord && fabs_(o.z) <= kWideMaxCoord && dot(d, d) <= kWideMaxD2;
+}
+
+PT_FN float sqrt_lb_(float x) {
+#if PT_FAST_DEV
+  return __builtin_amdgcn_sqrtf(x);
+#else
+  return sqrt_(x);
+#endif
+}
+
+// One child box: the reference slab test (same ops as slab()), its t_near,
+// and the cull threshold th (culled iff lim < th).
+PT_FN void wide_child(const WideRay& R, float lx, float hx, float ly, float hy, float lz, float hz, float rA,
+                      float C, bool* hit, float* tn, float* th) {
+  const float dlx = lx - R.o.x, dly = ly - R.o.y, dlz = lz - R.o.z;
+  const float dhx = hx - R.o.x, dhy = hy - R.o.y, dhz = hz - R.o.z;
+  const float t0x = dlx * R.inv.x, t0y = dly * R.inv.y, t0z = dlz * R.inv.z;
+  const float t1x = dhx * R.inv.x, t1y = dhy * R.inv.y, t1z = dhz * R.inv.z;
+  const float tmin = fmax_(fmax_(fmin_(t0x, t1x), fmin_(t0y, t1y)), fmin_(t0z, t1z));
+  const float tmax = fmin_(fmin_(fmax_(t0x, t1x), fmax_(t0y, t1y)), fmax_(t0z, t1z));
+  *hit = tmin <= tmax && tmax >= 0.0f;
+  *tn = tmin;
+  const float gx = fmax_(fmax_(dlx, -dhx), 0.0f);
+  const float gy = fmax_(fmax_(dly, -dhy), 0.0f);
+  const float gz = fmax_(fmax_(dlz, -dhz), 0.0f);
+  const float d2 = fma_(gz, gz, fma_(gy, gy, gx * gx));
+  *th = (sqrt_lb_(d2 * 0.999f) - C) * rA;
+}
+
+PT_FN int2 wide_pop(WideRay& R, const int2* lds, int ls, const int2* ovf, long long os) {
+  --R.sp;
+  if (R.sp < R.lo) {
+    R.lo = R.sp;
+    return ovf[(long long)R.sp * os];
+  }
+  return lds[(R.sp & (kWideLds - 1)) * ls];
+}
+
+PT_FN void wide_push(WideRay& R, int2 e, int2* lds, int ls, int2* ovf, long long os) {
+  if (R.sp - R.lo == kWideLds) {   // LDS part full: its oldest entry moves to the overflow area
+    ovf[(long long)R.lo * os] = lds[(R.lo & (kWideLds - 1)) * ls];
+    ++R.lo;
+  }
+  lds[(R.sp & (kWideLds - 1)) * ls] = e;
+  ++R.sp;
+}
+
+PT_FN void wide_start(WideRay& R, v3 o, v3 d, bool shadow, float limit) {
+  R.o = o;
+  R.d = d;
+  R.inv = mk(rcp_(d.x), rcp_(d.y), rcp_(d.z));
+  R.shadow = shadow ? 1 : 0;
+  R.lim = shadow ? limit : 1e30f;
+  R.best = shadow ? 0 : -1;
+  R.cur = 0;   // the root node
+  R.sp = 0;
+  R.lo = 0;
+}
+
+// One node of the walk; true when the ray is finished (R.lim / R.best hold
+// the answer) or must be handed to the exact walk (*exact).  stack_cap: the
+// builder's bound on entries (overflow area size per lane).
+template <bool CNT>
+PT_FN bool wide_step(WideRay& R, const float4* __restrict__ nodes, const float4* __restrict__ tris, int2* lds,
+                     int ls, int2* ovf, long long os, int stack_cap, bool* exact, uint32_t* cn, uint32_t* cl) {
+  while (R.cur < 0) {
+    if (R.sp == 0) return true;
+    const int2 e = wide_pop(R, lds, ls, ovf, os);
+    if (!(R.lim < u2f((uint32_t)e.y))) R.cur = e.x;   // still able to hold a winner
+  }
+  const float4* nd = nodes + (size_t)R.cur * kWideNodeF4;
+  const float4 lx = nd[0], hx = nd[1], ly = nd[2], hy = nd[3], lz = nd[4], hz = nd[5], cf = nd[6], kf = nd[7];
+  if (CNT) ++*cn;
+  const int c0 = (int)f2u(cf.x), c1 = (int)f2u(cf.y), c2 = (int)f2u(cf.z),
+            c3 = (int)f2u(cf.w);
+  bool h0, h1, h2, h3;
+  float n0, n1, n2, n3, th0, th1, th2, th3;
+  wide_child(R, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, kf.x, kf.y, &h0, &n0, &th0);
+  wide_child(R, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, kf.x, kf.y, &h1, &n1, &th1);
+  wide_child(R, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, kf.x, kf.y, &h2, &n2, &th2);
+  wide_child(R, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, kf.x, kf.y, &h3, &n3, &th3);
+  h0 = h0 && c0 != kWideEmpty && !(R.lim < th0);
+  h1 = h1 && c1 != kWideEmpty && !(R.lim < th1);
+  h2 = h2 && c2 != kWideEmpty && !(R.lim < th2);
+  h3 = h3 && c3 != kWideEmpty && !(R.lim < th3);
+  // leaves: test their triangles now (reference accept rules, rank tie-break)
+  uint32_t lm = (h0 && c0 < 0 ? 1u : 0u) | (h1 && c1 < 0 ? 2u : 0u) | (h2 && c2 < 0 ? 4u : 0u) |
+                (h3 && c3 < 0 ? 8u : 0u);
+  while (lm) {
+    const int j = __builtin_ctz(lm);
+    lm &= lm - 1u;
+    const int r = ~(j == 0 ? c0 : j == 1 ? c1 : j == 2 ? c2 : c3);
+    const float thj = j == 0 ? th0 : j == 1 ? th1 : j == 2 ? th2 : th3;
+    if (R.lim < thj) continue;   // culled by a hit found in this node
+    if (CNT) ++*cl;
+    const float4* T = tris + 3 * (size_t)r;
+    float t;
+    if (tri_test(R.o, R.d, T[0], T[1], T[2], &t)) {
+      if (R.shadow) {
+        if (t < 1e30f && !(t >= R.lim)) {   // :359, :398
+          R.best = 1;
+          R.cur = -1;
+          R.sp = 0;
+          return true;
+        }
+      } else if (t < R.lim || (t == R.lim && r < R.best)) {   // :185 strict '<' in visit order
+        R.lim = t;
+        R.best = r;
+      }
+    }
+  }
+  // inner children still live: nearest first, the others onto the stack
+  // (liveness is kept in its own mask: a live t_near may overflow to +inf)
+  const uint32_t live = (h0 && c0 >= 0 && !(R.lim < th0) ? 1u : 0u) | (h1 && c1 >= 0 && !(R.lim < th1) ? 2u : 0u) |
+                        (h2 && c2 >= 0 && !(R.lim < th2) ? 4u : 0u) | (h3 && c3 >= 0 && !(R.lim < th3) ? 8u : 0u);
+  float k0 = (live & 1u) ? n0 : __builtin_inff();
+  float k1 = (live & 2u) ? n1 : __builtin_inff();
+  float k2 = (live & 4u) ? n2 : __builtin_inff();
+  float k3 = (live & 8u) ? n3 : __builtin_inff();
+  int s0 = 0, s1 = 1, s2 = 2, s3 = 3;
+#define PT_CE(ka, sa, kb, sb)          \
+  if (kb < ka) {                       \
+    const float tk = ka; ka = kb; kb = tk; \
+    const int ts = sa; sa = sb; sb = ts;   \
+  }
+  PT_CE(k0, s0, k1, s1)
+  PT_CE(k2, s2, k3, s3)
+  PT_CE(k0, s0, k2, s2)
+  PT_CE(k1, s1, k3, s3)
+  PT_CE(k1, s1, k2, s2)
+#undef PT_CE
+  const int n_live = __builtin_popcount(live);
+  R.cur = -1;
+  if (n_live == 0) return false;
+  if (R.sp + n_live - 1 > stack_cap) {   // cannot happen with the builder's bound; stay memory-safe
+    *exact = true;
+    return true;
+  }
+  // sorted slots s0..s3: push the live ones farthest first, expand the nearest
+  int first = -1;
+  for (int i = 3; i >= 0; --i) {
+    const int s = i == 0 ? s0 : i == 1 ? s1 : i == 2 ? s2 : s3;
+    if (!((live >> s) & 1u)) continue;
+    if (first >= 0) {
+      const int ref = first == 0 ? c0 : first == 1 ? c1 : first == 2 ? c2 : c3;
+      const float th = first == 0 ? th0 : first == 1 ? th1 : first == 2 ? th2 : th3;
+      wide_push(R, make_int2(ref, (int)f2u(th)), lds, ls, ovf, os);
+    }
+    first = s;
+  }
+  R.cur = first == 0 ? c0 : first == 1 ? c1 : first == 2 ? c2 : c3;
+  return false;
+}
+
+}  // namespace ptd

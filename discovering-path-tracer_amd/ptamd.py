@@ -28,6 +28,7 @@ PT_OPT_ITEM_ORDER = 8
 PT_OPT_LAUNCH_TIMING = 9
 PT_OPT_COUNT_TRACED = 10
 PT_OPT_PAIRS = 11
+PT_OPT_WIDE = 12
 KERNEL_AUTO, KERNEL_RECURSIVE, KERNEL_STATE_MACHINE, KERNEL_WAVEFRONT = 0, 1, 2, 3
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).
@@ -42,7 +43,7 @@ EXPORTS = [
     "pt_default_camera", "pt_primary_cull_rects", "pt_scene_save", "pt_scene_load_cache",
     "pt_progressive_camera", "pt_progressive_advance", "pt_readback_begin", "pt_readback_end", "pt_write_image",
     "pt_items_live", "pt_items_pack", "pt_items_unpack_all", "pt_render_packed", "pt_launch_span_ms",
-    "pt_set_partition_slots", "pt_get_traced", "pt_partition_items",
+    "pt_set_partition_slots", "pt_get_traced", "pt_wide_info", "pt_partition_items",
     "pt_dist_unique_id", "pt_dist_init", "pt_dist_run", "pt_dist_slot_floats", "pt_dist_finalize",
     "pt_dist_set_streams", "pt_dist_wait", "pt_dist_abort",
 ]
@@ -94,6 +95,7 @@ def lib():
             "pt_tiles_owned": ([vp, ctypes.POINTER(i32)], i32), "pt_tiles_pack": ([vp, vp], i32),
             "pt_tiles_unpack": ([vp, vp, i32, vp], i32), "pt_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
             "pt_reset_stats": ([vp], i32), "pt_get_traced": ([vp, ctypes.POINTER(Traced)], i32),
+            "pt_wide_info": ([vp, ctypes.POINTER(ctypes.c_int)], i32),
             "pt_partition_items": ([i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, psz, vp, psz, vp], i32),
             "pt_dist_unique_id": ([vp, sz], i32), "pt_dist_init": ([vp, vp, i32, i32], i32),
             "pt_dist_run": ([vp, u32, i32, i32, vp, i32], i32), "pt_dist_slot_floats": ([vp, psz], i32),
@@ -506,6 +508,14 @@ class Renderer:
         t = Traced()
         _check(lib().pt_get_traced(self._c, ctypes.byref(t)), "pt_get_traced")
         return {k: int(getattr(t, k)) for k, _ in Traced._fields_}
+
+    def wide_info(self):
+        """(wide nodes, stack bound) of the culled wide walk, or (0, 0, reason)."""
+        info = (ctypes.c_int * 2)()
+        _check(lib().pt_wide_info(self._c, info), "pt_wide_info")
+        if info[0] == 0:
+            return 0, 0, lib().pt_last_error().decode()
+        return info[0], info[1]
 
     def last_launch_ms(self):
         ms = ctypes.c_float()

@@ -318,6 +318,17 @@ int pt_dist_finalize(pt_context* ctx);
  * stack); 0 (default) = the threaded node walk, faster on the BASELINE
  * scenes.  Output is identical. */
 #define PT_OPT_PAIRS 11
+/* PT_OPT_WIDE: 1 (default) = the wavefront pipeline walks device-memory
+ * scenes over a 4-wide BVH of the reference's own boxes, nearest child first,
+ * culling children that cannot hold a hit at or before the best one found
+ * (the bound is exact-safe for the shader's float
+ * Moller-Trumbore, so every hit is the exhaustive DFS's bit for bit).  Built
+ * at upload when the tree's boxes contain their subtrees (any
+ * BoundingVolumeHierarchy.cpp tree does); pt_wide_info reports it.  0 = the
+ * threaded exhaustive walk; 2 = the wide walk with every odd ray of each
+ * round handed to the exact walk (tests the hand-back path).  Output is
+ * identical. */
+#define PT_OPT_WIDE 12
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */
@@ -343,6 +354,10 @@ int pt_set_stats_mode(pt_context* ctx, int enabled);
 int pt_get_stats(pt_context* ctx, pt_stats* out);
 int pt_reset_stats(pt_context* ctx);
 int pt_get_traced(pt_context* ctx, pt_traced* out);
+/* The culled wide walk of the uploaded scene (PT_OPT_WIDE): info[0] = wide
+ * nodes (0 = not built; pt_last_error() then says why), info[1] = the most
+ * stack entries one walk can hold. */
+int pt_wide_info(pt_context* ctx, int info[2]);
 /* Device time of the last pt_render/pt_dispatch launch, from HIP events
  * recorded on the launch stream. */
 int pt_last_launch_ms(pt_context* ctx, float* ms);

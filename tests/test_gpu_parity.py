@@ -755,11 +755,12 @@ def test_count_traced_mode(scene):
     W, H, nb = 160, 96, 4
     ref, ost = _oracle(v, i, n, W, H, nb=nb, cam=cam)
     counts = {}
-    for name, lds, kernel in (("lds", 2, 1), ("dev", 0, 1), ("wf", 0, 3)):
+    for name, lds, kernel, wide in (("lds", 2, 1, 0), ("dev", 0, 1, 0), ("wf", 0, 3, 0), ("wide", 0, 3, 1)):
         if scene == "sphere" and lds == 2:
             continue   # 5K triangles do not fit the LDS variant
         r = _setup(v, i, n, cam=cam, lds=lds)
         r.set_option(ptamd.PT_OPT_KERNEL, kernel)
+        r.set_option(ptamd.PT_OPT_WIDE, wide)
         r.set_option(ptamd.PT_OPT_COUNT_TRACED, 1)
         r.resize_and_clear(W, H)
         r.reset_stats()
@@ -778,6 +779,10 @@ def test_count_traced_mode(scene):
     # walk may run a few nodes past its occluder before the queue is tested
     assert counts["wf"]["nodes"] >= counts["dev"]["nodes"]
     assert counts["wf"]["tri_tests"] >= counts["dev"]["tri_tests"]
+    # the culled wide walk: 4-wide nodes, nearest first, culled past the best hit
+    assert counts["wide"]["nodes"] < counts["dev"]["nodes"]
+    if scene == "sphere":
+        assert counts["wide"]["tri_tests"] < counts["dev"]["tri_tests"]
     walks = first["closest_walks"] + first["shadow_walks"]
     assert 0 < walks < int(ost[0])
     assert 0 < first["nodes"] < int(ost[1])
@@ -820,3 +825,64 @@ def test_wavefront_pair_records(case):
     r.render(1, 3)
     ref, _ = _oracle(v, i, n, 72, 56, first=1, nb=3, cam=cam, lights=lights, int_bits=int_bits)
     _assert_same(r.read_accum(), ref, f"pair records case {case}")
+
+
+# ---- culled wide walk (PT_OPT_WIDE, wide_walk.h) ---------------------------
+
+def _wide_case(case):
+    if case == "sphere":
+        sv, si = scenes.displaced_sphere(4)
+        return sv, si, scenes.camera((0.0, 0.5, 3.0)), scenes.REFERENCE_LIGHT, False
+    if case == "cloud_int_bits":
+        sv, si = scenes.random_triangles(20000, seed=7)
+        return sv, si, scenes.camera((0.3, 0.2, 2.2)), scenes.REFERENCE_LIGHT, True
+    if case == "dense_cloud":
+        sv, si = scenes.random_triangles(50000, seed=9, spread=0.3, size=0.004)
+        return sv, si, scenes.camera((0.1, 0.2, 1.2)), scenes.REFERENCE_LIGHT, False
+    if case == "grid2lights":
+        sv, si = scenes.grid_mesh(6)
+        two = np.concatenate([scenes.REFERENCE_LIGHT,
+                              ptamd.pack_light([0.5, 0.5, 1.5], [0, 0, -1], [2, 4, 8], [0.5, 1.0])])
+        return sv, si, scenes.camera((0.0, 0.0, 3.0)), two, False
+    s = ptamd.Scene.load_obj(scenes.BOX_OBJ)   # "box": big triangles, nothing culled
+    v, i, _, _, _ = s.build_bvh().arrays()
+    return v, i, scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, False
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("case", ["sphere", "cloud_int_bits", "dense_cloud", "grid2lights", "box"])
+def test_wide_walk_matches_oracle(case, mode):
+    """The culled wide walk (wavefront pipeline, device-memory scene) gives the
+    oracle's frame bit for bit; mode 2 hands every odd ray of each round to
+    the exact threaded walk in the shading kernel (the path rays with a zero
+    direction component take)."""
+    sv, si, cam, lights, int_bits = _wide_case(case)
+    v, i, n, _, _ = ptamd.Scene.from_arrays(sv, si).build_bvh(int_bits=int_bits).arrays()
+    r = _setup(v, i, n, cam=cam, lights=lights, int_bits=int_bits, lds=0)
+    r.set_option(ptamd.PT_OPT_KERNEL, 3)
+    r.set_option(ptamd.PT_OPT_WIDE, mode)
+    info = r.wide_info()
+    assert info[0] > 0 and info[1] > 0, info
+    r.resize_and_clear(80, 52)
+    r.render(1, 4)
+    ref, _ = _oracle(v, i, n, 80, 52, first=1, nb=4, cam=cam, lights=lights, int_bits=int_bits)
+    _assert_same(r.read_accum(), ref, f"wide walk {case} mode {mode}")
+
+
+def test_wide_walk_refused_tree_keeps_exact_walk():
+    """A tree whose parent box does not contain a child's (not a
+    BoundingVolumeHierarchy.cpp tree) gets no wide walk: pt_wide_info says why,
+    and the frame (exact threaded walk) still equals the oracle's on the same
+    arrays."""
+    sv, si = scenes.displaced_sphere(3)
+    v, i, n, _, _ = ptamd.Scene.from_arrays(sv, si).build_bvh().arrays()
+    n = n.copy()
+    n[0, 0] = n[1, 0] + 0.05   # the root's min.x inside its right child's box
+    r = _setup(v, i, n, cam=scenes.camera((0.0, 0.5, 3.0)), lds=0)
+    info = r.wide_info()
+    assert info[0] == 0 and "contain" in info[2]
+    r.set_option(ptamd.PT_OPT_KERNEL, 3)
+    r.resize_and_clear(48, 40)
+    r.render(0, 2)
+    ref, _ = _oracle(v, i, n, 48, 40, nb=2, cam=scenes.camera((0.0, 0.5, 3.0)))
+    _assert_same(r.read_accum(), ref, "refused wide tree")

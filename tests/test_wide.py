@@ -1,0 +1,204 @@
+"""The culled wide-BVH walk (csrc/wide_walk.h) against the oracle's exhaustive
+traceRay (raytrace_comp.comp:159-204), on the CPU.
+
+tests/wide_check.cpp compiles the walk's own step function for the host and
+runs it ray by ray beside oracle_trace.  Every closest hit must have the
+oracle's t bits and triangle (normal bits), every shadow query its
+"!hit || t >= limit" answer (:359, :398).  The rays are chosen to stress the
+cull bound: grazing rays nearly in a triangle's plane (|det| near the 1e-6
+acceptance), origins on surfaces (the reference's +-1e-3 offsets), origins
+inside boxes, axis-parallel directions (handed to the exact walk), and
+shadow limits just around the hit distance.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_lib
+import scenes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "discovering-path-tracer_amd", "csrc")
+SO = os.path.join(ROOT, "tests", "_build", "libwide_check.so")
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        srcs = [os.path.join(ROOT, "tests", "wide_check.cpp"), os.path.join(CSRC, "scene", "wide_bvh.cpp")]
+        deps = srcs + [os.path.join(CSRC, f) for f in ("wide_walk.h", "pt_isect.h", "pt_math.h")]
+        oracle_lib.lib()   # builds liboracle.so if needed
+        if not os.path.exists(SO) or any(os.path.getmtime(d) > os.path.getmtime(SO) for d in deps):
+            os.makedirs(os.path.dirname(SO), exist_ok=True)
+            subprocess.check_call(
+                ["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-fPIC", "-shared", "-D__HIP_PLATFORM_AMD__",
+                 "-ffp-contract=off", "-fno-fast-math", "-I", CSRC, "-o", SO] + srcs +
+                ["-L", os.path.join(ROOT, "oracle"), "-loracle", "-Wl,-rpath," + os.path.join(ROOT, "oracle")])
+        L = ctypes.CDLL(SO)
+        F32P = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+        U32P = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+        U64P = np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")
+        I32P = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+        F64P = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+        sz = ctypes.c_size_t
+        L.wide_info.argtypes = [F32P, sz, U32P, sz, F32P, sz, ctypes.c_int, I32P, ctypes.c_char_p, sz]
+        L.wide_check.argtypes = [F32P, sz, U32P, sz, F32P, sz, ctypes.c_int, F32P, sz, F32P, U64P,
+                                 ctypes.c_char_p, sz]
+        L.wide_coeffs.argtypes = [F32P, F32P, F64P]
+        _LIB = L
+    return _LIB
+
+
+def _scene(v, i):
+    idx, nodes = oracle_lib.bvh_build(v, i)
+    return np.ascontiguousarray(v, np.float32), idx, nodes
+
+
+def check(v, idx, nodes, rays):
+    L = lib()
+    rays = np.ascontiguousarray(rays, np.float32)
+    n = rays.size // 8
+    out = np.zeros(4 * n, np.float32)
+    st = np.zeros(8, np.uint64)
+    err = ctypes.create_string_buffer(256)
+    rc = L.wide_check(v, v.size, idx, idx.size // 3, nodes, nodes.size // 8, 0, rays, n, out, st, err, 256)
+    assert rc == 0, err.value.decode()
+    return out.reshape(n, 4), st
+
+
+def _unit(a):
+    a = np.asarray(a, np.float32)
+    return (a / np.sqrt((a * a).sum(-1, keepdims=True))).astype(np.float32)
+
+
+def make_rays(v, idx, n, seed, lo=-1.2, hi=1.2):
+    """A mix of ray families (see the module docstring); n x 8 float32."""
+    rng = np.random.default_rng(seed)
+    V = v.reshape(-1, 3)
+    T = idx.reshape(-1, 3)
+    P = V[T]                                 # triangles x 3 x 3
+    e1, e2 = P[:, 1] - P[:, 0], P[:, 2] - P[:, 0]
+    nrm = _unit(np.cross(e1, e2))
+    out = []
+    k = n // 6
+    # 1. random origins in / around the scene, random directions
+    o = rng.uniform(lo * 1.5, hi * 1.5, (k, 3)).astype(np.float32)
+    out.append((o, _unit(rng.normal(size=(k, 3)))))
+    # 2. from a camera-like point outside towards random scene points
+    o = np.tile(np.float32([0.3, 0.2, 3.0]), (k, 1))
+    tgt = rng.uniform(lo, hi, (k, 3)).astype(np.float32)
+    out.append((o, _unit(tgt - o)))
+    # 3. from surface points (offset +-1e-3 along the normal, :355, :370) in random directions
+    t = rng.integers(0, len(T), k)
+    b = rng.dirichlet([1, 1, 1], k).astype(np.float32)
+    sp = (P[t] * b[:, :, None]).sum(1)
+    sgn = np.where(rng.random(k) < 0.5, 1e-3, -1e-3).astype(np.float32)[:, None]
+    out.append(((sp + nrm[t] * sgn).astype(np.float32), _unit(rng.normal(size=(k, 3)))))
+    # 4. grazing: nearly in a triangle's plane, aimed at it from far away
+    t = rng.integers(0, len(T), k)
+    b = rng.dirichlet([1, 1, 1], k).astype(np.float32)
+    tp = (P[t] * b[:, :, None]).sum(1)
+    inplane = _unit(np.cross(nrm[t], rng.normal(size=(k, 3))))
+    tilt = (10.0 ** rng.uniform(-7, -2, k)).astype(np.float32)[:, None] * np.where(rng.random((k, 1)) < .5, 1, -1)
+    d = _unit(inplane + nrm[t] * tilt)
+    dist = rng.uniform(0.01, 2.0, (k, 1)).astype(np.float32)
+    out.append(((tp - d * dist).astype(np.float32), d))
+    # 5. axis-parallel and nearly axis-parallel directions (exact hand-back / huge invDir)
+    o = rng.uniform(lo, hi, (k, 3)).astype(np.float32)
+    d = np.zeros((k, 3), np.float32)
+    ax = rng.integers(0, 3, k)
+    d[np.arange(k), ax] = np.where(rng.random(k) < 0.5, 1.0, -1.0)
+    tiny = rng.random(k) < 0.5
+    d[tiny] += rng.normal(size=(int(tiny.sum()), 3)).astype(np.float32) * np.float32(1e-30)
+    out.append((o, d))
+    # 6. from inside leaf boxes: triangle centroids, random directions
+    t = rng.integers(0, len(T), n - 5 * k)
+    out.append((P[t].mean(1).astype(np.float32), _unit(rng.normal(size=(n - 5 * k, 3)))))
+    o = np.concatenate([a for a, _ in out]).astype(np.float32)
+    d = np.concatenate([b for _, b in out]).astype(np.float32)
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = o
+    rays[:, 3:6] = d
+    return rays
+
+
+def run_scene(v, i, n_rays, seed):
+    v, idx, nodes = _scene(v, i)
+    rays = make_rays(v, idx, n_rays, seed)
+    out, st = check(v, idx, nodes, rays)     # closest
+    assert st[0] == 0, f"closest-hit mismatches: {int(st[0])} (first ray {int(st[7])}: {rays[int(st[7])]})"
+    # shadow queries with limits around the closest hit (and far / negative / NaN ones)
+    rng = np.random.default_rng(seed + 1)
+    sh = rays.copy()
+    sh[:, 6] = 1.0
+    t = out[:, 2]
+    hit = out[:, 3] > 0
+    jitter = rng.choice(np.float32([0.0, 1e-7, -1e-7, 1e-4, -1e-4, 0.1, -0.5]), len(t))
+    lim = np.where(hit, t * (np.float32(1) + jitter.astype(np.float32)), rng.uniform(0.1, 5, len(t)))
+    special = rng.random(len(t))
+    lim = np.where(special < 0.02, np.float32(np.nan), lim)
+    lim = np.where((special >= 0.02) & (special < 0.04), np.float32(-1.0), lim)
+    lim = np.where((special >= 0.04) & (special < 0.06), np.float32(1e30), lim)
+    sh[:, 7] = lim.astype(np.float32)
+    _, st2 = check(v, idx, nodes, sh)
+    assert st2[1] == 0, f"shadow mismatches: {int(st2[1])} (first ray {int(st2[7])}: {sh[int(st2[7])]})"
+    return st, st2
+
+
+def test_coefficients_bound_shape():
+    """Small triangles get tight relative bounds; huge ones give up culling."""
+    a = np.zeros(3, np.float64)
+    assert lib().wide_coeffs(np.float32([0.02, 0, 0]), np.float32([0, 0.02, 0.001]), a) == 0
+    assert 1.0 < a[0] < 1.01 and a[1] < 0.01 and a[2] < 1e-3
+    assert lib().wide_coeffs(np.float32([2, 0, 0]), np.float32([0, 2, 0]), a) == 1
+
+
+def test_wide_walk_random_cloud():
+    v, i = scenes.random_triangles(20000, seed=7)
+    st, st2 = run_scene(v, i, 60000, seed=11)
+    # far fewer node fetches than the exhaustive walk, never more triangle tests
+    assert st[3] < st[5] / 3, (int(st[3]), int(st[5]))
+    assert st[4] <= st[6], (int(st[4]), int(st[6]))
+    assert st[2] > 0   # axis-parallel rays went to the exact walk
+
+
+def test_wide_walk_displaced_sphere():
+    v, i = scenes.displaced_sphere(subdiv=4)
+    run_scene(v, i, 60000, seed=12)
+
+
+def test_wide_walk_grid_ties():
+    """Axis-aligned coplanar quads: equal t across triangles, tie-break by visit rank."""
+    v, i = scenes.grid_mesh(8)
+    run_scene(v, i, 40000, seed=13)
+
+
+def test_wide_walk_box_big_triangles():
+    v, i, _ = oracle_lib.obj_parse(open(scenes.BOX_OBJ, "rb").read())
+    run_scene(v, i, 40000, seed=14)
+
+
+def test_wide_walk_dense_tiny_cloud():
+    """A dense cloud of small triangles: many near-equal hit distances, and
+    culling cuts the triangle tests."""
+    v, i = scenes.random_triangles(30000, seed=9, spread=0.2, size=0.004)
+    st, _ = run_scene(v, i, 40000, seed=15)
+    assert st[4] < 0.8 * st[6], (int(st[4]), int(st[6]))
+
+
+def test_wide_info_and_refusals():
+    v, i = scenes.random_triangles(1000, seed=3)
+    v, idx, nodes = _scene(v, i)
+    info = np.zeros(2, np.int32)
+    err = ctypes.create_string_buffer(256)
+    L = lib()
+    assert L.wide_info(v, v.size, idx, idx.size // 3, nodes, nodes.size // 8, 0, info, err, 256) == 0
+    assert 0 < info[0] < 1000 and 1 < info[1] < 64
+    bad = nodes.copy().reshape(-1, 8)
+    bad[1, 0] = bad[0, 0] - 1.0   # a child box sticking out of the root
+    assert L.wide_info(v, v.size, idx, idx.size // 3, bad.reshape(-1), nodes.size // 8, 0, info, err, 256) == 1
+    assert b"contain" in err.value

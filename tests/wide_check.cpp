@@ -1,0 +1,146 @@
+// Test infrastructure: runs the culled wide walk (csrc/wide_walk.h, the same
+// code the GPU kernel runs, compiled for the host) over a batch of rays and
+// compares every answer with the oracle's exhaustive traceRay restatement
+// (oracle/pt_oracle.cpp, raytrace_comp.comp:159-204).  Built by
+// tests/test_wide.py with hipcc (host code only) and linked to liboracle.so.
+#include <stdio.h>
+#include <string.h>
+
+#include <vector>
+
+#include "scene/wide_bvh.h"
+#include "wide_walk.h"
+
+extern "C" void oracle_trace(const float* verts, const uint32_t* idx, const float* nodes, size_t n_nodes,
+                             const float* o3, const float* d3, float* out, uint64_t* counters);
+
+using namespace ptd;
+
+namespace {
+struct Built {
+  pt::WideBVH w;
+  std::vector<float4> tris;   // by rank: {v0, e1.x} {e1.yz, e2.xy} {e2.z, n}
+};
+
+std::string build(const float* V, size_t nvf, const uint32_t* I, size_t nt, const float* N, size_t nn, int int_bits,
+                  Built* b) {
+  std::string why = pt::build_wide_bvh(N, nn, int_bits != 0, V, nvf, I, nt, &b->w);
+  if (!why.empty()) return why;
+  b->tris.resize(3 * nt);
+  for (size_t r = 0; r < nt; ++r) {
+    const uint32_t t = (uint32_t)b->w.rank_tri[r];
+    v3 p[3];
+    for (int c = 0; c < 3; ++c) {
+      const uint32_t vi = I[3 * (size_t)t + c];
+      p[c] = mk(V[3 * vi], V[3 * vi + 1], V[3 * vi + 2]);
+    }
+    const v3 e1 = sub(p[1], p[0]), e2 = sub(p[2], p[0]);
+    const v3 n = normalize(cross(e1, e2));
+    b->tris[3 * r] = make_float4(p[0].x, p[0].y, p[0].z, e1.x);
+    b->tris[3 * r + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
+    b->tris[3 * r + 2] = make_float4(e2.z, n.x, n.y, n.z);
+  }
+  return "";
+}
+}  // namespace
+
+extern "C" {
+
+// info[0] wide nodes, info[1] stack bound.  Returns 0, or 1 with the reason in err.
+int wide_info(const float* V, size_t nvf, const uint32_t* I, size_t nt, const float* N, size_t nn, int int_bits,
+              int* info, char* err, size_t errlen) {
+  Built b;
+  const std::string why = build(V, nvf, I, nt, N, nn, int_bits, &b);
+  if (!why.empty()) {
+    snprintf(err, errlen, "%s", why.c_str());
+    return 1;
+  }
+  info[0] = b.w.n_nodes;
+  info[1] = b.w.stack_cap;
+  return 0;
+}
+
+// rays: n x 8 floats {o.xyz, d.xyz, kind (0 closest, 1 shadow), limit}.
+// out: n x 4 {wide t|lim, wide hit/occluded (-1 exact walk needed), oracle t, oracle hit/occluded}.
+// stats: [0] closest mismatches [1] shadow mismatches [2] exact hand-backs
+// [3] wide nodes [4] wide triangle tests [5] oracle nodes [6] oracle leaf tests
+// [7] first mismatching ray (or ~0).  Returns 0 or 1 (err).
+int wide_check(const float* V, size_t nvf, const uint32_t* I, size_t nt, const float* N, size_t nn, int int_bits,
+               const float* rays, size_t n, float* out, uint64_t* stats, char* err, size_t errlen) {
+  Built b;
+  const std::string why = build(V, nvf, I, nt, N, nn, int_bits, &b);
+  if (!why.empty()) {
+    snprintf(err, errlen, "%s", why.c_str());
+    return 1;
+  }
+  std::vector<int2> lds(kWideLds), ovf((size_t)b.w.stack_cap + 1);
+  memset(stats, 0, 8 * sizeof(uint64_t));
+  stats[7] = ~0ull;
+  const float4* nodes = (const float4*)b.w.nodes.data();
+  for (size_t i = 0; i < n; ++i) {
+    const float* r = rays + 8 * i;
+    const v3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
+    const bool shadow = r[6] != 0.0f;
+    float ref[8];
+    uint64_t oc[3] = {0, 0, 0};
+    oracle_trace(V, I, N, nn, r, r + 3, ref, oc);
+    stats[5] += oc[1];
+    stats[6] += oc[2];
+    const bool ohit = ref[0] != 0.0f;
+    const float lim = r[7];
+    WideRay R;
+    wide_start(R, o, d, shadow, lim);
+    float wt = 0.0f, wres = -1.0f;
+    bool exact = !wide_ray_ok(R.o, R.d, R.inv);
+    uint32_t cn = 0, cl = 0;
+    if (!exact) {
+      while (!wide_step<true>(R, nodes, b.tris.data(), lds.data(), 1, ovf.data(), 1, b.w.stack_cap, &exact, &cn,
+                              &cl)) {
+      }
+    }
+    stats[3] += cn;
+    stats[4] += cl;
+    out[4 * i + 2] = ref[1];
+    if (exact) {
+      stats[2]++;
+      out[4 * i] = 0.0f;
+      out[4 * i + 1] = -1.0f;
+      out[4 * i + 3] = ohit ? 1.0f : 0.0f;
+      continue;
+    }
+    bool bad;
+    if (shadow) {
+      const bool occ_ref = ohit && !(ref[1] >= lim);   // :359 !hit || t >= dist - OFFSET
+      wt = R.lim;
+      wres = R.best ? 1.0f : 0.0f;
+      out[4 * i + 3] = occ_ref ? 1.0f : 0.0f;
+      bad = (R.best != 0) != occ_ref;
+      if (bad) stats[1]++;
+    } else {
+      wt = R.lim;
+      wres = R.best >= 0 ? 1.0f : 0.0f;
+      out[4 * i + 3] = ohit ? 1.0f : 0.0f;
+      bad = (R.best >= 0) != ohit;
+      if (!bad && ohit) {
+        // same t bits and the same triangle (its geometric normal, :189)
+        const float4* T = &b.tris[3 * (size_t)R.best];
+        const v3 e1 = mk(T[0].w, T[1].x, T[1].y), e2 = mk(T[1].z, T[1].w, T[2].x);
+        const v3 nn3 = normalize(cross(e1, e2));
+        bad = memcmp(&R.lim, &ref[1], 4) != 0 || memcmp(&nn3.x, &ref[5], 4) != 0 ||
+              memcmp(&nn3.y, &ref[6], 4) != 0 || memcmp(&nn3.z, &ref[7], 4) != 0;
+      }
+      if (bad) stats[0]++;
+    }
+    if (bad && stats[7] == ~0ull) stats[7] = i;
+    out[4 * i] = wt;
+    out[4 * i + 1] = wres;
+  }
+  return 0;
+}
+
+// The per-triangle cull coefficients (wide_tri_coeffs) for the bound test.
+int wide_coeffs(const float* e1, const float* e2, double* abc) {
+  return pt::wide_tri_coeffs(e1, e2, &abc[0], &abc[1], &abc[2]) ? 0 : 1;
+}
+
+}  // extern "C"
