@@ -2070,7 +2070,7 @@ __global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_ker
 // occluded).
 // ---------------------------------------------------------------------------
 #ifndef PT_WIDE_MIN_BLOCKS
-#define PT_WIDE_MIN_BLOCKS 6
+#define PT_WIDE_MIN_BLOCKS 8   // 64 VGPRs (56 B spilled): 10M cloud -7.5 %, sphere -1.5 % vs 6 (76 VGPRs); 7: between
 #endif
 template <int G, bool CNT = false>
 __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(RenderParams P, WfBuffers B,

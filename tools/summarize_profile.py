@@ -22,7 +22,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BOX_KERNEL = "render_kernel<false, true, false>"
-WF_KERNELS = ("wf_gen_kernel", "wf_trace_kernel", "wf_shade_kernel", "wf_fold_kernel", "fill_culled_kernel")
+WF_KERNELS = ("wf_gen_kernel", "wf_trace_kernel", "wf_trace_wide_kernel", "wf_trace_pairs_kernel", "wf_shade_kernel",
+              "wf_fold_kernel", "fill_culled_kernel")
 
 
 def main(tag, workload, frames):
