@@ -84,10 +84,17 @@ def load_scene(name):
     raise SystemExit(f"unknown scene {name}")
 
 
+KERNEL_SOURCES = ("pt_device.hip", "pt_device.h", "pt_isect.h", "wide_walk.h", "pt_math.h")
+
+
 def kernel_sha1():
+    """SHA-1 of the kernel source (pt_device.hip and the headers its kernels
+    are built from), as tools/summarize_profile.py records it."""
     import hashlib
-    src = os.path.join(ROOT, "discovering-path-tracer_amd", "csrc", "pt_device.hip")
-    return hashlib.sha1(open(src, "rb").read()).hexdigest()
+    h = hashlib.sha1()
+    for f in KERNEL_SOURCES:
+        h.update(open(os.path.join(ROOT, "discovering-path-tracer_amd", "csrc", f), "rb").read())
+    return h.hexdigest()
 
 
 def profiled_traffic(workload=None):
@@ -240,14 +247,20 @@ def roofline_block(prof, time_ms, alg_bytes, kernel, kernel_ms, interval_ms, n_t
     return out
 
 
-LEG_WORKLOADS = {"sphere": "sphere_1080p8", "synthetic:10000000": "synthetic10M_1080p8"}
+# the BASELINE configs the default run reports beside the headline, one GPU
+# each: (key, scene, W, H, spp, MAX_DEPTH, timed frames, profile workload)
+SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 3, "sphere_1080p8"),
+              ("config4", "sphere", 3840, 2160, 16, 8, 1, "sphere_4k16_d8"),
+              ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 1, "synthetic10M_1080p8"))
 
 
-def scene_leg(scene_name, W, H, spp, depth, sss, steps, device):
+def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaustive_too=False):
     """One BASELINE config on one GPU (N = 1 only): the reference rays of a
     stats-mode frame, the walks of a counting frame, `steps` timed frames
     after one warmup, and the roofline priced from the committed profile of
-    this workload (tools/gpu_scene_profile.sh)."""
+    this workload (tools/profile_workload.sh).  exhaustive_too: one more frame
+    with PT_OPT_WIDE 0 -- the threaded exhaustive walk, the reference's own
+    traversal shape -- reported as `exhaustive_walk` (workload + "_exhaustive")."""
     import ptamd
     import scenes
     import torch
@@ -280,7 +293,7 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device):
     kt = r.launch_times_ms()
     kernel_ms = float(np.mean(kt)) if kt.size else float("nan")
     alg = algorithmic_bytes({"nodes": ref[1], "leaf_tests": ref[2], "samples": ref[3]})
-    prof = profiled_traffic(LEG_WORKLOADS[scene_name])
+    prof = profiled_traffic(workload)
     cfg = {"workload": f"{desc} {W}x{H} {spp}spp {depth} bounces {sss} sss", "triangles": int(ntri),
            "int_bits_nodes": bool(int_bits), "rays_per_frame": int(ref[0])}
     add_traced(cfg, traced, dt)
@@ -291,6 +304,23 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device):
                                       kernel_ms, int(kt.size), "kernel_ms (HIP events around each frame's "
                                                                "launches on the render stream)"),
            "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
+    if exhaustive_too:
+        r.set_option(ptamd.PT_OPT_WIDE, 0)
+        r.reset_launch_times()
+        t0 = time.perf_counter()
+        r.render(0, spp)
+        r.synchronize()
+        dt0 = time.perf_counter() - t0
+        kt0 = r.launch_times_ms()
+        k0 = float(np.mean(kt0)) if kt0.size else float("nan")
+        name0 = "wavefront pipeline, threaded exhaustive walk (PT_OPT_WIDE 0), per frame"
+        out["exhaustive_walk"] = {
+            "value": round(ref[0] / dt0 / 1e6, 3), "unit": "Mrays/s", "ms_per_step": round(dt0 * 1e3, 2),
+            "steps": 1, "note": "the reference's traversal shape (every box a ray passes, visit order kept); "
+                                "same frame bit for bit",
+            "roofline": roofline_block(profiled_traffic(workload + "_exhaustive"), k0, alg, name0, k0, k0,
+                                       int(kt0.size), "kernel_ms (HIP events around the frame's launches)")}
+        r.set_option(ptamd.PT_OPT_WIDE, 1)
     del r
     return out
 
@@ -862,9 +892,10 @@ def main():
         if world == 1 and emu == 1 and default_cfg and not (args.no_scene_legs or args.profile_run or args.packed):
             del r
             out_line["configs"] = {}
-            for key, scene_name, steps in (("config3", "sphere", 3), ("config5", "synthetic:10000000", 1)):
-                print(f"bench: {key} leg ({scene_name})", file=sys.stderr, flush=True)
-                out_line["configs"][key] = scene_leg(scene_name, W, H, SPP, DEPTH, SSS, steps, device)
+            for key, scene_name, lw, lh, lspp, ldepth, steps, workload in SCENE_LEGS:
+                print(f"bench: {key} leg ({scene_name} {lw}x{lh} {lspp}spp D{ldepth})", file=sys.stderr, flush=True)
+                out_line["configs"][key] = scene_leg(scene_name, lw, lh, lspp, ldepth, SSS, steps, device, workload,
+                                                     exhaustive_too=key == "config5")
         print(json.dumps(out_line), flush=True)
     if dist is not None:
         dist.barrier()

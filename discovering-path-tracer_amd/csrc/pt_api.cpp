@@ -714,6 +714,7 @@ int upload_ints(const std::vector<int>& h, int** d, size_t* cap) {
 // (4.3 GB) are kept per launch; more batches run in chunks of that size.
 constexpr long long kWfMaxPaths = 1ll << 24;
 constexpr int kWfAutoTris = 32768;
+constexpr int kWfWideAutoTris = 16384;   // ... with the culled wide walk (render_impl)
 // The root's assembly table for frames rendered with params p: per rank its
 // live items {rank, tile*8 + part, slot} and its culled items {rank, tile*8 + part, -1}.
 int unpack_table(pt_context* c, const ptd::RenderParams& p, const std::vector<float>& key) {
@@ -874,9 +875,16 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   // sphere 550 -> 465, 100K cloud 113 -> 77; 1M cloud 2 spp 225 -> 236; a 1/8
   // tile share of the 10M cloud: 1 spp (259K paths) 147 -> 273, 8 spp (2M)
   // 742 -> 669; box 0.38 -> 8.4.
+  // With the culled wide walk (PT_OPT_WIDE) the wavefront pipeline wins from
+  // 2^20 paths on (1080p, ms recursive -> wavefront): displaced sphere 82K
+  // 1 spp 89.9 -> 39.6, 8 spp 498 -> 139, its 1/8 tile share 89.0 -> 39.1;
+  // 20K sphere 2 spp 29.6 -> 23.3; 1M cloud 1 spp 108 -> 47.5; a sparse 100K
+  // cloud at 1 spp (most rays miss) loses 14.3 -> 15.9.
   const long long paths = (long long)p.n_tiles * 256 * n_batches;
-  const bool wf_auto = c->n_tris >= kWfAutoTris && paths >= (1ll << 20) &&
-                       (c->n_tris >= (1 << 20) || paths >= (1ll << 23));
+  const bool wide_walk = c->opt_wide && c->n_wide > 0 && !c->opt_pairs;
+  const bool wf_auto = wide_walk ? c->n_tris >= kWfWideAutoTris && paths >= (1ll << 20)
+                                 : c->n_tris >= kWfAutoTris && paths >= (1ll << 20) &&
+                                       (c->n_tris >= (1 << 20) || paths >= (1ll << 23));
   const bool wf = c->opt_kernel == 3 || (c->opt_kernel == 0 && !lds && !c->stats_mode && wf_auto);
   if (wf && c->stats_mode) return fail(PT_ERR_UNSUPPORTED, "stats mode runs the path-recursive kernel only");
   if (sm) p.spl = 1;

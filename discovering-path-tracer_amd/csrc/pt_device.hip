@@ -2082,6 +2082,9 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
   const int wave = tid >> 6, lane = tid & 63;
   __shared__ int2 stk[4][kWideLds][64];
   int2* lds = &stk[wave][0][lane];
+  __shared__ int cq[PT_WIDE_QUEUE ? 4 : 1][PT_WIDE_QUEUE ? kWideQ : 1][64];
+  int* cand = PT_WIDE_QUEUE ? &cq[wave][0][lane] : nullptr;
+  bool fin = false;
   const long long os = (long long)gridDim.x * 256;
   int2* ovf = P.wide_ovf + ((long long)blockIdx.x * 256 + tid);
   const float4* __restrict__ rays = B.rays[cur];
@@ -2090,6 +2093,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
   WideRay R;
   R.cur = -1;
   R.sp = R.lo = 0;
+  R.nc = 0;
   Ctr c = {0u, 0u, 0u, 0u, 0u};
   for (;;) {
     const unsigned long long idle = __ballot(p < 0);
@@ -2124,14 +2128,40 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
     if (!more && __ballot(p >= 0) == 0ull) break;
     for (int it = 0; it < PT_WF_STEPS; ++it) {
       bool exact = false;
-      if (p >= 0 && wide_step<CNT>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
-                                   &c.leaves)) {
-        int res;
-        if (exact) res = R.shadow ? kNeedExactShadow : kNeedExactClosest;
-        else if (R.shadow) res = R.best;
-        else res = R.best >= 0 ? P.wide_tri_of[R.best] : -1;
-        B.hits[p] = make_float2(R.lim, __int_as_float(res));
-        p = -1;
+      if (!PT_WIDE_QUEUE) {
+        if (p >= 0 && wide_step<CNT>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
+                                     &c.leaves)) {
+          int res;
+          if (exact) res = R.shadow ? kNeedExactShadow : kNeedExactClosest;
+          else if (R.shadow) res = R.best;
+          else res = R.best >= 0 ? P.wide_tri_of[R.best] : -1;
+          B.hits[p] = make_float2(R.lim, __int_as_float(res));
+          p = -1;
+        }
+      } else {
+        // fin: the walk has no node left (its queue may still hold candidates)
+        if (p >= 0 && !fin)
+          fin = wide_step<CNT, true>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
+                                     &c.leaves, cand);
+        if (exact) {
+          R.nc = 0;
+          B.hits[p] = make_float2(R.lim, __int_as_float(R.shadow ? kNeedExactShadow : kNeedExactClosest));
+          p = -1;
+          fin = false;
+        }
+        if (__ballot(p >= 0 && R.nc > 0 && (fin || R.nc > kWideQ - 4))) {   // wave-uniform flush
+          if (p >= 0 && R.nc > 0 && wide_flush<CNT>(R, P.wide_tris, cand, &c.leaves)) {
+            fin = true;   // occluded
+            R.sp = 0;
+            R.cur = -1;
+          }
+        }
+        if (p >= 0 && fin && R.nc == 0) {
+          const int res = R.shadow ? R.best : (R.best >= 0 ? P.wide_tri_of[R.best] : -1);
+          B.hits[p] = make_float2(R.lim, __int_as_float(res));
+          p = -1;
+          fin = false;
+        }
       }
     }
   }

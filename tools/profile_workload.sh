@@ -4,7 +4,7 @@
 # own (they cannot share one on gfx950), plus VALU/SALU instruction counts,
 # then tools/summarize_profile.py -> profiles/<TAG>/<WORKLOAD>_summary.json,
 # which bench.py prices its roofline from (matched by kernel SHA and workload).
-#   TAG=r02b WORKLOAD=box|sphere_1080p8|synthetic10M_1080p8 tools/profile_workload.sh
+#   TAG=r02b WORKLOAD=box|sphere_1080p8|sphere_4k16_d8|synthetic10M_1080p8[_exhaustive] tools/profile_workload.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -14,6 +14,8 @@ case $WORKLOAD in
   box) ARGS="--steps 20 --warmup 2"; STEPS=20; WARM=2 ;;
   sphere_1080p8) ARGS="--scene sphere --steps 2 --warmup 1"; STEPS=2; WARM=1 ;;
   synthetic10M_1080p8) ARGS="--scene synthetic:10000000 --steps 1 --warmup 1"; STEPS=1; WARM=1 ;;
+  synthetic10M_1080p8_exhaustive) ARGS="--scene synthetic:10000000 --steps 1 --warmup 1 --opt 12=0"; STEPS=1; WARM=1 ;;
+  sphere_4k16_d8) ARGS="--scene sphere --width 3840 --height 2160 --spp 16 --depth 8 --steps 1 --warmup 1"; STEPS=1; WARM=1 ;;
   *) echo "unknown WORKLOAD $WORKLOAD"; exit 2 ;;
 esac
 OUT=gpurun_out/prof_${TAG}_${WORKLOAD}

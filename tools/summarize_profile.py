@@ -22,6 +22,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BOX_KERNEL = "render_kernel<false, true, false>"
+KERNEL_SOURCES = ("pt_device.hip", "pt_device.h", "pt_isect.h", "wide_walk.h", "pt_math.h")   # == bench.py
 WF_KERNELS = ("wf_gen_kernel", "wf_trace_kernel", "wf_trace_wide_kernel", "wf_trace_pairs_kernel", "wf_shade_kernel",
               "wf_fold_kernel", "fill_culled_kernel")
 
@@ -62,8 +63,11 @@ def main(tag, workload, frames):
     pmc.update(per_launch(os.path.join(src, "pmc_WRITE_SIZE", "run_counter_collection.csv"), ("WRITE_SIZE",)))
     sq = per_launch(os.path.join(src, "pmc_SQ_INSTS_VALU", "run_counter_collection.csv"),
                     ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"))
-    src_hash = hashlib.sha1(open(os.path.join(ROOT, "discovering-path-tracer_amd", "csrc", "pt_device.hip"),
-                                 "rb").read()).hexdigest()
+    # the kernel source: pt_device.hip and the headers its kernels are built from
+    h = hashlib.sha1()
+    for name in KERNEL_SOURCES:
+        h.update(open(os.path.join(ROOT, "discovering-path-tracer_amd", "csrc", name), "rb").read())
+    src_hash = h.hexdigest()
     if box:
         ns = [v["avg_ns"] for k, v in kern.items() if BOX_KERNEL in k]
         kernel_ms = ns[0] / 1e6 if ns else None
