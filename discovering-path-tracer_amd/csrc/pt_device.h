@@ -182,7 +182,7 @@ struct WfBuffers {
   int* ids[2];       // work lists: path id per slot
   float4* rays[2];   // ... and its ray, 2 float4 per slot: {o.xyz, limit} {d.xyz, shadow}
   float2* hits;      // per slot of the list being traced: {t, tri bits / occluded}
-  int* counters;     // [0],[1] list sizes, [2] trace fetch cursor
+  int* counters;     // [0],[1] list sizes, [2] trace fetch cursor ([4..6]: the second half's, two streams)
   long long cap;     // paths the buffers hold
 };
 constexpr int kWfStateF4 = 10;
@@ -193,8 +193,12 @@ constexpr size_t kWfBytesPerPath = (size_t)kWfStateF4 * 16 + 16 + 2 * (4 + 32) +
 inline int wf_max_rays(const RenderParams& p) {
   return 1 + p.max_depth * (p.n_lights + p.sss_bounces * (1 + p.n_lights) + 1);
 }
+// stream2 (with two events): the chunk's pixels run as two halves on stream
+// and stream2 (forked from and joined back into stream); the wide walk's
+// overflow area then holds two sets of wide_ovf_lanes lanes.
 hipError_t launch_wavefront(const RenderParams& p, const WfBuffers& b, bool lds_scene, hipStream_t stream,
-                            bool cnt = false);
+                            bool cnt = false, hipStream_t stream2 = nullptr, hipEvent_t ev_fork = nullptr,
+                            hipEvent_t ev_join = nullptr);
 // lanes of the wide walk's persistent grid on this device (overflow areas to allocate)
 long long wide_trace_lanes();
 // triangle records by rank: dst[r] = tris[tri_of[r]]

@@ -1646,11 +1646,11 @@ __device__ __forceinline__ bool pixel_live(const RenderParams& P, float ndcX0, f
 
 // Ray generation + shading up to the primary trace (path_step from PH_BEGIN).
 template <bool CNT>
-__global__ __launch_bounds__(256) void wf_gen_kernel(RenderParams P, WfBuffers B, long long n) {
-  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+__global__ __launch_bounds__(256) void wf_gen_kernel(RenderParams P, WfBuffers B, long long n, long long g0) {
+  const long long g = g0 + (long long)blockIdx.x * 256 + threadIdx.x;   // paths [g0, g0 + n)
   bool need = false, gen = false;
   Trav T;
-  if (g < n) {
+  if (g - g0 < n) {
     const long long pp = g / (long long)P.n_batches;
     CamFrame F;
     if (wf_pixel(P, pp, &F.px, &F.py)) {
@@ -2069,6 +2069,9 @@ __global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_ker
 // kNeedExact* and wf_shade_kernel walks them exactly (trace_closest /
 // occluded).
 // ---------------------------------------------------------------------------
+#ifndef PT_WIDE_FLUSH_T
+#define PT_WIDE_FLUSH_T 1
+#endif
 #ifndef PT_WIDE_MIN_BLOCKS
 #define PT_WIDE_MIN_BLOCKS 8   // 64 VGPRs (56 B spilled): 10M cloud -7.5 %, sphere -1.5 % vs 6 (76 VGPRs); 7: between
 #endif
@@ -2149,7 +2152,26 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
           p = -1;
           fin = false;
         }
-        if (__ballot(p >= 0 && R.nc > 0 && (fin || R.nc > kWideQ - 4))) {   // wave-uniform flush
+        // wave-uniform flush: a queue that cannot take another node's four
+        // leaves, or PT_WIDE_FLUSH_T finished walks waiting on their queue,
+        // or nothing left walking
+        const unsigned long long waiting = __ballot(p >= 0 && fin && R.nc > 0);
+#ifdef PT_WIDE_PROBE   // lane-state census per step (traced counters 0-4: walking, idle, waiting, steps, flushes)
+        {
+          const unsigned long long walking = __ballot(p >= 0 && !fin), idle_l = __ballot(p < 0);
+          const unsigned long long fl = __ballot(p >= 0 && R.nc > kWideQ - 4) || (int)__popcll(waiting) >= PT_WIDE_FLUSH_T ||
+                                        (waiting && walking == 0ull);
+          if (lane == 0) {
+            atomicAdd(&P.stats[4], (unsigned long long)__popcll(walking));
+            atomicAdd(&P.stats[5], (unsigned long long)__popcll(idle_l));
+            atomicAdd(&P.stats[6], (unsigned long long)__popcll(waiting));
+            atomicAdd(&P.stats[7], 1ull);
+            atomicAdd(&P.stats[8], fl ? 1ull : 0ull);
+          }
+        }
+#endif
+        if (__ballot(p >= 0 && R.nc > kWideQ - 4) || (int)__popcll(waiting) >= PT_WIDE_FLUSH_T ||
+            (waiting && __ballot(p >= 0 && !fin) == 0ull)) {
           if (p >= 0 && R.nc > 0 && wide_flush<CNT>(R, P.wide_tris, cand, &c.leaves)) {
             fin = true;   // occluded
             R.sp = 0;
@@ -2248,9 +2270,9 @@ __global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers
 }
 
 // Running mean (:467-469) of each pixel's samples, in batch order.
-__global__ __launch_bounds__(256) void wf_fold_kernel(RenderParams P, WfBuffers B, long long n_pix) {
-  const long long pp = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (pp >= n_pix) return;
+__global__ __launch_bounds__(256) void wf_fold_kernel(RenderParams P, WfBuffers B, long long n_pix, long long pp0) {
+  const long long pp = pp0 + (long long)blockIdx.x * 256 + threadIdx.x;   // pixels [pp0, pp0 + n_pix)
+  if (pp - pp0 >= n_pix) return;
   int px, py;
   if (!wf_pixel(P, pp, &px, &py)) return;
   float4* dst = P.accum + (size_t)py * (size_t)P.width + (size_t)px;
@@ -2392,7 +2414,8 @@ long long wide_trace_lanes() {
   return (long long)cus * std::max(most, 1) * 256;
 }
 
-hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds_scene, hipStream_t stream, bool cnt) {
+hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds_scene, hipStream_t stream, bool cnt,
+                            hipStream_t stream2, hipEvent_t ev_fork, hipEvent_t ev_join) {
   if (p0.spl != 1 && p0.spl != 2 && p0.spl != 4 && p0.spl != 8) return hipErrorInvalidValue;
   if (p0.n_batches == 0) return hipSuccess;
   const int per = 256 / p0.spl;
@@ -2441,24 +2464,59 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
   const unsigned grid_s = (unsigned)(cus * (per_cu_s > 0 ? per_cu_s : 1));
   const uint32_t chunk = (uint32_t)std::min<long long>((long long)p0.n_batches, b.cap / px);
   const int iters = wf_max_rays(p0);
+  // Two halves of the chunk's pixels on two streams (PT_OPT_WF_STREAMS):
+  // each trace launch ends in a tail where most lanes are out of rays
+  // (lane census: ~50 % of lane-steps idle), which the other half's trace
+  // and shading fill.  The halves share the path state (disjoint ranges)
+  // and get their own lists, counters and stack overflow areas.
+  const bool split = stream2 && px >= 2 * 4096;
+  const int H = split ? 2 : 1;
   for (uint32_t b0 = 0; b0 < p0.n_batches; b0 += chunk) {
     RenderParams p = p0;
     p.first_batch = p0.first_batch + b0;
     p.n_batches = std::min(chunk, p0.n_batches - b0);
-    const long long n = px * p.n_batches;
-    e = hipMemsetAsync(b.counters, 0, 3 * sizeof(int), stream);
-    if (e != hipSuccess) return e;
-    if (cnt)
-      wf_gen_kernel<true><<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(p, b, n);
-    else
-      wf_gen_kernel<false><<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(p, b, n);
+    RenderParams ph[2] = {p, p};
+    WfBuffers bh[2] = {b, b};
+    hipStream_t sh[2] = {stream, split ? stream2 : stream};
+    long long px0[2] = {0, 0}, pxn[2] = {px, 0};
+    if (split) {
+      pxn[0] = (px / 2 + 255) / 256 * 256;
+      pxn[1] = px - pxn[0];
+      px0[1] = pxn[0];
+      const long long sb = pxn[0] * p.n_batches;   // half 1's paths and list slots start here
+      for (int k = 0; k < 2; ++k) {
+        bh[1].rays[k] = b.rays[k] + 2 * sb;
+        bh[1].ids[k] = b.ids[k] + sb;
+      }
+      bh[1].hits = b.hits + sb;
+      bh[1].counters = b.counters + 4;
+      ph[1].wide_ovf = p.wide_ovf ? p.wide_ovf + (size_t)p.wide_ovf_lanes * (size_t)p.wide_stack : nullptr;
+      e = hipEventRecord(ev_fork, stream);
+      if (e == hipSuccess) e = hipStreamWaitEvent(stream2, ev_fork, 0);
+      if (e != hipSuccess) return e;
+    }
+    for (int h = 0; h < H; ++h) {
+      const long long n = pxn[h] * p.n_batches;
+      e = hipMemsetAsync(bh[h].counters, 0, 3 * sizeof(int), sh[h]);
+      if (e != hipSuccess) return e;
+      if (cnt)
+        wf_gen_kernel<true><<<(unsigned)((n + 255) / 256), 256, 0, sh[h]>>>(ph[h], bh[h], n, px0[h] * p.n_batches);
+      else
+        wf_gen_kernel<false><<<(unsigned)((n + 255) / 256), 256, 0, sh[h]>>>(ph[h], bh[h], n, px0[h] * p.n_batches);
+    }
     int cur = 0;
     for (int it = 0; it < iters; ++it) {
-      hipLaunchKernelGGL(trace, dim3(grid_t), dim3(256), lds_t, stream, p, b, cur);
-      wf_shade_kernel<<<grid_s, 256, 0, stream>>>(p, b, cur);
+      for (int h = 0; h < H; ++h) hipLaunchKernelGGL(trace, dim3(grid_t), dim3(256), lds_t, sh[h], ph[h], bh[h], cur);
+      for (int h = 0; h < H; ++h) wf_shade_kernel<<<grid_s, 256, 0, sh[h]>>>(ph[h], bh[h], cur);
       cur ^= 1;
     }
-    wf_fold_kernel<<<(unsigned)((px + 255) / 256), 256, 0, stream>>>(p, b, px);
+    for (int h = 0; h < H; ++h)
+      wf_fold_kernel<<<(unsigned)((pxn[h] + 255) / 256), 256, 0, sh[h]>>>(ph[h], bh[h], pxn[h], px0[h]);
+    if (split) {
+      e = hipEventRecord(ev_join, stream2);
+      if (e == hipSuccess) e = hipStreamWaitEvent(stream, ev_join, 0);
+      if (e != hipSuccess) return e;
+    }
   }
   return hipGetLastError();
 }

@@ -329,6 +329,12 @@ int pt_dist_finalize(pt_context* ctx);
  * round handed to the exact walk (tests the hand-back path).  Output is
  * identical. */
 #define PT_OPT_WIDE 12
+/* PT_OPT_WF_STREAMS: 2 = the wavefront pipeline runs a chunk's pixels as
+ * two halves on the context's stream and a second stream of its own (forked
+ * from and joined back into the context's stream), so one half's trace and
+ * shading can fill the other's launch tails; 1 (default; 2 measured slower
+ * on the random clouds) = one stream.  Output is identical. */
+#define PT_OPT_WF_STREAMS 13
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */

@@ -886,3 +886,22 @@ def test_wide_walk_refused_tree_keeps_exact_walk():
     r.render(0, 2)
     ref, _ = _oracle(v, i, n, 48, 40, nb=2, cam=scenes.camera((0.0, 0.5, 3.0)))
     _assert_same(r.read_accum(), ref, "refused wide tree")
+
+
+@pytest.mark.parametrize("case", ["sphere", "cloud_int_bits"])
+def test_wavefront_two_streams(case):
+    """PT_OPT_WF_STREAMS 2: the chunk's pixels as two halves on two streams
+    (own lists, counters and stack overflow areas), over a stale accumulator
+    and a culled camera: the oracle's frame."""
+    sv, si, cam, lights, int_bits = _wide_case(case)
+    v, i, n, _, _ = ptamd.Scene.from_arrays(sv, si).build_bvh(int_bits=int_bits).arrays()
+    W, H = 200, 120
+    ref, _ = _oracle(v, i, n, W, H, nb=2, cam=cam, lights=lights, int_bits=int_bits)
+    ref, _ = _oracle(v, i, n, W, H, first=2, nb=3, cam=cam, lights=lights, int_bits=int_bits, accum=ref)
+    r = _setup(v, i, n, cam=cam, lights=lights, int_bits=int_bits, lds=0)
+    r.set_option(ptamd.PT_OPT_KERNEL, 3)
+    r.set_option(ptamd.PT_OPT_WF_STREAMS, 2)
+    r.resize_and_clear(W, H)
+    r.render(0, 2)
+    r.render(2, 3)
+    _assert_same(r.read_accum(), ref, f"two streams {case}")
