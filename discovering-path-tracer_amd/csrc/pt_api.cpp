@@ -407,6 +407,7 @@ struct pt_context {
   int opt_wf_paths = 0;       // PT_OPT_WF_PATHS (0 = 2^24)
   int opt_count = 0;          // PT_OPT_COUNT_TRACED
   int opt_pairs = 0;          // PT_OPT_PAIRS
+  int opt_wide_build = 1;     // PT_OPT_WIDE_BUILD (pt::WideBuild; read at upload)
   int opt_wf_streams = 1;     // PT_OPT_WF_STREAMS (2 measured slower: 10M cloud +9 %, sphere -0.8 %)
   hipStream_t wf_stream2 = nullptr;           // the wavefront pipeline's second half (created on first use)
   hipEvent_t wf_fork = nullptr, wf_join = nullptr;
@@ -1142,7 +1143,7 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   pt::WideBVH wide;
   const std::string wide_reason =
       pt::build_wide_bvh((const float*)nodes, n_nodes, (flags & PT_NODES_INT_BITS) != 0, vertices, n_vertex_floats,
-                         indices, n_indices / 3, &wide);
+                         indices, n_indices / 3, &wide, c->opt_wide_build);
   float lo[3] = {threaded[0].x, threaded[0].y, threaded[0].z};   // node 0 is the root
   float hi[3] = {threaded[1].x, threaded[1].y, threaded[1].z};
   PT_HIP(hipSetDevice(c->device));
@@ -1469,6 +1470,10 @@ int pt_set_option(pt_context* c, int key, int value) {
     case PT_OPT_WF_STREAMS:
       if (value != 1 && value != 2) return fail(PT_ERR_INVALID, "PT_OPT_WF_STREAMS takes 1 or 2");
       c->opt_wf_streams = value;
+      return PT_OK;
+    case PT_OPT_WIDE_BUILD:
+      if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_WIDE_BUILD takes 0 or 1");
+      c->opt_wide_build = value;
       return PT_OK;
     case PT_OPT_PAIRS:
       if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_PAIRS takes 0 or 1");

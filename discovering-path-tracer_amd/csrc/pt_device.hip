@@ -2508,6 +2508,14 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
     for (int it = 0; it < iters; ++it) {
       for (int h = 0; h < H; ++h) hipLaunchKernelGGL(trace, dim3(grid_t), dim3(256), lds_t, sh[h], ph[h], bh[h], cur);
       for (int h = 0; h < H; ++h) wf_shade_kernel<<<grid_s, 256, 0, sh[h]>>>(ph[h], bh[h], cur);
+#ifdef PT_WF_ROUND_LOG   // A/B builds only: rays per round (synchronous)
+      {
+        int cnt2[2] = {0, 0};
+        if (hipStreamSynchronize(sh[0]) == hipSuccess &&
+            hipMemcpy(cnt2, bh[0].counters, 2 * sizeof(int), hipMemcpyDeviceToHost) == hipSuccess)
+          fprintf(stderr, "wf_round %d traced %d next %d\n", it, cnt2[cur], cnt2[cur ^ 1]);
+      }
+#endif
       cur ^= 1;
     }
     for (int h = 0; h < H; ++h)

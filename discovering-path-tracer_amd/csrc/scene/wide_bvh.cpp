@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <thread>
 
 namespace pt {
 
@@ -89,10 +90,148 @@ bool wide_tri_coeffs(const float e1f[3], const float e2f[3], double* A, double* 
   return true;
 }
 
+namespace {
+
+// A binary tree the wide nodes are collapsed from: the reference's own tree
+// (WIDE_FROM_REFERENCE) or a binned-SAH tree over the reference's leaves
+// (WIDE_SAH).  Children are stored after their parent; leaves carry the
+// reference leaf node they stand for.
+struct BinTree {
+  std::vector<float> box;       // 6 per node: lo.xyz, hi.xyz
+  std::vector<int32_t> kid;     // 2 per node: children, or {-1, reference leaf node}
+  std::vector<double> mA, mB, mC;
+  bool leaf(size_t v) const { return kid[2 * v] < 0; }
+};
+
+double half_area(const float* b) {
+  const double dx = (double)b[3] - b[0], dy = (double)b[4] - b[1], dz = (double)b[5] - b[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+
+void grow(float* b, const float* c) {
+  for (int a = 0; a < 3; ++a) {
+    b[a] = std::min(b[a], c[a]);
+    b[3 + a] = std::max(b[3 + a], c[3 + a]);
+  }
+}
+
+void empty_box(float* b) {
+  for (int a = 0; a < 3; ++a) {
+    b[a] = INFINITY;
+    b[3 + a] = -INFINITY;
+  }
+}
+
+// Binned SAH over leaves [b, e) of `ids` (reference leaf nodes; their boxes in
+// lbox by position), written at node `at` of T: a subtree of n leaves takes
+// the 2n - 1 nodes [at, at + 2n - 1), left subtree first, so disjoint ranges
+// build in parallel and the result does not depend on the thread count.
+constexpr int kBins = 32;
+void sah_build(BinTree& T, std::vector<int32_t>& ids, std::vector<float>& lbox, std::vector<float>& cen, size_t b,
+               size_t e, size_t at, int par_depth) {
+  const size_t n = e - b;
+  float* nb = &T.box[6 * at];
+  empty_box(nb);
+  for (size_t i = b; i < e; ++i) grow(nb, &lbox[6 * i]);
+  if (n == 1) {
+    T.kid[2 * at] = -1;
+    T.kid[2 * at + 1] = ids[b];
+    return;
+  }
+  float cb[6];
+  empty_box(cb);
+  for (size_t i = b; i < e; ++i) {
+    const float* c = &cen[3 * i];
+    for (int a = 0; a < 3; ++a) {
+      cb[a] = std::min(cb[a], c[a]);
+      cb[3 + a] = std::max(cb[3 + a], c[a]);
+    }
+  }
+  int axis = -1, split = 0;
+  double best = INFINITY;
+  float bin_lo[3], bin_scale[3];
+  for (int a = 0; a < 3; ++a) {
+    const double ext = (double)cb[3 + a] - cb[a];
+    if (!(ext > 0.0)) continue;
+    bin_lo[a] = cb[a];
+    bin_scale[a] = (float)(kBins / ext * (1.0 - 1e-6));
+    float bbox[kBins][6];
+    size_t bcnt[kBins] = {};
+    for (int k = 0; k < kBins; ++k) empty_box(bbox[k]);
+    for (size_t i = b; i < e; ++i) {
+      int k = (int)((cen[3 * i + a] - bin_lo[a]) * bin_scale[a]);
+      k = std::min(std::max(k, 0), kBins - 1);
+      bcnt[k]++;
+      grow(bbox[k], &lbox[6 * i]);
+    }
+    double right_cost[kBins];
+    float acc[6];
+    empty_box(acc);
+    size_t cnt = 0;
+    for (int k = kBins - 1; k > 0; --k) {
+      grow(acc, bbox[k]);
+      cnt += bcnt[k];
+      right_cost[k] = cnt ? half_area(acc) * (double)cnt : 0.0;
+    }
+    empty_box(acc);
+    cnt = 0;
+    for (int k = 0; k < kBins - 1; ++k) {
+      grow(acc, bbox[k]);
+      cnt += bcnt[k];
+      if (cnt == 0 || cnt == n) continue;
+      const double cost = half_area(acc) * (double)cnt + right_cost[k + 1];
+      if (cost < best) {
+        best = cost;
+        axis = a;
+        split = k + 1;
+      }
+    }
+  }
+  size_t m;
+  if (axis >= 0) {
+    const float lo = bin_lo[axis], sc = bin_scale[axis];
+    // partition ids, boxes and centroids together
+    size_t i = b, j = e;
+    auto bin_of = [&](size_t q) {
+      int k = (int)((cen[3 * q + axis] - lo) * sc);
+      return std::min(std::max(k, 0), kBins - 1);
+    };
+    while (i < j) {
+      if (bin_of(i) < split) {
+        ++i;
+      } else {
+        --j;
+        std::swap(ids[i], ids[j]);
+        for (int q = 0; q < 6; ++q) std::swap(lbox[6 * i + q], lbox[6 * j + q]);
+        for (int q = 0; q < 3; ++q) std::swap(cen[3 * i + q], cen[3 * j + q]);
+      }
+    }
+    m = i;
+  } else {
+    m = b + n / 2;   // every centroid equal: any split
+  }
+  if (m == b || m == e) m = b + n / 2;
+  const size_t nl = m - b;
+  const size_t left = at + 1, right = at + 2 * nl;
+  T.kid[2 * at] = (int32_t)left;
+  T.kid[2 * at + 1] = (int32_t)right;
+  if (par_depth > 0 && n > 65536) {
+    std::thread th([&] { sah_build(T, ids, lbox, cen, b, m, left, par_depth - 1); });
+    sah_build(T, ids, lbox, cen, m, e, right, par_depth - 1);
+    th.join();
+  } else {
+    sah_build(T, ids, lbox, cen, b, m, left, 0);
+    sah_build(T, ids, lbox, cen, m, e, right, 0);
+  }
+}
+
+}  // namespace
+
 std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float* V, size_t n_vf,
-                           const uint32_t* I, size_t n_tris, WideBVH* out) {
+                           const uint32_t* I, size_t n_tris, WideBVH* out, int mode) {
   *out = WideBVH();
   if (n == 0) return "no nodes";
+  if (mode != WIDE_FROM_REFERENCE && mode != WIDE_SAH) return "unknown wide build mode";
   auto link = [&](size_t i, int which) -> int32_t {
     const float f = N[8 * i + (which ? 7 : 3)];
     int32_t v;
@@ -123,12 +262,13 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
   }
   if (out->rank_tri.size() != n_tris) return "tree leaves do not cover the triangles once";
   // the walk's premises on the uploaded arrays: finite, bounded coordinates;
-  // parent boxes contain their children's; leaf boxes contain their triangle
+  // parent boxes contain their children's (so the reference tests a triangle
+  // iff its leaf box passes); leaf boxes contain their triangle
   for (size_t i = 0; i < n; ++i)
     for (int a = 0; a < 3; ++a)
       if (!(fabs((double)lo(i, a)) <= kMaxCoord && fabs((double)hi(i, a)) <= kMaxCoord))
         return "node coordinates not finite or beyond 1e15";
-  std::vector<double> mA(n), mB(n), mC(n);   // max cull coefficients over each subtree
+  std::vector<double> lA(n), lB(n), lC(n);   // per reference node: max cull coefficients over its subtree
   for (size_t k = order.size(); k-- > 0;) {
     const int32_t v = order[k];
     if (leaf(v)) {
@@ -149,29 +289,81 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
       }
       double A, B, C;
       if (wide_tri_coeffs(e1, e2, &A, &B, &C)) {
-        mA[v] = A;
-        mB[v] = B;
-        mC[v] = C;
+        lA[v] = A;
+        lB[v] = B;
+        lC[v] = C;
       } else {
-        mA[v] = INFINITY;
-        mB[v] = mC[v] = 0;
+        lA[v] = INFINITY;
+        lB[v] = lC[v] = 0;
       }
     } else {
       const int32_t l = link(v, 0), r = link(v, 1);
       for (int32_t ch : {l, r})
         for (int a = 0; a < 3; ++a)
           if (!(lo(v, a) <= lo(ch, a) && hi(v, a) >= hi(ch, a))) return "a parent box does not contain its child's";
-      mA[v] = std::max(mA[l], mA[r]);
-      mB[v] = std::max(mB[l], mB[r]);
-      mC[v] = std::max(mC[l], mC[r]);
+      lA[v] = std::max(lA[l], lA[r]);
+      lB[v] = std::max(lB[l], lB[r]);
+      lC[v] = std::max(lC[l], lC[r]);
     }
   }
-  // wide nodes: expand the reference node's children, largest box first,
-  // until four entries or all leaves
-  auto area = [&](int32_t v) {
-    const double dx = (double)hi(v, 0) - lo(v, 0), dy = (double)hi(v, 1) - lo(v, 1), dz = (double)hi(v, 2) - lo(v, 2);
-    return dx * dy + dy * dz + dz * dx;
-  };
+  // the binary tree to collapse
+  BinTree T;
+  if (mode == WIDE_FROM_REFERENCE) {
+    T.box.resize(6 * n);
+    T.kid.resize(2 * n);
+    T.mA = std::move(lA);
+    T.mB = std::move(lB);
+    T.mC = std::move(lC);
+    for (size_t v = 0; v < n; ++v) {
+      for (int a = 0; a < 3; ++a) {
+        T.box[6 * v + a] = lo(v, a);
+        T.box[6 * v + 3 + a] = hi(v, a);
+      }
+      if (leaf(v)) {
+        T.kid[2 * v] = -1;
+        T.kid[2 * v + 1] = (int32_t)v;
+      } else {   // right child first, as the reference visits them
+        T.kid[2 * v] = link(v, 1);
+        T.kid[2 * v + 1] = link(v, 0);
+      }
+    }
+  } else {
+    std::vector<int32_t> ids;
+    ids.reserve(n_tris);
+    for (int32_t v : order)
+      if (leaf(v)) ids.push_back(v);
+    std::vector<float> lbox(6 * n_tris), cen(3 * n_tris);
+    for (size_t i = 0; i < n_tris; ++i)
+      for (int a = 0; a < 3; ++a) {
+        const float l = lo(ids[i], a), h = hi(ids[i], a);
+        lbox[6 * i + a] = l;
+        lbox[6 * i + 3 + a] = h;
+        cen[3 * i + a] = 0.5f * l + 0.5f * h;
+      }
+    const size_t nb = 2 * n_tris - 1;
+    T.box.resize(6 * nb);
+    T.kid.resize(2 * nb);
+    sah_build(T, ids, lbox, cen, 0, n_tris, 0, 4);
+    T.mA.resize(nb);
+    T.mB.resize(nb);
+    T.mC.resize(nb);
+    for (size_t v = nb; v-- > 0;) {   // children are stored after their parent
+      if (T.leaf(v)) {
+        const int32_t r = T.kid[2 * v + 1];
+        T.mA[v] = lA[r];
+        T.mB[v] = lB[r];
+        T.mC[v] = lC[r];
+      } else {
+        const int32_t l = T.kid[2 * v], r = T.kid[2 * v + 1];
+        T.mA[v] = std::max(T.mA[l], T.mA[r]);
+        T.mB[v] = std::max(T.mB[l], T.mB[r]);
+        T.mC[v] = std::max(T.mC[l], T.mC[r]);
+      }
+    }
+  }
+  // wide nodes: expand the binary node's children, largest box first, until
+  // four entries or all leaves
+  auto area = [&](int32_t v) { return half_area(&T.box[6 * (size_t)v]); };
   std::vector<float>& W = out->nodes;
   std::vector<int32_t> n_inner;              // per wide node: inner children
   std::vector<std::vector<int32_t>> kids;    // per wide node: its inner children's wide indices
@@ -181,28 +373,28 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
     kids.emplace_back();
     return (int32_t)(n_inner.size() - 1);
   };
-  std::vector<std::pair<int32_t, int32_t>> st;   // (reference node, wide node)
+  std::vector<std::pair<int32_t, int32_t>> st;   // (binary node, wide node)
   st.push_back({0, alloc()});
   while (!st.empty()) {
     const auto [v, w] = st.back();
     st.pop_back();
     std::vector<int32_t> list;
-    if (leaf(v)) {
+    if (T.leaf(v)) {
       list.push_back(v);   // a one-triangle tree: the root leaf is the only child
     } else {
-      list = {link(v, 1), link(v, 0)};
+      list = {T.kid[2 * v], T.kid[2 * v + 1]};
       while (list.size() < 4) {
         int best = -1;
         double ba = -1.0;
         for (size_t j = 0; j < list.size(); ++j)
-          if (!leaf(list[j]) && area(list[j]) > ba) {
+          if (!T.leaf(list[j]) && area(list[j]) > ba) {
             ba = area(list[j]);
             best = (int)j;
           }
         if (best < 0) break;
         const int32_t x = list[best];
-        list[best] = link(x, 1);
-        list.insert(list.begin() + best + 1, link(x, 0));
+        list[best] = T.kid[2 * x];
+        list.insert(list.begin() + best + 1, T.kid[2 * x + 1]);
       }
     }
     double A = 0.0, C = 0.0;
@@ -211,16 +403,16 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
       int32_t ref = kEmpty;
       if (j < (int)list.size()) {
         const int32_t c = list[j];
+        const float* cb = &T.box[6 * (size_t)c];
         for (int a = 0; a < 3; ++a) {
-          rec[8 * a + j] = lo(c, a);
-          rec[8 * a + 4 + j] = hi(c, a);
+          rec[8 * a + j] = cb[a];
+          rec[8 * a + 4 + j] = cb[3 + a];
         }
-        const double ext = std::max({(double)hi(c, 0) - lo(c, 0), (double)hi(c, 1) - lo(c, 1),
-                                     (double)hi(c, 2) - lo(c, 2)});
-        A = std::max(A, mA[c]);
-        C = std::max(C, ext * mB[c] + mC[c]);
-        if (leaf(c)) {
-          ref = ~rank[c];
+        const double ext = std::max({(double)cb[3] - cb[0], (double)cb[4] - cb[1], (double)cb[5] - cb[2]});
+        A = std::max(A, T.mA[c]);
+        C = std::max(C, ext * T.mB[c] + T.mC[c]);
+        if (T.leaf(c)) {
+          ref = ~rank[T.kid[2 * (size_t)c + 1]];
         } else {
           ref = alloc();
           rec = &W[32 * (size_t)w];   // alloc may move W

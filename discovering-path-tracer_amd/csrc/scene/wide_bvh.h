@@ -24,13 +24,21 @@ struct WideBVH {
   int stack_cap = 0;               // most stack entries a walk can hold
 };
 
+// How the 4-wide nodes group the reference's leaves.  Either way every child
+// box is a reference leaf box (bitwise) or contains the leaf boxes below it,
+// which is all the walk's exactness needs (wide_walk.h).
+enum WideBuild {
+  WIDE_FROM_REFERENCE = 0,   // collapse the reference's own tree (its internal boxes)
+  WIDE_SAH = 1,              // binned-SAH tree over the reference's leaf boxes
+};
+
 // nodes: n reference nodes, 8 floats each ({min.xyz, left}, {max.xyz, right};
 // links float- or int-encoded).  Returns "" on success, else the reason the
 // culled walk cannot take this scene (the caller keeps the exact walk): a
 // parent box not containing a child's, a leaf box not containing its
 // triangle, non-finite or huge coordinates, or a degenerate depth.
 std::string build_wide_bvh(const float* nodes, size_t n, bool int_bits, const float* verts, size_t n_vertex_floats,
-                           const uint32_t* idx, size_t n_tris, WideBVH* out);
+                           const uint32_t* idx, size_t n_tris, WideBVH* out, int mode = WIDE_SAH);
 
 // The cull coefficients of one triangle (edges e1 = fl(v1-v0), e2 = fl(v2-v0)):
 // accepted with t <= b implies dist(o, B) <= A*b + Bc*ext(B) + C for every box

@@ -335,6 +335,12 @@ int pt_dist_finalize(pt_context* ctx);
  * shading can fill the other's launch tails; 1 (default; 2 measured slower
  * on the random clouds) = one stream.  Output is identical. */
 #define PT_OPT_WF_STREAMS 13
+/* PT_OPT_WIDE_BUILD (read by pt_upload_scene): how the culled wide walk's
+ * 4-wide nodes group the reference's leaves.  1 (default) = a binned-SAH tree
+ * over the reference's leaf boxes; 0 = the reference's own tree collapsed to
+ * 4-wide nodes.  Every child box is a reference leaf box bitwise or contains
+ * the leaf boxes below it, so the walk's answers are the same. */
+#define PT_OPT_WIDE_BUILD 14
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */

@@ -49,6 +49,7 @@ def lib():
         L.wide_check.argtypes = [F32P, sz, U32P, sz, F32P, sz, ctypes.c_int, F32P, sz, F32P, U64P,
                                  ctypes.c_char_p, sz]
         L.wide_coeffs.argtypes = [F32P, F32P, F64P]
+        L.wide_set_mode.argtypes = [ctypes.c_int]
         _LIB = L
     return _LIB
 
@@ -58,8 +59,14 @@ def _scene(v, i):
     return np.ascontiguousarray(v, np.float32), idx, nodes
 
 
-def check(v, idx, nodes, rays):
+# the two ways the wide nodes group the reference's leaves (scene/wide_bvh.h)
+WIDE_FROM_REFERENCE, WIDE_SAH = 0, 1
+BUILDS = pytest.mark.parametrize("build", [WIDE_SAH, WIDE_FROM_REFERENCE], ids=["sah", "reference_tree"])
+
+
+def check(v, idx, nodes, rays, build=WIDE_SAH):
     L = lib()
+    L.wide_set_mode(build)
     rays = np.ascontiguousarray(rays, np.float32)
     n = rays.size // 8
     out = np.zeros(4 * n, np.float32)
@@ -126,10 +133,10 @@ def make_rays(v, idx, n, seed, lo=-1.2, hi=1.2):
     return rays
 
 
-def run_scene(v, i, n_rays, seed):
+def run_scene(v, i, n_rays, seed, build=WIDE_SAH):
     v, idx, nodes = _scene(v, i)
     rays = make_rays(v, idx, n_rays, seed)
-    out, st = check(v, idx, nodes, rays)     # closest
+    out, st = check(v, idx, nodes, rays, build)     # closest
     assert st[0] == 0, f"closest-hit mismatches: {int(st[0])} (first ray {int(st[7])}: {rays[int(st[7])]})"
     # shadow queries with limits around the closest hit (and far / negative / NaN ones)
     rng = np.random.default_rng(seed + 1)
@@ -144,7 +151,7 @@ def run_scene(v, i, n_rays, seed):
     lim = np.where((special >= 0.02) & (special < 0.04), np.float32(-1.0), lim)
     lim = np.where((special >= 0.04) & (special < 0.06), np.float32(1e30), lim)
     sh[:, 7] = lim.astype(np.float32)
-    _, st2 = check(v, idx, nodes, sh)
+    _, st2 = check(v, idx, nodes, sh, build)
     assert st2[1] == 0, f"shadow mismatches: {int(st2[1])} (first ray {int(st2[7])}: {sh[int(st2[7])]})"
     return st, st2
 
@@ -157,36 +164,41 @@ def test_coefficients_bound_shape():
     assert lib().wide_coeffs(np.float32([2, 0, 0]), np.float32([0, 2, 0]), a) == 1
 
 
-def test_wide_walk_random_cloud():
+@BUILDS
+def test_wide_walk_random_cloud(build):
     v, i = scenes.random_triangles(20000, seed=7)
-    st, st2 = run_scene(v, i, 60000, seed=11)
+    st, st2 = run_scene(v, i, 60000, seed=11, build=build)
     # far fewer node fetches than the exhaustive walk, never more triangle tests
     assert st[3] < st[5] / 3, (int(st[3]), int(st[5]))
     assert st[4] <= st[6], (int(st[4]), int(st[6]))
     assert st[2] > 0   # axis-parallel rays went to the exact walk
 
 
-def test_wide_walk_displaced_sphere():
+@BUILDS
+def test_wide_walk_displaced_sphere(build):
     v, i = scenes.displaced_sphere(subdiv=4)
-    run_scene(v, i, 60000, seed=12)
+    run_scene(v, i, 60000, seed=12, build=build)
 
 
-def test_wide_walk_grid_ties():
+@BUILDS
+def test_wide_walk_grid_ties(build):
     """Axis-aligned coplanar quads: equal t across triangles, tie-break by visit rank."""
     v, i = scenes.grid_mesh(8)
-    run_scene(v, i, 40000, seed=13)
+    run_scene(v, i, 40000, seed=13, build=build)
 
 
-def test_wide_walk_box_big_triangles():
+@BUILDS
+def test_wide_walk_box_big_triangles(build):
     v, i, _ = oracle_lib.obj_parse(open(scenes.BOX_OBJ, "rb").read())
-    run_scene(v, i, 40000, seed=14)
+    run_scene(v, i, 40000, seed=14, build=build)
 
 
-def test_wide_walk_dense_tiny_cloud():
+@BUILDS
+def test_wide_walk_dense_tiny_cloud(build):
     """A dense cloud of small triangles: many near-equal hit distances, and
     culling cuts the triangle tests."""
     v, i = scenes.random_triangles(30000, seed=9, spread=0.2, size=0.004)
-    st, _ = run_scene(v, i, 40000, seed=15)
+    st, _ = run_scene(v, i, 40000, seed=15, build=build)
     assert st[4] < 0.8 * st[6], (int(st[4]), int(st[6]))
 
 

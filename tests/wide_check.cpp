@@ -17,6 +17,8 @@ extern "C" void oracle_trace(const float* verts, const uint32_t* idx, const floa
 using namespace ptd;
 
 namespace {
+int g_mode = pt::WIDE_SAH;   // wide_set_mode
+
 struct Built {
   pt::WideBVH w;
   std::vector<float4> tris;   // by rank: {v0, e1.x} {e1.yz, e2.xy} {e2.z, n}
@@ -24,7 +26,7 @@ struct Built {
 
 std::string build(const float* V, size_t nvf, const uint32_t* I, size_t nt, const float* N, size_t nn, int int_bits,
                   Built* b) {
-  std::string why = pt::build_wide_bvh(N, nn, int_bits != 0, V, nvf, I, nt, &b->w);
+  std::string why = pt::build_wide_bvh(N, nn, int_bits != 0, V, nvf, I, nt, &b->w, g_mode);
   if (!why.empty()) return why;
   b->tris.resize(3 * nt);
   for (size_t r = 0; r < nt; ++r) {
@@ -45,6 +47,9 @@ std::string build(const float* V, size_t nvf, const uint32_t* I, size_t nt, cons
 }  // namespace
 
 extern "C" {
+
+// The wide builder the next calls use (pt::WideBuild).
+void wide_set_mode(int mode) { g_mode = mode; }
 
 // info[0] wide nodes, info[1] stack bound.  Returns 0, or 1 with the reason in err.
 int wide_info(const float* V, size_t nvf, const uint32_t* I, size_t nt, const float* N, size_t nn, int int_bits,
