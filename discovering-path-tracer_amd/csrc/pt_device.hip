@@ -1582,23 +1582,37 @@ __global__ __launch_bounds__(256, PT_SM_MIN_BLOCKS) void render_sm_kernel(Render
 // ===========================================================================
 static_assert(sizeof(PathSt) == kWfStateF4 * 16, "PathSt is stored as kWfStateF4 float4");
 
-__device__ __forceinline__ void wf_load_state(const float4* __restrict__ src, PathSt* S) {
+// A path's state is one 160-B record (kWfStateF4 float4): the live paths of
+// a list are sparse after the first bounces, and a record per path keeps
+// each one in one or two lines (by component, 16 B per line touched: sphere
+// +2.5 %, 10M cloud +4 %).  A list slot's ray is stored by component --
+// rays[s] and rays[cap + s] -- since a wave reads and writes consecutive
+// slots.
+__device__ __forceinline__ void wf_load_state(const WfBuffers& B, long long p, PathSt* S) {
+  const float4* __restrict__ src = B.state + (size_t)p * kWfStateF4;
   float4 v[kWfStateF4];
 #pragma unroll
   for (int i = 0; i < kWfStateF4; ++i) v[i] = src[i];
   __builtin_memcpy(S, v, sizeof(PathSt));
 }
 
-__device__ __forceinline__ void wf_store_state(float4* __restrict__ dst, const PathSt& S) {
+__device__ __forceinline__ void wf_store_state(const WfBuffers& B, long long p, const PathSt& S) {
+  float4* __restrict__ dst = B.state + (size_t)p * kWfStateF4;
   float4 v[kWfStateF4];
   __builtin_memcpy(v, &S, sizeof(PathSt));
 #pragma unroll
   for (int i = 0; i < kWfStateF4; ++i) dst[i] = v[i];
 }
 
-__device__ __forceinline__ void wf_store_ray(float4* __restrict__ dst, const Trav& T) {
-  dst[0] = make_float4(T.o.x, T.o.y, T.o.z, T.lim);
-  dst[1] = make_float4(T.d.x, T.d.y, T.d.z, __int_as_float(T.shadow));
+__device__ __forceinline__ void wf_store_ray(float4* __restrict__ rays, long long cap, int slot, const Trav& T) {
+  rays[slot] = make_float4(T.o.x, T.o.y, T.o.z, T.lim);
+  rays[(size_t)cap + (size_t)slot] = make_float4(T.d.x, T.d.y, T.d.z, __int_as_float(T.shadow));
+}
+
+__device__ __forceinline__ void wf_load_ray(const float4* __restrict__ rays, long long cap, int slot, float4* r0,
+                                            float4* r1) {
+  *r0 = rays[slot];
+  *r1 = rays[(size_t)cap + (size_t)slot];
 }
 
 // A list slot for every lane with pred set (-1 for the others): one atomic
@@ -1616,7 +1630,7 @@ __device__ __forceinline__ int wave_slot(int* counter, bool pred) {
 
 __device__ __forceinline__ void wf_push(const WfBuffers& B, int list, int slot, int p, const Trav& T) {
   B.ids[list][slot] = p;
-  wf_store_ray(B.rays[list] + 2 * (size_t)slot, T);
+  wf_store_ray(B.rays[list], B.cap, slot, T);
 }
 
 // Path g of a launch: pixel (item, q) = g / n_batches, sample g % n_batches
@@ -1672,7 +1686,7 @@ __global__ __launch_bounds__(256) void wf_gen_kernel(RenderParams P, WfBuffers B
         S.phase = PH_BEGIN;
         Ctr c = {0u, 0u, 0u, 0u, 0u};
         need = path_step<false>(P, F, S, T, c, &col);
-        if (need) wf_store_state(B.state + (size_t)g * kWfStateF4, S);
+        if (need) wf_store_state(B, g, S);
       }
       if (!need) B.colors[g] = make_float4(col.x, col.y, col.z, 1.0f);
     }
@@ -1697,15 +1711,14 @@ struct WfLane {
 
 // CNT: a ray handed to the traversal kernel -- closest (kind 0) or shadow
 // (kind 1) walk; a null shadow query (kind 2, trav_null) is no walk.
-__device__ __forceinline__ void count_start(const float4* __restrict__ ray, Ctr& c) {
-  const int kind = __float_as_int(ray[1].w);
+__device__ __forceinline__ void count_start(float4 r1, Ctr& c) {
+  const int kind = __float_as_int(r1.w);
   c.rays += kind == 0 ? 1u : 0u;
   c.srays += kind == 1 ? 1u : 0u;
 }
 
-__device__ __forceinline__ void wf_lane_start(const RenderParams& P, const float4* __restrict__ ray, float4 root_a,
+__device__ __forceinline__ void wf_lane_start(const RenderParams& P, float4 r0, float4 r1, float4 root_a,
                                               float4 root_b, WfLane& L) {
-  const float4 r0 = ray[0], r1 = ray[1];
   L.o = mk(r0.x, r0.y, r0.z);
   L.d = mk(r1.x, r1.y, r1.z);
   L.inv = mk(rcp_(L.d.x), rcp_(L.d.y), rcp_(L.d.z));
@@ -1866,8 +1879,10 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
         const int slot = base + (int)__popcll(gm & ((1ull << lead) - 1ull)) * G + (lane - lead);
         if (slot < count) {
           p = slot;
-          wf_lane_start(P, rays + 2 * (size_t)slot, root_a, root_b, L);
-          if (CNT) count_start(rays + 2 * (size_t)slot, c);
+          float4 r0, r1;
+          wf_load_ray(rays, B.cap, slot, &r0, &r1);
+          wf_lane_start(P, r0, r1, root_a, root_b, L);
+          if (CNT) count_start(r1, c);
         }
       }
     }
@@ -1919,8 +1934,7 @@ struct PairLane {
   float lim;
 };
 
-__device__ __forceinline__ void pair_lane_start(const float4* __restrict__ ray, PairLane& L) {
-  const float4 r0 = ray[0], r1 = ray[1];
+__device__ __forceinline__ void pair_lane_start(float4 r0, float4 r1, PairLane& L) {
   L.o = mk(r0.x, r0.y, r0.z);
   L.d = mk(r1.x, r1.y, r1.z);
   L.inv = mk(rcp_(L.d.x), rcp_(L.d.y), rcp_(L.d.z));
@@ -2027,8 +2041,10 @@ __global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_ker
         const int slot = base + (int)__popcll(gm & ((1ull << lead) - 1ull)) * G + (lane - lead);
         if (slot < count) {
           p = slot;
-          pair_lane_start(rays + 2 * (size_t)slot, L);
-          if (CNT) count_start(rays + 2 * (size_t)slot, c);
+          float4 r0, r1;
+          wf_load_ray(rays, B.cap, slot, &r0, &r1);
+          pair_lane_start(r0, r1, L);
+          if (CNT) count_start(r1, c);
         }
       }
     }
@@ -2073,7 +2089,10 @@ __global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_ker
 #define PT_WIDE_FLUSH_T 1
 #endif
 #ifndef PT_WIDE_MIN_BLOCKS
-#define PT_WIDE_MIN_BLOCKS 8   // 64 VGPRs (56 B spilled): 10M cloud -7.5 %, sphere -1.5 % vs 6 (76 VGPRs); 7: between
+// 6: the LDS stack and leaf queue (96 B per lane) fit 6 workgroups per CU;
+// 79 VGPRs, no spills.  8 workgroups with a 6-entry stack ring (80 B per lane,
+// 64 VGPRs, 60 B spilled): sphere +6.5 %, 10M cloud +5.4 %; with 7: +1 %.
+#define PT_WIDE_MIN_BLOCKS 6
 #endif
 template <int G, bool CNT = false>
 __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(RenderParams P, WfBuffers B,
@@ -2114,9 +2133,10 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
       if ((gm >> lead) & 1ull) {
         const int slot = base + (int)__popcll(gm & ((1ull << lead) - 1ull)) * G + (lane - lead);
         if (slot < count) {
-          const float4 r0 = rays[2 * (size_t)slot], r1 = rays[2 * (size_t)slot + 1];
+          float4 r0, r1;
+          wf_load_ray(rays, B.cap, slot, &r0, &r1);
           const int kind = __float_as_int(r1.w);   // 0 closest, 1 shadow, 2 null shadow (trav_null)
-          if (CNT) count_start(rays + 2 * (size_t)slot, c);
+          if (CNT) count_start(r1, c);
           wide_start(R, mk(r0.x, r0.y, r0.z), mk(r1.x, r1.y, r1.z), kind != 0, r0.w);
           if (kind == 2) {
             B.hits[slot] = make_float2(R.lim, __int_as_float(0));
@@ -2219,8 +2239,9 @@ __global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers
     if (i < count) {
       p = B.ids[cur][i];
       PathSt S;
-      wf_load_state(B.state + (size_t)p * kWfStateF4, &S);
-      const float4 r0 = B.rays[cur][2 * (size_t)i], r1 = B.rays[cur][2 * (size_t)i + 1];
+      wf_load_state(B, p, &S);
+      float4 r0, r1;
+      wf_load_ray(B.rays[cur], B.cap, i, &r0, &r1);
       const float2 h = B.hits[i];
       T.o = mk(r0.x, r0.y, r0.z);
       T.d = mk(r1.x, r1.y, r1.z);
@@ -2240,7 +2261,7 @@ __global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers
       v3 col;
       need = path_step<false>(P, F, S, T, c, &col);
       if (need)
-        wf_store_state(B.state + (size_t)p * kWfStateF4, S);
+        wf_store_state(B, p, S);
       else
         B.colors[p] = make_float4(col.x, col.y, col.z, 1.0f);
     }
@@ -2485,7 +2506,7 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
       px0[1] = pxn[0];
       const long long sb = pxn[0] * p.n_batches;   // half 1's paths and list slots start here
       for (int k = 0; k < 2; ++k) {
-        bh[1].rays[k] = b.rays[k] + 2 * sb;
+        bh[1].rays[k] = b.rays[k] + sb;   // slot s of half 1: rays[sb + s], rays[cap + sb + s]
         bh[1].ids[k] = b.ids[k] + sb;
       }
       bh[1].hits = b.hits + sb;

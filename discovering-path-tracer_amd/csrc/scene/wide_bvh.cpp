@@ -30,6 +30,30 @@ float down_f(double x) {
 
 }  // namespace
 
+WideCoeffs coeff_max(const WideCoeffs& a, const WideCoeffs& b) {
+  return WideCoeffs{std::max(a.k1, b.k1), std::max(a.k2, b.k2), std::max(a.eps0, b.eps0), std::max(a.eps1, b.eps1)};
+}
+
+// The node's cull constants {c1, E0, E1, 0} (wide_walk.h wide_child) from the
+// largest coefficients of the triangles below it: a child is culled when
+// lim < th = c1 * (t_near (1 - 2^-20) - (E0 + E1 Smax) (|1/d|_max + 1)).
+// Margins: the float slab's t_near is within (1+u)^3 of the exact entry;
+// S <= (1 + 3u) Smax (Smax from the slab's own differences); |1/d| within 2u
+// of the float reciprocal; each float op of the evaluation rounds once --
+// all covered by the 2^-18 and 2^-20 factors.  A triangle without a bound
+// (k1 infinite) gives c1 = 0: th = 0 culls nothing a hit (t > 1e-6) could need.
+void node_cull_consts(const WideCoeffs& co, float* out) {
+  out[3] = 0.0f;
+  if (!(co.k1 <= 0.5) || !(co.eps0 < 1e30) || !(co.eps1 < 1e30) || !(co.k2 < 1e30)) {
+    out[0] = out[1] = out[2] = 0.0f;
+    return;
+  }
+  const double c1 = down_f((1.0 - co.k1) / (1.0 + gam(3)) * (1.0 - 0x1p-20));
+  out[0] = (float)c1;
+  out[1] = up_f(co.eps0 * (1.0 + 0x1p-18));
+  out[2] = up_f(std::max(co.eps1, co.k2 / c1) * (1.0 + 3.0 * kU) * (1.0 + 0x1p-18));
+}
+
 // Error bound of intersectTriangle (raytrace_comp.comp:114-157) as the
 // kernels evaluate it (tri_test: edges e1, e2 precomputed, no contraction,
 // IEEE reciprocal).  Notation: u = 2^-24, g_k = k u / (1 - k u), |x|_1 and
@@ -50,14 +74,13 @@ float down_f(double x) {
 // (dm >= |d|_2, |d|_inf: the walk takes only rays with fl(d.d) <= 1.00002).
 // X lies within rho (inf-norm) of conv(v0, v0+e1, v0+e2) -- hence of the
 // triangle (|e1 - (v1 - v0)| <= u|e1|) and of any box B containing it:
-//   rho = u max(|e1|inf, |e2|inf) + du |e1|inf + dv |e2|inf.
-// An accepted triangle with t_b <= b then has |T| <= (b (1+g3) + g D0 S) /
-// (1 - g dm D0), and dist(o, B) <= |o - o''| + |o'' - X| + sqrt3 rho
-//   <= dm |T| + sqrt3 (rho + u S / (1-u)).
-// Every term is linear in S, and S <= (1+u)(dist(o, B) + ext(B)) (v0 is in
-// B; ext = the box's largest extent), so dist(o,B) <= a b + b' (dist + ext) + c
-// and, for b' < 1: dist(o,B) <= (a b + b' ext + c) / (1 - b').
-bool wide_tri_coeffs(const float e1f[3], const float e2f[3], double* A, double* Bc, double* C) {
+//   rho = u max(|e1|inf, |e2|inf) + du |e1|inf + dv |e2|inf = rho0 + rhoS S.
+// So the point o + T d lies in B grown by eps = rho + u S / (1 - u) on every
+// side, and on each axis i, T >= entry_i(B) - eps / |d_i|: T is at least the
+// ray's exact entry parameter into B less eps |1/d|_max.  With t_b > 1e-6
+// (:153) and T > 0, t_b >= (T (1 - k1) - k2 S) / (1 + g3), k1 = g dm D0,
+// k2 = g D0.  wide_walk.h evaluates the resulting threshold per child.
+bool wide_tri_coeffs(const float e1f[3], const float e2f[3], WideCoeffs* out) {
   const double dm = 1.0000102;   // sqrt(1.00002 (1 + g3)) rounded up
   const double g = gam(6) / 0.999e-6;
   double n1 = 0, n2 = 0, m1 = 0, m2 = 0, D0 = 0;
@@ -78,15 +101,10 @@ bool wide_tri_coeffs(const float e1f[3], const float e2f[3], double* A, double* 
   const double beta = (g * dm * D0 + gam(3)) / den;
   const double rhoS = alpha_u * m1 + alpha_v * m2;
   const double rho0 = 1.01 * kU * std::max(m1, m2) + beta * (m1 + m2);
-  const double s3 = 1.7320508075688774;
-  const double a = dm * (1.0 + gam(3)) / den;
-  const double b = dm * g * D0 / den + s3 * (rhoS + kU / (1.0 - kU));
-  const double c = s3 * rho0;
-  const double bp = b * (1.0 + kU);
-  if (!(bp < 0.5)) return false;
-  *A = a / (1.0 - bp);
-  *Bc = bp / (1.0 - bp);
-  *C = c / (1.0 - bp);
+  out->k1 = g * dm * D0;
+  out->k2 = g * D0;
+  out->eps0 = rho0;
+  out->eps1 = rhoS + kU / (1.0 - kU);
   return true;
 }
 
@@ -99,7 +117,7 @@ namespace {
 struct BinTree {
   std::vector<float> box;       // 6 per node: lo.xyz, hi.xyz
   std::vector<int32_t> kid;     // 2 per node: children, or {-1, reference leaf node}
-  std::vector<double> mA, mB, mC;
+  std::vector<WideCoeffs> co;   // per node: the largest coefficients over its subtree
   bool leaf(size_t v) const { return kid[2 * v] < 0; }
 };
 
@@ -268,7 +286,7 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
     for (int a = 0; a < 3; ++a)
       if (!(fabs((double)lo(i, a)) <= kMaxCoord && fabs((double)hi(i, a)) <= kMaxCoord))
         return "node coordinates not finite or beyond 1e15";
-  std::vector<double> lA(n), lB(n), lC(n);   // per reference node: max cull coefficients over its subtree
+  std::vector<WideCoeffs> lc(n);   // per reference node: the largest coefficients over its subtree
   for (size_t k = order.size(); k-- > 0;) {
     const int32_t v = order[k];
     if (leaf(v)) {
@@ -287,23 +305,13 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
         e1[a] = p[1][a] - p[0][a];   // fl(v1 - v0), as setup_tris_kernel
         e2[a] = p[2][a] - p[0][a];
       }
-      double A, B, C;
-      if (wide_tri_coeffs(e1, e2, &A, &B, &C)) {
-        lA[v] = A;
-        lB[v] = B;
-        lC[v] = C;
-      } else {
-        lA[v] = INFINITY;
-        lB[v] = lC[v] = 0;
-      }
+      if (!wide_tri_coeffs(e1, e2, &lc[v])) lc[v] = WideCoeffs{INFINITY, 0.0, 0.0, 0.0};   // no culling
     } else {
       const int32_t l = link(v, 0), r = link(v, 1);
       for (int32_t ch : {l, r})
         for (int a = 0; a < 3; ++a)
           if (!(lo(v, a) <= lo(ch, a) && hi(v, a) >= hi(ch, a))) return "a parent box does not contain its child's";
-      lA[v] = std::max(lA[l], lA[r]);
-      lB[v] = std::max(lB[l], lB[r]);
-      lC[v] = std::max(lC[l], lC[r]);
+      lc[v] = coeff_max(lc[l], lc[r]);
     }
   }
   // the binary tree to collapse
@@ -311,9 +319,7 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
   if (mode == WIDE_FROM_REFERENCE) {
     T.box.resize(6 * n);
     T.kid.resize(2 * n);
-    T.mA = std::move(lA);
-    T.mB = std::move(lB);
-    T.mC = std::move(lC);
+    T.co = std::move(lc);
     for (size_t v = 0; v < n; ++v) {
       for (int a = 0; a < 3; ++a) {
         T.box[6 * v + a] = lo(v, a);
@@ -344,22 +350,9 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
     T.box.resize(6 * nb);
     T.kid.resize(2 * nb);
     sah_build(T, ids, lbox, cen, 0, n_tris, 0, 4);
-    T.mA.resize(nb);
-    T.mB.resize(nb);
-    T.mC.resize(nb);
-    for (size_t v = nb; v-- > 0;) {   // children are stored after their parent
-      if (T.leaf(v)) {
-        const int32_t r = T.kid[2 * v + 1];
-        T.mA[v] = lA[r];
-        T.mB[v] = lB[r];
-        T.mC[v] = lC[r];
-      } else {
-        const int32_t l = T.kid[2 * v], r = T.kid[2 * v + 1];
-        T.mA[v] = std::max(T.mA[l], T.mA[r]);
-        T.mB[v] = std::max(T.mB[l], T.mB[r]);
-        T.mC[v] = std::max(T.mC[l], T.mC[r]);
-      }
-    }
+    T.co.resize(nb);
+    for (size_t v = nb; v-- > 0;)   // children are stored after their parent
+      T.co[v] = T.leaf(v) ? lc[T.kid[2 * v + 1]] : coeff_max(T.co[T.kid[2 * v]], T.co[T.kid[2 * v + 1]]);
   }
   // wide nodes: expand the binary node's children, largest box first, until
   // four entries or all leaves
@@ -397,7 +390,7 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
         list.insert(list.begin() + best + 1, T.kid[2 * x + 1]);
       }
     }
-    double A = 0.0, C = 0.0;
+    WideCoeffs co{0.0, 0.0, 0.0, 0.0};
     float* rec = &W[32 * (size_t)w];
     for (int j = 0; j < 4; ++j) {
       int32_t ref = kEmpty;
@@ -408,9 +401,7 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
           rec[8 * a + j] = cb[a];
           rec[8 * a + 4 + j] = cb[3 + a];
         }
-        const double ext = std::max({(double)cb[3] - cb[0], (double)cb[4] - cb[1], (double)cb[5] - cb[2]});
-        A = std::max(A, T.mA[c]);
-        C = std::max(C, ext * T.mB[c] + T.mC[c]);
+        co = coeff_max(co, T.co[c]);
         if (T.leaf(c)) {
           ref = ~rank[T.kid[2 * (size_t)c + 1]];
         } else {
@@ -423,14 +414,7 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
       }
       memcpy(&rec[24 + j], &ref, 4);
     }
-    if (A == INFINITY || !(C < 1e30)) {
-      rec[28] = 0.0f;   // 1/A = 0: th = 0, nothing is culled (lim < 0 culls nothing that could win)
-      rec[29] = 0.0f;
-    } else {
-      rec[28] = down_f(1.0 / (A * (1.0 + 1e-6)));
-      rec[29] = up_f(C * (1.0 + 1e-6));
-    }
-    rec[30] = rec[31] = 0.0f;
+    node_cull_consts(co, &rec[28]);
   }
   // stack bound: a node pushes at most (inner children - 1) entries, which
   // stay until its subtree is done: the most along any root-to-node path

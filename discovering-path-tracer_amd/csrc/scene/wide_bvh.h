@@ -40,9 +40,17 @@ enum WideBuild {
 std::string build_wide_bvh(const float* nodes, size_t n, bool int_bits, const float* verts, size_t n_vertex_floats,
                            const uint32_t* idx, size_t n_tris, WideBVH* out, int mode = WIDE_SAH);
 
-// The cull coefficients of one triangle (edges e1 = fl(v1-v0), e2 = fl(v2-v0)):
-// accepted with t <= b implies dist(o, B) <= A*b + Bc*ext(B) + C for every box
-// B containing it.  false: the bound does not apply (no culling).
-bool wide_tri_coeffs(const float e1[3], const float e2[3], double* A, double* Bc, double* C);
+// The cull coefficients of one triangle (edges e1 = fl(v1-v0), e2 = fl(v2-v0)),
+// wide_bvh.cpp: an accepted t_b and the exact T of the same test satisfy
+// t_b >= (T (1 - k1) - k2 S) / (1 + g3), and o + T d lies within
+// eps0 + eps1 S (inf-norm) of the triangle, S = |o - v0|_inf.  false: no
+// bound (the triangle is too large for the |det| >= 1e-6 analysis).
+struct WideCoeffs {
+  double k1, k2, eps0, eps1;
+};
+bool wide_tri_coeffs(const float e1[3], const float e2[3], WideCoeffs* out);
+WideCoeffs coeff_max(const WideCoeffs& a, const WideCoeffs& b);
+// The 4 floats of a node's cull constants from its children's coefficients.
+void node_cull_consts(const WideCoeffs& co, float* out);
 
 }  // namespace pt

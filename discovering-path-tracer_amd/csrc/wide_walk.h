@@ -25,20 +25,24 @@
 // box B when no triangle inside it can have t <= the current best t (closest
 // rays) or t < limit (shadow rays).  The cull test must be exact-safe, i.e.
 // hold for the t the reference's float Moller-Trumbore computes, not the
-// real intersection.  wide_bvh.cpp derives, per triangle, a bound of the
-// form
-//     tri accepted with t_comp <= b   =>   dist(o, B) <= A*b + C
-// from IEEE error bounds of every op of intersectTriangle (:114-157) under its
-// |det| >= 1e-6 acceptance test, with dist the Euclidean distance from the
-// origin to the box (the intersection point lies within rho of the triangle,
-// rho from the barycentric errors, and |X - o| = |T| |d|).  A node stores,
-// for its children, 1/A rounded down and C rounded up; a child is culled iff
-//     b < th,   th = (sqrt(0.999 * dist^2) - C) * (1/A)
-// with dist^2 computed from the slab test's own (lo - o), (hi - o).  The
-// 0.999 covers every rounding of this evaluation (hardware sqrt <= 1 ulp).
-// Culling never removes a triangle that could win or tie, so the answer is
-// the reference's.  tests/wide_check.cpp checks it against the exhaustive
-// walk on millions of rays (grazing, axis-aligned, inside-box origins).
+// real intersection.  wide_bvh.cpp derives from IEEE error bounds of every op
+// of intersectTriangle (:114-157), under its |det| >= 1e-6 and t > 1e-6
+// acceptance: an accepted t_b comes from an exact T at which the ray o + T d
+// lies within eps = eps0 + eps1 S of the triangle (S = |o - v0|_inf), so T is
+// at least the ray's exact entry parameter into B less eps |1/d|_max; and
+// t_b >= (T (1 - k1) - k2 S) / (1 + g3).  A node stores, over the triangles
+// below each child, c1 = min (1 - k1) / (1 + g3) rounded down and E0, E1
+// rounded up (E1 also covering k2 / c1); a child is culled iff
+//     lim < th,  th = c1 * (t_near (1 - 2^-20) - (E0 + E1 Smax) (|1/d|_max + 1))
+// with t_near the slab test's own entry value and Smax the largest |lo - o|,
+// |hi - o| of its own differences (>= S / (1 + 3u): v0 lies in B).  The
+// margins cover every rounding of this evaluation.  Culling never removes a
+// triangle that could win or tie, so the answer is the reference's.
+// (Round 2's first bound used the Euclidean distance to the box instead of
+// the entry parameter: it culled less -- the box nearest the origin is often
+// entered far along the ray -- and needed a square root per child.)
+// tests/wide_check.cpp checks it against the exhaustive walk on hundreds of
+// thousands of rays (grazing, axis-aligned, inside-box origins).
 #pragma once
 #include "pt_isect.h"
 
@@ -48,7 +52,7 @@ namespace ptd {
 //   [0] lo.x[4] [1] hi.x[4] [2] lo.y[4] [3] hi.y[4] [4] lo.z[4] [5] hi.z[4]
 //   [6] child refs (int bits): >= 0 node index, < 0 ~rank of a leaf,
 //       kWideEmpty unused slot
-//   [7] {1/A (rounded down), C (rounded up), 0, 0}
+//   [7] cull constants {c1 (rounded down), E0, E1 (rounded up), 0}
 // Leaf boxes are the reference's leaf boxes bitwise.  Triangle records are
 // stored by rank (the reference tris layout, 3 float4), with rank -> slot.
 constexpr int kWideNodeF4 = 8;
@@ -56,17 +60,21 @@ constexpr int32_t kWideEmpty = (int32_t)0x80000000;
 #ifndef PT_WIDE_LDS_STACK
 #define PT_WIDE_LDS_STACK 8
 #endif
-constexpr int kWideLds = PT_WIDE_LDS_STACK;   // stack entries per lane kept in LDS (power of two)
-static_assert((kWideLds & (kWideLds - 1)) == 0, "LDS stack entries: power of two");
+constexpr int kWideLds = PT_WIDE_LDS_STACK;   // stack entries per lane kept in LDS (a ring)
+// position of stack entry i in the LDS ring
+PT_FN int wide_ring(int i) { return (kWideLds & (kWideLds - 1)) == 0 ? (i & (kWideLds - 1)) : (i % kWideLds); }
 // hits[] markers: the ray needs the exact threaded walk (wide_ray_ok false,
 // or a stack bound violation, which the builder rules out)
 constexpr int kNeedExactClosest = -2;
 constexpr int kNeedExactShadow = 2;
 // direction-length guard of the cull bound: |d|^2 <= 1 + 2e-5 (computed)
 constexpr float kWideMaxD2 = 1.00002f;
+// |1/d_i| bound: with coordinates <= 1e15 every slab t stays finite (< 1e28)
+constexpr float kWideMaxInv = 0x1p40f;
 
 struct WideRay {
   v3 o, d, inv;
+  v3 ainv;      // fl(|1/d_i| + 1)
   float lim;    // closest: best t (1e30 = none yet); shadow: occlusion limit
   int best;     // closest: rank of the best triangle (-1 none); shadow: 1 once occluded
   int shadow;
@@ -96,22 +104,16 @@ PT_FN bool finite_(float x) { return fabs_(x) <= 3.40282347e38f; }
 constexpr float kWideMaxCoord = 1e15f;
 
 PT_FN bool wide_ray_ok(v3 o, v3 d, v3 inv) {
-  return finite_(inv.x) && finite_(inv.y) && finite_(inv.z) && fabs_(o.x) <= kWideMaxCoord &&
+  return fabs_(inv.x) <= kWideMaxInv && fabs_(inv.y) <= kWideMaxInv && fabs_(inv.z) <= kWideMaxInv &&
+         fabs_(o.x) <= kWideMaxCoord &&
          fabs_(o.y) <= kWideMaxCoord && fabs_(o.z) <= kWideMaxCoord && dot(d, d) <= kWideMaxD2;
 }
 
-PT_FN float sqrt_lb_(float x) {
-#if PT_FAST_DEV
-  return __builtin_amdgcn_sqrtf(x);
-#else
-  return sqrt_(x);
-#endif
-}
-
 // One child box: the reference slab test (same ops as slab()), its t_near,
-// and the cull threshold th (culled iff lim < th).
-PT_FN void wide_child(const WideRay& R, float lx, float hx, float ly, float hy, float lz, float hz, float rA,
-                      float C, bool* hit, float* tn, float* th) {
+// and the cull threshold th (culled iff lim < th).  kf: the node's
+// {c1, E0, E1, 0}.
+PT_FN void wide_child(const WideRay& R, float lx, float hx, float ly, float hy, float lz, float hz, float4 kf,
+                      bool* hit, float* tn, float* th) {
   const float dlx = lx - R.o.x, dly = ly - R.o.y, dlz = lz - R.o.z;
   const float dhx = hx - R.o.x, dhy = hy - R.o.y, dhz = hz - R.o.z;
   const float t0x = dlx * R.inv.x, t0y = dly * R.inv.y, t0z = dlz * R.inv.z;
@@ -120,11 +122,13 @@ PT_FN void wide_child(const WideRay& R, float lx, float hx, float ly, float hy, 
   const float tmax = fmin_(fmin_(fmax_(t0x, t1x), fmax_(t0y, t1y)), fmax_(t0z, t1z));
   *hit = tmin <= tmax && tmax >= 0.0f;
   *tn = tmin;
-  const float gx = fmax_(fmax_(dlx, -dhx), 0.0f);
-  const float gy = fmax_(fmax_(dly, -dhy), 0.0f);
-  const float gz = fmax_(fmax_(dlz, -dhz), 0.0f);
-  const float d2 = fma_(gz, gz, fma_(gy, gy, gx * gx));
-  *th = (sqrt_lb_(d2 * 0.999f) - C) * rA;
+  const float smax = fmax_(fmax_(fmax_(fabs_(dlx), fabs_(dhx)), fmax_(fabs_(dly), fabs_(dhy))),
+                           fmax_(fabs_(dlz), fabs_(dhz)));
+  const float eps = fma_(kf.z, smax, kf.y);
+  const float e0 = fma_(-eps, R.ainv.x, fmin_(t0x, t1x) * (1.0f - 0x1p-20f));
+  const float e1 = fma_(-eps, R.ainv.y, fmin_(t0y, t1y) * (1.0f - 0x1p-20f));
+  const float e2 = fma_(-eps, R.ainv.z, fmin_(t0z, t1z) * (1.0f - 0x1p-20f));
+  *th = kf.x * fmax_(fmax_(e0, e1), e2);
 }
 
 #ifndef PT_WIDE_LINEAR
@@ -140,7 +144,7 @@ PT_FN int2 wide_pop(WideRay& R, const int2* lds, int ls, const int2* ovf, long l
     R.lo = R.sp;
     return ovf[(long long)R.sp * os];
   }
-  return lds[(R.sp & (kWideLds - 1)) * ls];
+  return lds[wide_ring(R.sp) * ls];
 }
 
 PT_FN void wide_push(WideRay& R, int2 e, int2* lds, int ls, int2* ovf, long long os) {
@@ -151,10 +155,10 @@ PT_FN void wide_push(WideRay& R, int2 e, int2* lds, int ls, int2* ovf, long long
     return;
   }
   if (R.sp - R.lo == kWideLds) {   // LDS part full: its oldest entry moves to the overflow area
-    ovf[(long long)R.lo * os] = lds[(R.lo & (kWideLds - 1)) * ls];
+    ovf[(long long)R.lo * os] = lds[wide_ring(R.lo) * ls];
     ++R.lo;
   }
-  lds[(R.sp & (kWideLds - 1)) * ls] = e;
+  lds[wide_ring(R.sp) * ls] = e;
   ++R.sp;
 }
 
@@ -162,6 +166,7 @@ PT_FN void wide_start(WideRay& R, v3 o, v3 d, bool shadow, float limit) {
   R.o = o;
   R.d = d;
   R.inv = mk(rcp_(d.x), rcp_(d.y), rcp_(d.z));
+  R.ainv = mk(fabs_(R.inv.x) + 1.0f, fabs_(R.inv.y) + 1.0f, fabs_(R.inv.z) + 1.0f);
   R.shadow = shadow ? 1 : 0;
   R.lim = shadow ? limit : 1e30f;
   R.best = shadow ? 0 : -1;
@@ -216,10 +221,10 @@ PT_FN bool wide_step(WideRay& R, const float4* __restrict__ nodes, const float4*
             c3 = (int)f2u(cf.w);
   bool h0, h1, h2, h3;
   float n0, n1, n2, n3, th0, th1, th2, th3;
-  wide_child(R, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, kf.x, kf.y, &h0, &n0, &th0);
-  wide_child(R, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, kf.x, kf.y, &h1, &n1, &th1);
-  wide_child(R, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, kf.x, kf.y, &h2, &n2, &th2);
-  wide_child(R, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, kf.x, kf.y, &h3, &n3, &th3);
+  wide_child(R, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, kf, &h0, &n0, &th0);
+  wide_child(R, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, kf, &h1, &n1, &th1);
+  wide_child(R, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, kf, &h2, &n2, &th2);
+  wide_child(R, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, kf, &h3, &n3, &th3);
   h0 = h0 && c0 != kWideEmpty && !(R.lim < th0);
   h1 = h1 && c1 != kWideEmpty && !(R.lim < th1);
   h2 = h2 && c2 != kWideEmpty && !(R.lim < th2);

@@ -48,7 +48,7 @@ def lib():
         L.wide_info.argtypes = [F32P, sz, U32P, sz, F32P, sz, ctypes.c_int, I32P, ctypes.c_char_p, sz]
         L.wide_check.argtypes = [F32P, sz, U32P, sz, F32P, sz, ctypes.c_int, F32P, sz, F32P, U64P,
                                  ctypes.c_char_p, sz]
-        L.wide_coeffs.argtypes = [F32P, F32P, F64P]
+        L.wide_coeffs.argtypes = [F32P, F32P, F64P, F32P]
         L.wide_set_mode.argtypes = [ctypes.c_int]
         _LIB = L
     return _LIB
@@ -157,11 +157,16 @@ def run_scene(v, i, n_rays, seed, build=WIDE_SAH):
 
 
 def test_coefficients_bound_shape():
-    """Small triangles get tight relative bounds; huge ones give up culling."""
-    a = np.zeros(3, np.float64)
-    assert lib().wide_coeffs(np.float32([0.02, 0, 0]), np.float32([0, 0.02, 0.001]), a) == 0
-    assert 1.0 < a[0] < 1.01 and a[1] < 0.01 and a[2] < 1e-3
-    assert lib().wide_coeffs(np.float32([2, 0, 0]), np.float32([0, 2, 0]), a) == 1
+    """Small triangles get tight bounds (c1 just below 1, eps tiny); huge ones
+    give up culling."""
+    co = np.zeros(4, np.float64)
+    node = np.zeros(4, np.float32)
+    assert lib().wide_coeffs(np.float32([0.02, 0, 0]), np.float32([0, 0.02, 0.001]), co, node) == 0
+    k1, k2, eps0, eps1 = co
+    assert 0 < k1 < 1e-3 and 0 < k2 < 1e-3 and eps0 < 1e-5 and eps1 < 1e-3
+    c1, E0, E1, _ = node
+    assert 0.999 < c1 < 1.0 and E0 >= eps0 and E1 >= eps1 and E1 >= k2 / c1
+    assert lib().wide_coeffs(np.float32([2, 0, 0]), np.float32([0, 2, 0]), co, node) == 1
 
 
 @BUILDS

@@ -143,9 +143,17 @@ int wide_check(const float* V, size_t nvf, const uint32_t* I, size_t nt, const f
   return 0;
 }
 
-// The per-triangle cull coefficients (wide_tri_coeffs) for the bound test.
-int wide_coeffs(const float* e1, const float* e2, double* abc) {
-  return pt::wide_tri_coeffs(e1, e2, &abc[0], &abc[1], &abc[2]) ? 0 : 1;
+// The per-triangle cull coefficients (wide_tri_coeffs) {k1, k2, eps0, eps1}
+// and the node constants {c1, E0, E1, 0} a node over that one triangle gets.
+int wide_coeffs(const float* e1, const float* e2, double* co, float* node) {
+  pt::WideCoeffs c;
+  if (!pt::wide_tri_coeffs(e1, e2, &c)) return 1;
+  co[0] = c.k1;
+  co[1] = c.k2;
+  co[2] = c.eps0;
+  co[3] = c.eps1;
+  pt::node_cull_consts(c, node);
+  return 0;
 }
 
 }  // extern "C"
