@@ -2085,6 +2085,17 @@ __global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_ker
 // kNeedExact* and wf_shade_kernel walks them exactly (trace_closest /
 // occluded).
 // ---------------------------------------------------------------------------
+// Refill group of the wide walk: single lanes (G = 1).  Lane census of the
+// wide walk with G = 4 on the 10M cloud: 56 % of lane-steps idle while the
+// list still held rays -- a lane could refill only once its whole aligned
+// group of four was idle.  G = 1 vs the earlier choice (2 below 500K
+// triangles, 4 above): sphere 78.0 -> 75.1 ms, 10M cloud 237 -> 206 ms;
+// a refill threshold of 16 or 8 lanes instead of 32: +3-15 % (each refill is
+// an atomic and a dependent ray load the whole wave waits for).
+#ifndef PT_WIDE_G
+#define PT_WIDE_G 1
+#endif
+constexpr int kWideG = PT_WIDE_G;
 #ifndef PT_WIDE_FLUSH_T
 #define PT_WIDE_FLUSH_T 1
 #endif
@@ -2176,17 +2187,15 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
         // leaves, or PT_WIDE_FLUSH_T finished walks waiting on their queue,
         // or nothing left walking
         const unsigned long long waiting = __ballot(p >= 0 && fin && R.nc > 0);
-#ifdef PT_WIDE_PROBE   // lane-state census per step (traced counters 0-4: walking, idle, waiting, steps, flushes)
+#ifdef PT_WIDE_PROBE   // lane-state census per step (traced counters 0-4: walking, idle with rays left
+                       // in the list, idle in the drain, steps, waiting on the leaf queue)
         {
           const unsigned long long walking = __ballot(p >= 0 && !fin), idle_l = __ballot(p < 0);
-          const unsigned long long fl = __ballot(p >= 0 && R.nc > kWideQ - 4) || (int)__popcll(waiting) >= PT_WIDE_FLUSH_T ||
-                                        (waiting && walking == 0ull);
           if (lane == 0) {
             atomicAdd(&P.stats[4], (unsigned long long)__popcll(walking));
-            atomicAdd(&P.stats[5], (unsigned long long)__popcll(idle_l));
-            atomicAdd(&P.stats[6], (unsigned long long)__popcll(waiting));
+            atomicAdd(&P.stats[more ? 5 : 6], (unsigned long long)__popcll(idle_l));
             atomicAdd(&P.stats[7], 1ull);
-            atomicAdd(&P.stats[8], fl ? 1ull : 0ull);
+            atomicAdd(&P.stats[8], (unsigned long long)__popcll(waiting));
           }
         }
 #endif
@@ -2224,6 +2233,19 @@ __device__ __forceinline__ int ray_bin(const Trav& T) {
   const int oct = (T.d.x < 0.0f ? 1 : 0) | (T.d.y < 0.0f ? 2 : 0) | (T.d.z < 0.0f ? 4 : 0);
   return (T.shadow ? 8 : 0) | oct;
 }
+// PT_WF_NULL_INLINE: a null shadow query (trav_null: its answer cannot change
+// the image) is answered by the shading kernel itself, with the wide walk --
+// path_step runs on with "unoccluded" -- instead of taking a list slot, a refill and a lane of
+// the next traversal launch (where it started finished and left its lane
+// idle until the wave's next refill) and a second shading pass.  The path's
+// arithmetic and draws are the same; it only reaches its next real ray a
+// round earlier.  1080p 8 spp, wide walk: sphere 75.1 -> 70.6 ms, 10M cloud
+// 206 -> 181 ms; with the exhaustive threaded walk (PT_OPT_WIDE 0) the 10M
+// cloud measured 2799 -> 2980 ms (paths drift out of phase), so it keeps the
+// null rays in its lists.
+#ifndef PT_WF_NULL_INLINE
+#define PT_WF_NULL_INLINE 1
+#endif
 __global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers B, int cur) {
   if (blockIdx.x == 0 && threadIdx.x == 0) B.counters[2] = 0;   // the next traversal's cursor
   const int count = B.counters[cur];
@@ -2260,6 +2282,12 @@ __global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers
       }
       v3 col;
       need = path_step<false>(P, F, S, T, c, &col);
+#if PT_WF_NULL_INLINE
+      while (P.wide && need && T.shadow == 2) {   // a null shadow query (trav_null): unoccluded, answered here
+        T.res = 0;
+        need = path_step<false>(P, F, S, T, c, &col);
+      }
+#endif
       if (need)
         wf_store_state(B, p, S);
       else
@@ -2427,8 +2455,7 @@ long long wide_trace_lanes() {
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
   int most = 0;
-  for (auto k : {wf_trace_wide_kernel<2>, wf_trace_wide_kernel<4>, wf_trace_wide_kernel<2, true>,
-                 wf_trace_wide_kernel<4, true>}) {
+  for (auto k : {wf_trace_wide_kernel<kWideG>, wf_trace_wide_kernel<kWideG, true>}) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess) return 0;
     most = std::max(most, per_cu);
   }
@@ -2469,8 +2496,7 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
                 : (g2 ? wf_trace_pairs_kernel<2> : wf_trace_pairs_kernel<4>);
   const bool wide = p0.wide && !lds_scene && !p0.pairs;
   if (wide)   // culled wide walk (PT_OPT_WIDE, default)
-    trace = cnt ? (g2 ? wf_trace_wide_kernel<2, true> : wf_trace_wide_kernel<4, true>)
-                : (g2 ? wf_trace_wide_kernel<2> : wf_trace_wide_kernel<4>);
+    trace = cnt ? wf_trace_wide_kernel<kWideG, true> : wf_trace_wide_kernel<kWideG>;
   size_t lds_t = lds;
   if (p0.pairs && !lds_scene) lds_t = (size_t)4 * 64 * p0.pair_depth * sizeof(int);   // the walk stacks
   if (wide) lds_t = 0;

@@ -31,11 +31,12 @@ def main():
     r.render(0, a.spp)
     r.synchronize()
     t = r.traced()
-    walking, idle, waiting, steps, flushes = (t["closest_walks"], t["shadow_walks"], t["nodes"], t["tri_tests"],
-                                              t["primaries"])
+    walking, idle_more, idle_drain, steps, waiting = (t["closest_walks"], t["shadow_walks"], t["nodes"],
+                                                      t["tri_tests"], t["primaries"])
     lanes = 64.0 * max(steps, 1)
-    print(json.dumps({"scene": a.scene, "wave_steps": steps, "walking": walking / lanes, "idle": idle / lanes,
-                      "waiting_on_queue": waiting / lanes, "flush_share": flushes / max(steps, 1)}))
+    print(json.dumps({"scene": a.scene, "wave_steps": steps, "walking": walking / lanes,
+                      "idle_rays_left": idle_more / lanes, "idle_drain": idle_drain / lanes,
+                      "waiting_on_queue": waiting / lanes}))
 
 
 if __name__ == "__main__":
