@@ -84,7 +84,7 @@ def load_scene(name):
     raise SystemExit(f"unknown scene {name}")
 
 
-KERNEL_SOURCES = ("pt_device.hip", "pt_device.h", "pt_isect.h", "wide_walk.h", "pt_math.h")
+KERNEL_SOURCES = ("pt_device.hip", "pt_device.h", "pt_isect.h", "wide_walk.h", "pt_math.h", "scene/wide_bvh.cpp")
 
 
 def kernel_sha1():
