@@ -751,10 +751,11 @@ int wf_reserve(pt_context* c, long long pixels, uint32_t batches, long long* chu
   const size_t n = (size_t)want;
   const size_t b_state = n * ptd::kWfStateF4 * 16, b_col = n * 16, b_rays = n * 32, b_ids = n * 4, b_hits = n * 8;
   char* base = nullptr;
-  PT_HIP(hipMalloc((void**)&base, b_state + b_col + 2 * (b_rays + b_ids) + b_hits + 64));
+  PT_HIP(hipMalloc((void**)&base, 2 * b_state + b_col + 2 * (b_rays + b_ids) + b_hits + 64));
   c->wf_block = base;
   char* q = base;
-  c->wf.state = (float4*)q;    q += b_state;
+  c->wf.state[0] = (float4*)q; q += b_state;
+  c->wf.state[1] = (float4*)q; q += b_state;
   c->wf.colors = (float4*)q;   q += b_col;
   c->wf.rays[0] = (float4*)q;  q += b_rays;
   c->wf.rays[1] = (float4*)q;  q += b_rays;

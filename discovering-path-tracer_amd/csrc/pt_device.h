@@ -177,7 +177,7 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool
 // emits the next rays; finally fold each pixel's sample colours in batch
 // order.  Buffers hold `cap` paths; larger launches run in batch chunks.
 struct WfBuffers {
-  float4* state;     // kWfStateF4 float4 per path (PathSt)
+  float4* state[2];  // per list slot: the waiting path's PathSt, by component (float4 j of slot s at [j * cap + s])
   float4* colors;    // per path radiance
   int* ids[2];       // work lists: path id per slot
   float4* rays[2];   // ... and its ray, 2 float4 per slot: {o.xyz, limit} {d.xyz, shadow}
@@ -186,7 +186,7 @@ struct WfBuffers {
   long long cap;     // paths the buffers hold
 };
 constexpr int kWfStateF4 = 10;
-constexpr size_t kWfBytesPerPath = (size_t)kWfStateF4 * 16 + 16 + 2 * (4 + 32) + 8;
+constexpr size_t kWfBytesPerPath = 2 * (size_t)kWfStateF4 * 16 + 16 + 2 * (4 + 32) + 8;
 // rays a path may trace in one sample: the primary ray, then per bounce the
 // light shadow rays, sss_bounces x (walk ray + light shadow rays) and the
 // next bounce ray

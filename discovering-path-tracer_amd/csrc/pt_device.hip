@@ -74,7 +74,10 @@ struct Hit {
 #define PT_WF_WAVEFLUSH 1   // wf_trace_kernel: wave-wide candidate flush (see there)
 #endif
 #ifndef PT_WF_SORT
-#define PT_WF_SORT 0   // wf_shade_kernel: bin each workgroup's next rays by kind and octant (see there)
+#define PT_WF_SORT 1   // wf_shade_kernel: bin each workgroup's next rays (see there)
+#endif
+#ifndef PT_WF_SORT_PHASE
+#define PT_WF_SORT_PHASE 1   // ... by the phase the path waits in (0: by ray kind and octant)
 #endif
 #ifndef PT_WF_SHADOW_QUEUE
 #define PT_WF_SHADOW_QUEUE 1   // wf_trace_kernel: shadow rays queue their leaves too (see there)
@@ -1584,26 +1587,27 @@ __global__ __launch_bounds__(256, PT_SM_MIN_BLOCKS) void render_sm_kernel(Render
 // ===========================================================================
 static_assert(sizeof(PathSt) == kWfStateF4 * 16, "PathSt is stored as kWfStateF4 float4");
 
-// A path's state is one 160-B record (kWfStateF4 float4): the live paths of
-// a list are sparse after the first bounces, and a record per path keeps
-// each one in one or two lines (by component, 16 B per line touched: sphere
-// +2.5 %, 10M cloud +4 %).  A list slot's ray is stored by component --
-// rays[s] and rays[cap + s] -- since a wave reads and writes consecutive
-// slots.
-__device__ __forceinline__ void wf_load_state(const WfBuffers& B, long long p, PathSt* S) {
-  const float4* __restrict__ src = B.state + (size_t)p * kWfStateF4;
+// A waiting path's state travels with its ray: list slot s holds both, each
+// stored by component (float4 j of the state at state[list][j * cap + s];
+// the ray at rays[list][s] and rays[list][cap + s]).  A wave reads and writes
+// consecutive slots, so every access instruction covers consecutive 16-B
+// words.  (Indexed by path, the state of a list's sparse surviving paths
+// cost 64 lines per instruction and a dependent load of the path id first;
+// by path and by component it measured +2.5 % / +4 %.)
+__device__ __forceinline__ void wf_load_state(const WfBuffers& B, int list, long long slot, PathSt* S) {
+  const float4* __restrict__ src = B.state[list] + slot;
   float4 v[kWfStateF4];
 #pragma unroll
-  for (int i = 0; i < kWfStateF4; ++i) v[i] = src[i];
+  for (int j = 0; j < kWfStateF4; ++j) v[j] = src[(size_t)j * (size_t)B.cap];
   __builtin_memcpy(S, v, sizeof(PathSt));
 }
 
-__device__ __forceinline__ void wf_store_state(const WfBuffers& B, long long p, const PathSt& S) {
-  float4* __restrict__ dst = B.state + (size_t)p * kWfStateF4;
+__device__ __forceinline__ void wf_store_state(const WfBuffers& B, int list, long long slot, const PathSt& S) {
+  float4* __restrict__ dst = B.state[list] + slot;
   float4 v[kWfStateF4];
   __builtin_memcpy(v, &S, sizeof(PathSt));
 #pragma unroll
-  for (int i = 0; i < kWfStateF4; ++i) dst[i] = v[i];
+  for (int j = 0; j < kWfStateF4; ++j) dst[(size_t)j * (size_t)B.cap] = v[j];
 }
 
 __device__ __forceinline__ void wf_store_ray(float4* __restrict__ rays, long long cap, int slot, const Trav& T) {
@@ -1666,6 +1670,7 @@ __global__ __launch_bounds__(256) void wf_gen_kernel(RenderParams P, WfBuffers B
   const long long g = g0 + (long long)blockIdx.x * 256 + threadIdx.x;   // paths [g0, g0 + n)
   bool need = false, gen = false;
   Trav T;
+  PathSt S;
   if (g - g0 < n) {
     const long long pp = g / (long long)P.n_batches;
     CamFrame F;
@@ -1683,18 +1688,19 @@ __global__ __launch_bounds__(256) void wf_gen_kernel(RenderParams P, WfBuffers B
       v3 col = mk(0.0f, 0.0f, 0.0f);
       if (pixel_live(P, F.ndcX0, F.ndcY0)) {
         gen = true;
-        PathSt S;
         S.s = (uint32_t)(g - pp * (long long)P.n_batches);
         S.phase = PH_BEGIN;
         Ctr c = {0u, 0u, 0u, 0u, 0u};
         need = path_step<false>(P, F, S, T, c, &col);
-        if (need) wf_store_state(B, g, S);
       }
       if (!need) B.colors[g] = make_float4(col.x, col.y, col.z, 1.0f);
     }
   }
   const int slot = wave_slot(&B.counters[0], need);
-  if (need) wf_push(B, 0, slot, (int)g, T);
+  if (need) {
+    wf_push(B, 0, slot, (int)g, T);
+    wf_store_state(B, 0, slot, S);
+  }
   if (CNT) {
     const unsigned long long m = __ballot(gen);
     if (__lane_id() == 0 && m) atomicAdd(&P.stats[8], (unsigned long long)__popcll(m));
@@ -2263,13 +2269,17 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
 // Shading of every path in list `cur` (path_step on the returned hit);
 // paths that need another ray go to list cur^1, finished ones store colour.
 //
-// PT_WF_SORT: a workgroup appends its next rays binned by kind (closest-hit
-// / shadow) and direction octant -- one atomic per workgroup, a counting sort
-// in LDS -- so the traversal kernel's waves, which take consecutive list
-// slots, get rays of one kind heading the same way: fewer divergent branches
-// and more shared nodes per wave.  A ray's result does not depend on where
-// it sits in the list, so the image is unchanged.  Measured at 1080p 8 spp:
-// sphere -0.5 %, 1M cloud +0.5 %, 10M cloud +3.5 % -- off by default.
+// PT_WF_SORT: a workgroup appends its next rays binned -- one atomic per
+// workgroup, a counting sort in LDS -- by the phase the path waits in
+// (PT_WF_SORT_PHASE; closest-hit and shadow rays apart, and the next shading
+// pass runs one case of path_step per wave instead of several), or by ray
+// kind and direction octant.  A ray's result does not depend on where it
+// sits in the list, so the image is unchanged.  Measured at 1080p 8 spp with
+// the wide walk (G = 1, null queries inline): sphere 70.7 -> 65.0 ms, 10M
+// cloud 181.5 -> 158.0 ms by phase; by kind and octant 65.7 / 158.3; by
+// phase and octant 65.7 / 159.1.  (With the exhaustive walks and refill
+// groups of round 2's first half, kind and octant had measured sphere -0.5 %,
+// 10M cloud +3.5 %.)
 __device__ __forceinline__ int ray_bin(const Trav& T) {
   const int oct = (T.d.x < 0.0f ? 1 : 0) | (T.d.y < 0.0f ? 2 : 0) | (T.d.z < 0.0f ? 4 : 0);
   return (T.shadow ? 8 : 0) | oct;
@@ -2287,11 +2297,15 @@ __device__ __forceinline__ int ray_bin(const Trav& T) {
 #ifndef PT_WF_NULL_INLINE
 #define PT_WF_NULL_INLINE 1
 #endif
-__global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers B, int cur) {
+#ifndef PT_WF_SHADE_MIN_BLOCKS
+#define PT_WF_SHADE_MIN_BLOCKS 4
+#endif
+constexpr int kWfBins = 16;
+__global__ __launch_bounds__(256, PT_WF_SHADE_MIN_BLOCKS) void wf_shade_kernel(RenderParams P, WfBuffers B, int cur) {
   if (blockIdx.x == 0 && threadIdx.x == 0) B.counters[2] = 0;   // the next traversal's cursor
   const int count = B.counters[cur];
   CamFrame F = {};   // camera frame: used by PH_BEGIN only
-  __shared__ int bin_cnt[16], bin_base[16], wg_base;
+  __shared__ int bin_cnt[kWfBins], bin_base[kWfBins], wg_base;
   __shared__ int cand_buf[4][kCand][64];   // exact walks of handed-back rays
   int* cand = &cand_buf[threadIdx.x >> 6][0][threadIdx.x & 63];
   for (int base = (int)blockIdx.x * 256; base < count; base += (int)gridDim.x * 256) {
@@ -2299,10 +2313,10 @@ __global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers
     bool need = false;
     int p = -1;
     Trav T;
+    PathSt S;
     if (i < count) {
       p = B.ids[cur][i];
-      PathSt S;
-      wf_load_state(B, p, &S);
+      wf_load_state(B, cur, i, &S);
       float4 r0, r1;
       wf_load_ray(B.rays[cur], B.cap, i, &r0, &r1);
       const float2 h = B.hits[i];
@@ -2329,32 +2343,40 @@ __global__ __launch_bounds__(256) void wf_shade_kernel(RenderParams P, WfBuffers
         need = path_step<false>(P, F, S, T, c, &col);
       }
 #endif
-      if (need)
-        wf_store_state(B, p, S);
-      else
-        B.colors[p] = make_float4(col.x, col.y, col.z, 1.0f);
+      if (!need) B.colors[p] = make_float4(col.x, col.y, col.z, 1.0f);
     }
     if (PT_WF_SORT) {   // uniform: every thread of the workgroup runs each iteration
       const int tid = (int)threadIdx.x;
-      if (tid < 16) bin_cnt[tid] = 0;
+      if (tid < kWfBins) bin_cnt[tid] = 0;
       __syncthreads();
+#if PT_WF_SORT_PHASE
+      const int bin = need ? (S.phase & 7) : 0;   // the phase the path waits in
+#else
       const int bin = need ? ray_bin(T) : 0;
+#endif
       const int rank = need ? atomicAdd(&bin_cnt[bin], 1) : 0;
       __syncthreads();
       if (tid == 0) {
         int acc = 0;
-        for (int k = 0; k < 16; ++k) {
+        for (int k = 0; k < kWfBins; ++k) {
           bin_base[k] = acc;
           acc += bin_cnt[k];
         }
         wg_base = acc ? atomicAdd(&B.counters[cur ^ 1], acc) : 0;
       }
       __syncthreads();
-      if (need) wf_push(B, cur ^ 1, wg_base + bin_base[bin] + rank, p, T);
+      if (need) {
+        const int slot = wg_base + bin_base[bin] + rank;
+        wf_push(B, cur ^ 1, slot, p, T);
+        wf_store_state(B, cur ^ 1, slot, S);
+      }
       __syncthreads();   // the bins are reused by the next iteration
     } else {
       const int slot = wave_slot(&B.counters[cur ^ 1], need);
-      if (need) wf_push(B, cur ^ 1, slot, p, T);
+      if (need) {
+        wf_push(B, cur ^ 1, slot, p, T);
+        wf_store_state(B, cur ^ 1, slot, S);
+      }
     }
   }
 }
@@ -2575,6 +2597,7 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
       for (int k = 0; k < 2; ++k) {
         bh[1].rays[k] = b.rays[k] + sb;   // slot s of half 1: rays[sb + s], rays[cap + sb + s]
         bh[1].ids[k] = b.ids[k] + sb;
+        bh[1].state[k] = b.state[k] + sb;
       }
       bh[1].hits = b.hits + sb;
       bh[1].counters = b.counters + 4;
