@@ -2279,7 +2279,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
 // cloud 181.5 -> 158.0 ms by phase; by kind and octant 65.7 / 158.3; by
 // phase and octant 65.7 / 159.1.  (With the exhaustive walks and refill
 // groups of round 2's first half, kind and octant had measured sphere -0.5 %,
-// 10M cloud +3.5 %.)
+// 10M cloud +3.5 %; the exhaustive walk keeps the unsorted lists.)
 __device__ __forceinline__ int ray_bin(const Trav& T) {
   const int oct = (T.d.x < 0.0f ? 1 : 0) | (T.d.y < 0.0f ? 2 : 0) | (T.d.z < 0.0f ? 4 : 0);
   return (T.shadow ? 8 : 0) | oct;
@@ -2345,7 +2345,7 @@ __global__ __launch_bounds__(256, PT_WF_SHADE_MIN_BLOCKS) void wf_shade_kernel(R
 #endif
       if (!need) B.colors[p] = make_float4(col.x, col.y, col.z, 1.0f);
     }
-    if (PT_WF_SORT) {   // uniform: every thread of the workgroup runs each iteration
+    if (PT_WF_SORT && P.wide) {   // uniform: every thread of the workgroup runs each iteration
       const int tid = (int)threadIdx.x;
       if (tid < kWfBins) bin_cnt[tid] = 0;
       __syncthreads();
