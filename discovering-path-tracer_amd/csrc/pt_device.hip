@@ -2103,9 +2103,6 @@ __global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_ker
 #ifndef PT_WIDE_G
 #define PT_WIDE_G 1
 #endif
-#ifndef PT_WIDE_CLAIM
-#define PT_WIDE_CLAIM 0
-#endif
 constexpr int kWideG = PT_WIDE_G;
 #ifndef PT_WIDE_FLUSH_T
 #define PT_WIDE_FLUSH_T 1
@@ -2134,12 +2131,6 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
   const float4* __restrict__ rays = B.rays[cur];
   int p = -1;   // list slot this lane traces
   bool more = true;
-  // PT_WIDE_CLAIM: the wave claims list slots in batches -- [wb, we), wave-
-  // uniform -- so most refills take slots without an atomic on the shared
-  // cursor; a batch is about 1/8 of the wave's share of the list
-  int wb = 0, we = 0;
-  bool dry = false;   // the cursor has passed the end of the list
-  const int batch = PT_WIDE_CLAIM ? min(256, count / (int)(gridDim.x * 4 * 8)) : 0;
   WideRay R;
   R.cur = -1;
   R.sp = R.lo = 0;
@@ -2152,36 +2143,16 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
     for (int sh = 1; sh < G; sh <<= 1) gm &= gm >> sh;
     gm &= group_lead<G>();
     const int ng = (int)__popcll(gm);
-    if (PT_WIDE_CLAIM) more = !dry || wb < we;
     if (more && ng * G >= PT_WF_REFILL) {
       const int need = ng * G;
-      int base = 0, avail = 0, nb = 0, ne = 0;
-      if (PT_WIDE_CLAIM) {
-        avail = we - wb;
-        if (!dry && avail < need) {   // claim a batch
-          const int want = max(need - avail, batch);
-          int b0 = 0;
-          if (lane == 0) b0 = atomicAdd(&B.counters[2], want);
-          b0 = __builtin_amdgcn_readfirstlane(__shfl(b0, 0));
-          if (b0 + want >= count) dry = true;
-          nb = min(b0, count);
-          ne = min(b0 + want, count);
-        }
-      } else {
-        if (lane == 0) base = atomicAdd(&B.counters[2], need);
-        base = __shfl(base, 0);
-        if (base + need >= count) more = false;
-      }
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&B.counters[2], need);
+      base = __shfl(base, 0);
+      if (base + need >= count) more = false;
       const int lead = lane & ~(G - 1);
       if ((gm >> lead) & 1ull) {
-        const int j = (int)__popcll(gm & ((1ull << lead) - 1ull)) * G + (lane - lead);
-        int slot = base + j;
-        bool ok = slot < count;
-        if (PT_WIDE_CLAIM) {
-          slot = j < avail ? wb + j : nb + (j - avail);
-          ok = j < avail || slot < ne;
-        }
-        if (ok) {
+        const int slot = base + (int)__popcll(gm & ((1ull << lead) - 1ull)) * G + (lane - lead);
+        if (slot < count) {
           float4 r0, r1;
           wf_load_ray(rays, B.cap, slot, &r0, &r1);
           const int kind = __float_as_int(r1.w);   // 0 closest, 1 shadow, 2 null shadow (trav_null)
@@ -2195,15 +2166,6 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
             p = slot;
           }
         }
-      }
-      if (PT_WIDE_CLAIM) {   // what the refill took
-        if (need <= avail) {
-          wb += need;
-        } else {
-          wb = min(nb + (need - avail), ne);
-          we = ne;
-        }
-        more = !dry || wb < we;
       }
     }
     if (!more && __ballot(p >= 0) == 0ull) break;
