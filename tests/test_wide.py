@@ -50,6 +50,8 @@ def lib():
                                  ctypes.c_char_p, sz]
         L.wide_coeffs.argtypes = [F32P, F32P, F64P, F32P]
         L.wide_set_mode.argtypes = [ctypes.c_int]
+        L.wide_dump.argtypes = [F32P, sz, U32P, sz, F32P, sz, ctypes.c_int, F32P, sz, I32P, ctypes.c_char_p, sz]
+        L.wide_dump.restype = ctypes.c_longlong
         _LIB = L
     return _LIB
 
@@ -219,3 +221,70 @@ def test_wide_info_and_refusals():
     bad[1, 0] = bad[0, 0] - 1.0   # a child box sticking out of the root
     assert L.wide_info(v, v.size, idx, idx.size // 3, bad.reshape(-1), nodes.size // 8, 0, info, err, 256) == 1
     assert b"contain" in err.value
+
+
+def _dump(v, idx, nodes, build):
+    L = lib()
+    L.wide_set_mode(build)
+    nt = idx.size // 3
+    cap = 32 * (nt + 8)
+    out = np.zeros(cap, np.float32)
+    rt = np.zeros(nt, np.int32)
+    err = ctypes.create_string_buffer(256)
+    n = L.wide_dump(v, v.size, idx, nt, nodes, nodes.size // 8, 0, out, cap, rt, err, 256)
+    assert n > 0, err.value.decode()
+    return out[:n].reshape(-1, 32).copy(), rt
+
+
+@BUILDS
+def test_wide_tree_invariants(build):
+    """The premises of the walk's exactness (wide_walk.h), on the built tree:
+    every leaf child carries the reference's leaf box bitwise and every leaf
+    rank appears once; every inner child's box contains every leaf box below
+    it; the SAH build is deterministic (threaded, same tree twice)."""
+    sv, si = scenes.displaced_sphere(subdiv=4)
+    v, idx, nodes = _scene(sv, si)
+    W, rank_tri = _dump(v, idx, nodes, build)
+    if build == WIDE_SAH:
+        W2, rank_tri2 = _dump(v, idx, nodes, build)
+        assert np.array_equal(W.view(np.uint32), W2.view(np.uint32)) and np.array_equal(rank_tri, rank_tri2)
+    N = nodes.reshape(-1, 8)
+    # reference leaves in right-first DFS order -> their boxes by rank
+    order, st = [], [0]
+    while st:
+        k = st.pop()
+        left, right = N[k, 3], N[k, 7]
+        if left == -1:
+            order.append(k)
+        else:
+            st += [int(left), int(right)]
+    leaf_lo = N[order, 0:3]
+    leaf_hi = N[order, 4:7]
+    assert np.array_equal(N[order, 7].astype(np.int64), rank_tri.astype(np.int64))
+    refs = W[:, 24:28].copy().view(np.int32)
+    lo = np.stack([W[:, 0:4], W[:, 8:12], W[:, 16:20]], -1)    # node, child, axis
+    hi = np.stack([W[:, 4:8], W[:, 12:16], W[:, 20:24]], -1)
+    seen = np.zeros(len(order), np.int32)
+
+    def leaves_below(w):
+        out = []
+        for j in range(4):
+            r = int(refs[w, j])
+            if r == -2 ** 31:
+                continue
+            out += [~r] if r < 0 else leaves_below(r)
+        return out
+
+    for w in range(len(W)):
+        for j in range(4):
+            r = int(refs[w, j])
+            if r == -2 ** 31:
+                continue
+            if r < 0:
+                seen[~r] += 1
+                assert np.array_equal(lo[w, j].view(np.uint32), leaf_lo[~r].view(np.uint32))
+                assert np.array_equal(hi[w, j].view(np.uint32), leaf_hi[~r].view(np.uint32))
+            elif w < 64 or w % 97 == 0:   # containment of every leaf below (a sample of inner nodes)
+                below = leaves_below(r)
+                assert (leaf_lo[below] >= lo[w, j]).all() and (leaf_hi[below] <= hi[w, j]).all()
+    assert (seen == 1).all()

@@ -65,6 +65,26 @@ int wide_info(const float* V, size_t nvf, const uint32_t* I, size_t nt, const fl
   return 0;
 }
 
+// The built wide tree itself: node floats (32 per node) into nodes (room for
+// cap floats) and rank -> triangle slot into rank_tri (room for n_tris).
+// Returns the float count, or -1 (err).
+long long wide_dump(const float* V, size_t nvf, const uint32_t* I, size_t nt, const float* N, size_t nn, int int_bits,
+                    float* nodes, size_t cap, int32_t* rank_tri, char* err, size_t errlen) {
+  pt::WideBVH w;
+  const std::string why = pt::build_wide_bvh(N, nn, int_bits != 0, V, nvf, I, nt, &w, g_mode);
+  if (!why.empty()) {
+    snprintf(err, errlen, "%s", why.c_str());
+    return -1;
+  }
+  if (w.nodes.size() > cap || w.rank_tri.size() != nt) {
+    snprintf(err, errlen, "buffer too small");
+    return -1;
+  }
+  memcpy(nodes, w.nodes.data(), w.nodes.size() * sizeof(float));
+  memcpy(rank_tri, w.rank_tri.data(), nt * sizeof(int32_t));
+  return (long long)w.nodes.size();
+}
+
 // rays: n x 8 floats {o.xyz, d.xyz, kind (0 closest, 1 shadow), limit}.
 // out: n x 4 {wide t|lim, wide hit/occluded (-1 exact walk needed), oracle t, oracle hit/occluded}.
 // stats: [0] closest mismatches [1] shadow mismatches [2] exact hand-backs
