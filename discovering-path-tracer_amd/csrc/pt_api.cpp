@@ -404,7 +404,8 @@ struct pt_context {
   int opt_kernel = 0;         // PT_OPT_KERNEL: 0 auto, 1 path-recursive, 2 lane state machine, 3 wavefront
   int opt_sm_batch = 1;       // PT_OPT_SM_BATCH
   int opt_cull = 1;           // PT_OPT_PRIMARY_CULL
-  int opt_wf_paths = 0;       // PT_OPT_WF_PATHS (0 = 2^24)
+  int opt_wf_paths = 0;       // PT_OPT_WF_PATHS (0 = 2^27)
+  long long wf_fail = 0;      // wavefront paths whose allocation failed (0: none)
   int opt_count = 0;          // PT_OPT_COUNT_TRACED
   int opt_pairs = 0;          // PT_OPT_PAIRS
   int opt_wide_build = 1;     // PT_OPT_WIDE_BUILD (pt::WideBuild; read at upload)
@@ -714,9 +715,13 @@ int upload_ints(const std::vector<int>& h, int** d, size_t* cap) {
   if (!h.empty()) PT_HIP(hipMemcpy(*d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice));
   return PT_OK;
 }
-// Wavefront buffers for `paths` paths in one allocation.  Up to 2^24 paths
-// (4.3 GB) are kept per launch; more batches run in chunks of that size.
-constexpr long long kWfMaxPaths = 1ll << 24;
+// Wavefront buffers for `paths` paths in one allocation.  Up to 2^27 paths
+// (416 B each: 56 GB of the 288-GB HBM) are kept per launch, so config 4's
+// 4K x 16 spp frame (133M paths) runs as one chunk: every ray round has 8x
+// the rays of a 2^24 chunk, and each round's drain (its longest walk) is paid
+// 65 times per frame instead of 520 -- 767 -> 560 ms (2^26: 591).  More
+// batches run in chunks of that size; an allocation that fails halves it.
+constexpr long long kWfMaxPaths = 1ll << 27;
 constexpr int kWfAutoTris = 32768;
 constexpr int kWfWideAutoTris = 16384;   // ... with the culled wide walk (render_impl)
 // The root's assembly table for frames rendered with params p: per rank its
@@ -741,17 +746,27 @@ int unpack_table(pt_context* c, const ptd::RenderParams& p, const std::vector<fl
 }
 int wf_reserve(pt_context* c, long long pixels, uint32_t batches, long long* chunk_paths) {
   const long long limit = c->opt_wf_paths > 0 ? c->opt_wf_paths : kWfMaxPaths;
-  const long long want = std::max(pixels, std::min(pixels * (long long)batches, limit));
+  long long want = std::max(pixels, std::min(pixels * (long long)batches, limit));
+  if (c->wf_fail > 0) want = std::max(pixels, std::min(want, c->wf_fail / 2));   // an earlier allocation failed
   if (want > 0x7fffffffll) return fail(PT_ERR_UNSUPPORTED, "frame too large for the wavefront kernel");
   *chunk_paths = want;
   if (want <= c->wf.cap) return PT_OK;
   { const int rc_ = quiesce(c); if (rc_) return rc_; }
   dev_free(c->wf_block);
   c->wf = ptd::WfBuffers{};
-  const size_t n = (size_t)want;
-  const size_t b_state = n * ptd::kWfStateF4 * 16, b_col = n * 16, b_rays = n * 32, b_ids = n * 4, b_hits = n * 8;
   char* base = nullptr;
-  PT_HIP(hipMalloc((void**)&base, 2 * b_state + b_col + 2 * (b_rays + b_ids) + b_hits + 64));
+  size_t n = 0, b_state = 0, b_col = 0, b_rays = 0, b_ids = 0, b_hits = 0;
+  for (;;) {
+    n = (size_t)want;
+    b_state = n * ptd::kWfStateF4 * 16, b_col = n * 16, b_rays = n * 32, b_ids = n * 4, b_hits = n * 8;
+    const hipError_t e = hipMalloc((void**)&base, 2 * b_state + b_col + 2 * (b_rays + b_ids) + b_hits + 64);
+    if (e == hipSuccess) break;
+    (void)hipGetLastError();
+    if (e != hipErrorOutOfMemory || want <= pixels) PT_HIP(e);
+    c->wf_fail = want;
+    want = std::max(pixels, want / 2);   // less memory than that: smaller chunks
+  }
+  *chunk_paths = want;
   c->wf_block = base;
   char* q = base;
   c->wf.state[0] = (float4*)q; q += b_state;

@@ -282,8 +282,9 @@ int pt_dist_finalize(pt_context* ctx);
  * are not LDS-resident, else path-recursive), 1 path-recursive, 2 lane state
  * machine (slower on every scene measured; kept for comparison), 3 wavefront
  * pipeline (paths held in device memory, traversal and shading in separate
- * kernels; ~224 bytes of device memory per pixel x sample, at most 2^24 paths
- * per chunk; not with stats mode).  Output is identical for every value.
+ * kernels; 416 bytes of device memory per pixel x sample, at most 2^27 paths
+ * per chunk; not with stats mode; auto picks it from 16384 triangles with the
+ * culled wide walk).  Output is identical for every value.
  * PT_OPT_SM_BATCH: state machine only — finished rays wait until this many
  * lanes of the wave need shading (1..64, default 1).  Output is identical. */
 #define PT_OPT_KERNEL 4
@@ -296,8 +297,9 @@ int pt_dist_finalize(pt_context* ctx);
  * Path-recursive and wavefront kernels; output is identical either way. */
 #define PT_OPT_PRIMARY_CULL 6
 /* PT_OPT_WF_PATHS: wavefront kernel only — paths (pixel x sample) held in
- * device memory per chunk; 0 = 2^24 (3.8 GB).  A launch with more runs in
- * chunks of whole batches (at least one batch of the frame per chunk).
+ * device memory per chunk; 0 = 2^27 (56 GB; halved until the allocation
+ * succeeds).  A launch with more runs in chunks of whole batches (at least
+ * one batch of the frame per chunk).
  * Output is identical for every value. */
 #define PT_OPT_WF_PATHS 7
 /* PT_OPT_ITEM_ORDER: 1 (default) = live items (tile parts) launched heaviest
