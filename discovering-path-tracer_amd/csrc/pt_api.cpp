@@ -368,7 +368,7 @@ struct pt_context {
   // slot, per-lane stack overflow areas (grown on demand)
   float4* d_wide = nullptr;
   float4* d_wide_tris = nullptr;
-  int* d_wide_tri_of = nullptr;
+  int* d_wide_rank_of = nullptr;
   int2* d_wide_ovf = nullptr;
   long long wide_ovf_lanes = 0;
   int n_wide = 0, wide_stack = 0;
@@ -805,13 +805,14 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.pair_depth = 0;
   p.wide = nullptr;
   p.wide_tris = nullptr;
-  p.wide_tri_of = nullptr;
+  p.wide_rank_of = nullptr;
   p.wide_ovf = nullptr;
   p.wide_ovf_lanes = 0;
   p.wide_stack = 0;
   p.wide_handback = 0;
   p.nodes = c->stats_mode ? c->d_nodes_full : c->d_nodes;
   p.tris = c->d_tris;
+  p.hit_tris = c->d_tris;
   p.lights = c->d_lights_dev;
   p.accum = c->d_accum;
   p.stats = c->d_stats;
@@ -997,7 +998,8 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
       }
       p.wide = c->d_wide;
       p.wide_tris = c->d_wide_tris;
-      p.wide_tri_of = c->d_wide_tri_of;
+      p.wide_rank_of = c->d_wide_rank_of;
+      p.hit_tris = c->d_wide_tris;   // closest hits come back as ranks
       p.wide_ovf = c->d_wide_ovf;
       p.wide_ovf_lanes = c->wide_ovf_lanes;
       p.wide_stack = c->wide_stack;
@@ -1086,7 +1088,7 @@ int pt_destroy(pt_context* c) {
   dev_free(c->d_pairs);
   dev_free(c->d_wide);
   dev_free(c->d_wide_tris);
-  dev_free(c->d_wide_tri_of);
+  dev_free(c->d_wide_rank_of);
   dev_free(c->d_wide_ovf);
   dev_free(c->d_tris);
   dev_free(c->d_lights);
@@ -1169,7 +1171,7 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   dev_free(c->d_pairs);
   dev_free(c->d_wide);
   dev_free(c->d_wide_tris);
-  dev_free(c->d_wide_tri_of);
+  dev_free(c->d_wide_rank_of);
   c->n_wide = 0;
   c->has_scene = false;
   const int T = (int)(n_indices / 3);
@@ -1196,15 +1198,20 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   PT_HIP(hipMemcpyAsync(st.v, vertices, n_vertex_floats * sizeof(float), hipMemcpyHostToDevice, c->stream));
   PT_HIP(hipMemcpyAsync(st.i, indices, n_indices * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream));
   PT_HIP(ptd::launch_setup_tris(st.v, st.i, T, c->d_tris, c->stream));
+  std::vector<int> rank_of_host(wide_reason.empty() ? (size_t)T : 0);
   if (wide_reason.empty()) {
     PT_HIP(hipMalloc((void**)&c->d_wide, wide.nodes.size() * sizeof(float)));
-    PT_HIP(hipMalloc((void**)&c->d_wide_tri_of, (size_t)T * sizeof(int)));
+    PT_HIP(hipMalloc((void**)&c->d_wide_rank_of, (size_t)T * sizeof(int)));
     PT_HIP(hipMalloc((void**)&c->d_wide_tris, (size_t)T * 3 * sizeof(float4)));
     PT_HIP(hipMemcpyAsync(c->d_wide, wide.nodes.data(), wide.nodes.size() * sizeof(float), hipMemcpyHostToDevice,
                           c->stream));
-    PT_HIP(hipMemcpyAsync(c->d_wide_tri_of, wide.rank_tri.data(), (size_t)T * sizeof(int), hipMemcpyHostToDevice,
+    PT_HIP(hipMemcpyAsync(c->d_wide_rank_of, wide.rank_tri.data(), (size_t)T * sizeof(int), hipMemcpyHostToDevice,
                           c->stream));
-    PT_HIP(ptd::launch_gather_tris(c->d_tris, c->d_wide_tri_of, T, c->d_wide_tris, c->stream));
+    PT_HIP(ptd::launch_gather_tris(c->d_tris, c->d_wide_rank_of, T, c->d_wide_tris, c->stream));
+    // then the same buffer becomes slot -> rank (the kernels' only use of it)
+    for (int r = 0; r < T; ++r) rank_of_host[wide.rank_tri[r]] = r;
+    PT_HIP(hipMemcpyAsync(c->d_wide_rank_of, rank_of_host.data(), (size_t)T * sizeof(int), hipMemcpyHostToDevice,
+                          c->stream));
   }
   PT_HIP(hipStreamSynchronize(c->stream));
   c->n_wide = wide_reason.empty() ? wide.n_nodes : 0;

@@ -85,11 +85,12 @@ struct RenderParams {
   const float4* pairs;      // child-pair records, or null (threaded walk)
   int pair_depth;           // tree depth: entries of the pair walk's stack
   // culled wide walk (wide_walk.h), or null: 4-wide nodes, triangle records
-  // by leaf rank, rank -> triangle slot, per-lane stack overflow areas
+  // by leaf rank, triangle slot -> rank, per-lane stack overflow areas
   // (wide_ovf_lanes lanes of wide_stack entries, lane-strided)
+  const float4* hit_tris;   // the records a closest hit's index refers to: wide_tris (by rank) with the wide walk, else tris
   const float4* wide;
   const float4* wide_tris;
-  const int* wide_tri_of;
+  const int* wide_rank_of;
   int2* wide_ovf;
   long long wide_ovf_lanes;
   int wide_stack;

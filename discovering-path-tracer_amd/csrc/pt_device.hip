@@ -372,7 +372,7 @@ __device__ __forceinline__ v3 sample_hemisphere(v3 n, uint32_t* rng) {
 }
 
 __device__ __forceinline__ v3 tri_normal(const RenderParams& P, int tri) {
-  const float4 C = P.tris[3 * tri + 2];
+  const float4 C = P.hit_tris[3 * tri + 2];
   return mk(C.y, C.z, C.w);
 }
 
@@ -898,6 +898,7 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
     __syncthreads();
     P.nodes = lds_scene;
     P.tris = lds_scene + nn;
+    P.hit_tris = P.tris;   // no wide walk here: hits are slots
   }
   {
     const v3 cpos = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
@@ -1501,6 +1502,7 @@ __global__ __launch_bounds__(256, PT_SM_MIN_BLOCKS) void render_sm_kernel(Render
     __syncthreads();
     P.nodes = lds_scene;
     P.tris = lds_scene + nn;
+    P.hit_tris = P.tris;   // no wide walk here: hits are slots
   }
   // one pixel per lane, all its samples in order: 16x16 tile per workgroup,
   // 8x8 per wave
@@ -1848,6 +1850,7 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
     __syncthreads();
     P.nodes = lds_scene;
     P.tris = lds_scene + nn;
+    P.hit_tris = P.tris;   // no wide walk here: hits are slots
   }
   const int wave = tid >> 6, lane = tid & 63;
   __shared__ int cand_buf[4][kCand][64];
@@ -2177,7 +2180,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
           int res;
           if (exact) res = R.shadow ? kNeedExactShadow : kNeedExactClosest;
           else if (R.shadow) res = R.best;
-          else res = R.best >= 0 ? P.wide_tri_of[R.best] : -1;
+          else res = R.best;   // the rank (hit_tris = wide_tris)
           B.hits[p] = make_float2(R.lim, __int_as_float(res));
           p = -1;
         }
@@ -2217,7 +2220,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
           }
         }
         if (p >= 0 && fin && R.nc == 0) {
-          const int res = R.shadow ? R.best : (R.best >= 0 ? P.wide_tri_of[R.best] : -1);
+          const int res = R.best;   // occluded, or the hit's rank (hit_tris = wide_tris; the record the flush just tested)
           B.hits[p] = make_float2(R.lim, __int_as_float(res));
           p = -1;
           fin = false;
@@ -2293,7 +2296,7 @@ __global__ __launch_bounds__(256, PT_WF_SHADE_MIN_BLOCKS) void wf_shade_kernel(R
       if (T.shadow == 0 && T.res == kNeedExactClosest) {   // handed back by wf_trace_wide_kernel
         const Hit e = trace_closest<false, false, true, false>(P, T.o, T.d, c, cand);
         T.lim = e.t;
-        T.res = e.tri;
+        T.res = e.tri >= 0 ? P.wide_rank_of[e.tri] : e.tri;   // a slot; hit_tris is by rank
       } else if (T.shadow == 1 && T.res == kNeedExactShadow) {
         T.res = occluded<false, false>(P, T.o, T.d, T.lim, c) ? 1 : 0;
       }
