@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <system_error>
 #include <thread>
 #include <utility>
 
@@ -66,7 +67,12 @@ class Builder {
     size_t chunk = (n + nt - 1) / nt;
     for (int i = 0; i < nt; ++i) {
       size_t a = i * chunk, b = std::min(n, a + chunk);
-      if (a < b) th.emplace_back(f, a, b);
+      if (a >= b) continue;
+      try {
+        th.emplace_back(f, a, b);
+      } catch (const std::system_error&) {   // no thread to be had: this chunk here
+        f(a, b);
+      }
     }
     for (auto& t : th) t.join();
   }
@@ -126,8 +132,15 @@ class Builder {
     node.minBounds[3] = enc(left);
     node.maxBounds[3] = enc(right);
     nodes_[cur] = node;
+    std::thread th;
     if (cnt >= 200000 && try_take_thread()) {
-      std::thread th([=] { build(s, mid, left); });
+      try {
+        th = std::thread([=] { build(s, mid, left); });
+      } catch (const std::system_error&) {   // no thread to be had: build both halves here
+        spare_threads_.fetch_add(1);
+      }
+    }
+    if (th.joinable()) {
       build(mid, e, right);
       th.join();
       spare_threads_.fetch_add(1);

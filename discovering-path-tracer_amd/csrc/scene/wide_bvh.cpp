@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <system_error>
 #include <thread>
 
 namespace pt {
@@ -234,9 +235,14 @@ void sah_build(BinTree& T, std::vector<int32_t>& ids, std::vector<float>& lbox, 
   T.kid[2 * at] = (int32_t)left;
   T.kid[2 * at + 1] = (int32_t)right;
   if (par_depth > 0 && n > 65536) {
-    std::thread th([&] { sah_build(T, ids, lbox, cen, b, m, left, par_depth - 1); });
+    std::thread th;
+    try {
+      th = std::thread([&] { sah_build(T, ids, lbox, cen, b, m, left, par_depth - 1); });
+    } catch (const std::system_error&) {   // no thread to be had: build both halves here
+      sah_build(T, ids, lbox, cen, b, m, left, 0);
+    }
     sah_build(T, ids, lbox, cen, m, e, right, par_depth - 1);
-    th.join();
+    if (th.joinable()) th.join();
   } else {
     sah_build(T, ids, lbox, cen, b, m, left, 0);
     sah_build(T, ids, lbox, cen, m, e, right, 0);
