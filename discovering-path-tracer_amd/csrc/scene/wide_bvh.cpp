@@ -171,7 +171,7 @@ void sah_build(BinTree& T, std::vector<int32_t>& ids, std::vector<float>& lbox, 
   float bin_lo[3], bin_scale[3];
   for (int a = 0; a < 3; ++a) {
     const double ext = (double)cb[3 + a] - cb[a];
-    if (!(ext > 0.0)) continue;
+    if (!(ext > 1e-30)) continue;   // (a bin scale must stay a finite float)
     bin_lo[a] = cb[a];
     bin_scale[a] = (float)(kBins / ext * (1.0 - 1e-6));
     float bbox[kBins][6];
