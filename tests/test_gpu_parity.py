@@ -909,3 +909,29 @@ def test_wavefront_two_streams(case):
     r.render(0, 2)
     r.render(2, 3)
     _assert_same(r.read_accum(), ref, f"two streams {case}")
+
+
+@pytest.mark.parametrize("case", ["sphere", "cloud_int_bits"])
+def test_wide_walk_partitioned_ranks_sum_to_oracle(case):
+    """Tile shares of a device-memory scene on the culled wide walk (the
+    wavefront pipeline as each rank of a multi-GPU frame runs it: equal
+    shares over 3 ranks and unequal slotted shares over 2): the ranks'
+    +0/-0 partial frames sum to the oracle's full frame bit for bit."""
+    sv, si, cam, lights, int_bits = _wide_case(case)
+    v, i, n, _, _ = ptamd.Scene.from_arrays(sv, si).build_bvh(int_bits=int_bits).arrays()
+    W, H, nb = 96, 64, 3
+    ref, _ = _oracle(v, i, n, W, H, nb=nb, cam=cam, lights=lights, int_bits=int_bits)
+    for nranks, slots in ((3, None), (2, [3, 1])):
+        acc = np.full(W * H * 4, -0.0, np.float32)   # -0 is the IEEE additive identity
+        for rank in range(nranks):
+            r = _setup(v, i, n, cam=cam, lights=lights, int_bits=int_bits, lds=0)
+            r.set_option(ptamd.PT_OPT_KERNEL, 3)
+            if slots is None:
+                r.set_partition(nranks, rank)
+            else:
+                r.set_partition(nranks, rank, slots)
+            assert r.wide_info()[0] > 0
+            r.resize_and_clear(W, H)
+            r.render(0, nb)
+            acc = (acc + r.read_accum()).astype(np.float32)
+        _assert_same(acc, ref.reshape(-1), f"wide walk {case}, {nranks} ranks, slots {slots}")
