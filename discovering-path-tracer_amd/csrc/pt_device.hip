@@ -2102,9 +2102,14 @@ __global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_ker
 // group of four was idle.  G = 1 vs the earlier choice (2 below 500K
 // triangles, 4 above): sphere 78.0 -> 75.1 ms, 10M cloud 237 -> 206 ms;
 // a refill threshold of 16 or 8 lanes instead of 32: +3-15 % (each refill is
-// an atomic and a dependent ray load the whole wave waits for).
+// an atomic and a dependent ray load the whole wave waits for); 24: PT_WIDE_REFILL.
 #ifndef PT_WIDE_G
 #define PT_WIDE_G 1
+#endif
+// refill threshold of the wide walk: 24 idle lanes (sphere -0.9 %, 10M cloud
+// -0.35 % against 32, repeated; 16: +3 %)
+#ifndef PT_WIDE_REFILL
+#define PT_WIDE_REFILL 24
 #endif
 constexpr int kWideG = PT_WIDE_G;
 #ifndef PT_WIDE_FLUSH_T
@@ -2146,7 +2151,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
     for (int sh = 1; sh < G; sh <<= 1) gm &= gm >> sh;
     gm &= group_lead<G>();
     const int ng = (int)__popcll(gm);
-    if (more && ng * G >= PT_WF_REFILL) {
+    if (more && ng * G >= PT_WIDE_REFILL) {
       const int need = ng * G;
       int base = 0;
       if (lane == 0) base = atomicAdd(&B.counters[2], need);
