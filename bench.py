@@ -47,6 +47,7 @@ import time
 
 import numpy as np
 
+T_START = time.perf_counter()
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "discovering-path-tracer_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -70,17 +71,18 @@ def load_scene(name):
     import scenes
     if name == "box":
         s = ptamd.Scene.load_obj(scenes.BOX_OBJ).build_bvh()
-        return s, scenes.DEFAULT_CAMERA, False, "box.obj"
+        return s, scenes.DEFAULT_CAMERA, False, "box.obj, camera (0,0,5) fov 60"
     if name == "sphere":
         v, i = scenes.displaced_sphere(6)
         s = ptamd.Scene.from_arrays(v, i).build_bvh()
-        return s, scenes.camera((0.0, 0.5, 3.0)), False, f"displaced icosphere ({i.size // 3} tris, Sylveon substitute)"
+        return (s, scenes.camera((0.0, 0.5, 3.0)), False,
+                f"displaced icosphere ({i.size // 3} tris, Sylveon substitute), camera (0,0.5,3) fov 60")
     if name.startswith("synthetic:"):
         t = int(name.split(":")[1])
         v, i = scenes.random_triangles(t, seed=42)
         big = 2 * t - 1 >= (1 << 24)
         s = ptamd.Scene.from_arrays(v, i).build_bvh(int_bits=big)
-        return s, scenes.camera((0.0, 0.0, 2.2)), big, f"synthetic {t} random triangles, camera z=2.2"
+        return s, scenes.camera((0.0, 0.0, 2.2)), big, f"synthetic {t} random triangles, camera (0,0,2.2) fov 60"
     raise SystemExit(f"unknown scene {name}")
 
 
@@ -249,9 +251,27 @@ def roofline_block(prof, time_ms, alg_bytes, kernel, kernel_ms, interval_ms, n_t
 
 # the BASELINE configs the default run reports beside the headline, one GPU
 # each: (key, scene, W, H, spp, MAX_DEPTH, timed frames, profile workload)
-SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 3, "sphere_1080p8"),
-              ("config4", "sphere", 3840, 2160, 16, 8, 1, "sphere_4k16_d8"),
-              ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 1, "synthetic10M_1080p8"))
+SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 5, "sphere_1080p8"),
+              ("config4", "sphere", 3840, 2160, 16, 8, 3, "sphere_4k16_d8"),
+              ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5, "synthetic10M_1080p8"))
+
+
+def time_frames(r, spp, steps):
+    """`steps` timed frames, one at a time (each synchronized): wall ms per
+    frame and the kernel ms of each frame's launches (HIP events)."""
+    walls = []
+    r.reset_launch_times()
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        r.render(0, spp)
+        r.synchronize()
+        walls.append((time.perf_counter() - t0) * 1e3)
+    return np.array(walls), r.launch_times_ms()
+
+
+def spread(ms):
+    return {"min": round(float(np.min(ms)), 3), "median": round(float(np.median(ms)), 3),
+            "max": round(float(np.max(ms)), 3), "frames": int(ms.size)}
 
 
 def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaustive_too=False):
@@ -284,14 +304,9 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
     r.render(0, spp)
     r.synchronize()
     torch.cuda.synchronize()
-    r.reset_launch_times()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        r.render(0, spp)
-    r.synchronize()
-    dt = (time.perf_counter() - t0) / steps
-    kt = r.launch_times_ms()
-    kernel_ms = float(np.mean(kt)) if kt.size else float("nan")
+    walls, kt = time_frames(r, spp, steps)
+    dt = float(np.median(walls)) * 1e-3   # the median frame (min/max beside it)
+    kernel_ms = float(np.median(kt)) if kt.size else float("nan")
     alg = algorithmic_bytes({"nodes": ref[1], "leaf_tests": ref[2], "samples": ref[3]})
     prof = profiled_traffic(workload)
     cfg = {"workload": f"{desc} {W}x{H} {spp}spp {depth} bounces {sss} sss", "triangles": int(ntri),
@@ -299,10 +314,11 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
     add_traced(cfg, traced, dt)
     out = {"metric": "Mrays/s (reference-equivalent traceRay calls)", "value": round(ref[0] / dt / 1e6, 3),
            "unit": "Mrays/s", "ms_per_step": round(dt * 1e3, 2), "steps": steps, "warmup": 1,
+           "ms_per_frame": spread(walls), "kernel_ms_per_frame": spread(kt) if kt.size else None,
            "kernel": KERNEL_NAMES.get(r.last_kernel(), "?"), "config": cfg,
            "roofline": roofline_block(prof, kernel_ms, alg, KERNEL_NAMES.get(r.last_kernel(), "?"), kernel_ms,
-                                      kernel_ms, int(kt.size), "kernel_ms (HIP events around each frame's "
-                                                               "launches on the render stream)"),
+                                      kernel_ms, int(kt.size), "median kernel_ms (HIP events around each "
+                                                               "frame's launches on the render stream)"),
            "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
     if exhaustive_too:
         r.set_option(ptamd.PT_OPT_WIDE, 0)
@@ -321,6 +337,22 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
             "roofline": roofline_block(profiled_traffic(workload + "_exhaustive"), k0, alg, name0, k0, k0,
                                        int(kt0.size), "kernel_ms (HIP events around the frame's launches)")}
         r.set_option(ptamd.PT_OPT_WIDE, 1)
+    # the same scene at the reference's default camera (Camera.cpp:7-9,
+    # Camera.h:34-36: pos (0,0,5) looking at the origin, fov 60)
+    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 0)
+    r.set_camera(scenes.DEFAULT_CAMERA)
+    ref2, traced2 = reference_and_traced_counts(r, spp)
+    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+    r.render(0, spp)
+    r.synchronize()
+    walls2, kt2 = time_frames(r, spp, steps)
+    dt2 = float(np.median(walls2)) * 1e-3
+    cfg2 = {"workload": cfg["workload"].replace(desc, desc.split(", camera")[0] + ", camera (0,0,5) fov 60"),
+            "rays_per_frame": int(ref2[0])}
+    add_traced(cfg2, traced2, dt2)
+    out["reference_camera"] = {"value": round(ref2[0] / dt2 / 1e6, 3), "unit": "Mrays/s",
+                               "ms_per_step": round(dt2 * 1e3, 2), "ms_per_frame": spread(walls2),
+                               "kernel_ms_per_frame": spread(kt2) if kt2.size else None, "config": cfg2}
     del r
     return out
 
@@ -870,13 +902,20 @@ def main():
             add_traced(out_line["config"], traced, dt / args.steps)
         if prof is not None and prof[1].get("sq_per_launch", {}).get("SQ_INSTS_VALU"):
             # the box frame is bound by vector-instruction issue, not HBM (its
-            # scene lives in LDS): VALU wave-instructions per launch from the
-            # committed PMC profile over the measured kernel time
+            # scene lives in LDS): the primary roofline is VALU
+            # wave-instructions per launch from the committed PMC profile over
+            # the measured kernel time; the HBM roofline stays beside it
             valu = prof[1]["sq_per_launch"]["SQ_INSTS_VALU"]
             gi = valu / (roof_ms * 1e-3) / 1e9
-            out_line["roofline_valu"] = {"bound": "valu_issue", "achieved": round(gi, 2), "peak": VALU_PEAK_GINST,
-                                         "unit": "G wave-instr/s", "frac": round(gi / VALU_PEAK_GINST, 4),
-                                         "valu_wave_instr_per_launch": int(valu), "source": prof[0]}
+            hbm = out_line["roofline"]
+            out_line["roofline"] = {"bound": "valu_issue", "achieved": round(gi, 2), "peak": VALU_PEAK_GINST,
+                                    "unit": "G wave-instr/s", "frac": round(gi / VALU_PEAK_GINST, 4),
+                                    "traffic": hbm["traffic"], "valu_wave_instr_per_launch": int(valu),
+                                    "source": prof[0], "kernel": hbm["kernel"], "kernel_ms": hbm["kernel_ms"],
+                                    "time_basis": hbm["time_basis"],
+                                    "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 f32 instruction",
+                                    "hbm": {k: hbm[k] for k in ("achieved", "peak", "unit", "frac", "traffic",
+                                                                "traffic_source", "effective_GBps")}}
         if emu > 1:
             out_line["metric"] = f"EMULATED (1 GPU, not a multi-GPU result): rank {emu_rank} of {emu}, " + out_line["metric"]
             out_line["emulated_ranks"] = emu
@@ -896,6 +935,7 @@ def main():
                 print(f"bench: {key} leg ({scene_name} {lw}x{lh} {lspp}spp D{ldepth})", file=sys.stderr, flush=True)
                 out_line["configs"][key] = scene_leg(scene_name, lw, lh, lspp, ldepth, SSS, steps, device, workload,
                                                      exhaustive_too=key == "config5")
+        out_line["bench_wall_s"] = round(time.perf_counter() - T_START, 1)
         print(json.dumps(out_line), flush=True)
     if dist is not None:
         dist.barrier()

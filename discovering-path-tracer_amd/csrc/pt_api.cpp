@@ -371,6 +371,7 @@ struct pt_context {
   int* d_wide_rank_of = nullptr;
   int2* d_wide_ovf = nullptr;
   long long wide_ovf_lanes = 0;
+  int wide_ovf_stack = 0;   // the stack bound d_wide_ovf was sized for
   int n_wide = 0, wide_stack = 0;
   std::string wide_reason = "no scene";
   int opt_wide = 1;           // PT_OPT_WIDE
@@ -988,13 +989,14 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     } else if (c->opt_wide && c->n_wide > 0 && !lds) {
       const long long lanes = ptd::wide_trace_lanes();
       if (lanes <= 0) return fail(PT_ERR_HIP, "wide walk: occupancy query failed");
-      if (lanes > c->wide_ovf_lanes) {   // every lane of the persistent grid gets its overflow area
+      if (lanes > c->wide_ovf_lanes || c->wide_stack > c->wide_ovf_stack) {   // every lane of the grid gets its area
         { const int rc_ = quiesce(c); if (rc_) return rc_; }
         dev_free(c->d_wide_ovf);
         c->wide_ovf_lanes = 0;
         // two sets: the two halves of a chunk trace concurrently (launch_wavefront)
         PT_HIP(hipMalloc((void**)&c->d_wide_ovf, 2 * (size_t)lanes * (size_t)c->wide_stack * sizeof(int2)));
         c->wide_ovf_lanes = lanes;
+        c->wide_ovf_stack = c->wide_stack;
       }
       p.wide = c->d_wide;
       p.wide_tris = c->d_wide_tris;
@@ -1172,6 +1174,12 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   dev_free(c->d_wide);
   dev_free(c->d_wide_tris);
   dev_free(c->d_wide_rank_of);
+  dev_free(c->d_tris);
+  // the wide walk's overflow area is sized by the scene's stack bound: a
+  // deeper tree needs a new one (it is reallocated at the next wide launch)
+  dev_free(c->d_wide_ovf);
+  c->wide_ovf_lanes = 0;
+  c->wide_ovf_stack = 0;
   c->n_wide = 0;
   c->has_scene = false;
   const int T = (int)(n_indices / 3);

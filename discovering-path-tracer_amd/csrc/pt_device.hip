@@ -82,6 +82,8 @@ struct Hit {
 #ifndef PT_WF_SHADOW_QUEUE
 #define PT_WF_SHADOW_QUEUE 1   // wf_trace_kernel: shadow rays queue their leaves too (see there)
 #endif
+// queued shadow leaves are only ever flushed by the wave-wide flush
+static_assert(PT_WF_WAVEFLUSH || !PT_WF_SHADOW_QUEUE, "PT_WF_SHADOW_QUEUE needs PT_WF_WAVEFLUSH");
 constexpr int kCand = PT_KCAND;
 
 // PF (prefetch): load node k+1 while node k is being tested — it is the next

@@ -285,6 +285,13 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
     }
   }
   if (out->rank_tri.size() != n_tris) return "tree leaves do not cover the triangles once";
+  {   // every triangle slot exactly once: the rank <-> slot maps must be bijective
+    std::vector<uint8_t> seen(n_tris, 0);
+    for (const int32_t t : out->rank_tri) {
+      if (t < 0 || (size_t)t >= n_tris || seen[(size_t)t]) return "tree leaves do not cover the triangles once";
+      seen[(size_t)t] = 1;
+    }
+  }
   // the walk's premises on the uploaded arrays: finite, bounded coordinates;
   // parent boxes contain their children's (so the reference tests a triangle
   // iff its leaf box passes); leaf boxes contain their triangle

@@ -17,6 +17,14 @@ k-th row (row_stride / row_phase of oracle_render) instead of the whole frame.
   reference's float-encoded child indices hold (BoundingVolumeHierarchy.cpp:74,77),
   so the tree travels with PT_NODES_INT_BITS and the oracle reads the same
   int32 links.
+
+Every config is also rendered twice over the whole frame -- with the default
+culled wide walk and with the reference-shaped exhaustive walk
+(PT_OPT_WIDE 0, raytrace_comp.comp:159-204 node for node) -- and the two
+frames must agree bitwise in every pixel; the exhaustive walk itself is the
+one the oracle row subsets pin.  And every config runs once more at the
+reference's default camera (Camera.cpp:7-9, Camera.h:34-36: pos (0,0,5),
+fov 60), row subsets against the oracle.
 """
 import os
 
@@ -61,6 +69,26 @@ def _check_rows(gpu, v, i, n, cam, W, H, spp, depth, stride, phase, int_bits=Fal
     return rows, st
 
 
+def _exhaustive_frame_equals(r, gpu, W, H, spp):
+    """Re-render the same frame on `r` with the exhaustive walk and require
+    every float of it to equal `gpu` (rendered with the culled wide walk)."""
+    info = r.wide_info()
+    assert info[0] > 0, f"the wide walk must be the default here: {info}"
+    r.set_option(ptamd.PT_OPT_WIDE, 0)
+    try:
+        r.clear()
+        r.render(0, spp)
+        ex = r.read_accum().reshape(H, W, 4)
+    finally:
+        r.set_option(ptamd.PT_OPT_WIDE, 1)
+    assert r.last_kernel() == 3
+    if not np.array_equal(ex.view(np.uint32), gpu.view(np.uint32)):
+        bad = np.argwhere(ex.view(np.uint32) != gpu.view(np.uint32))
+        y, x, ch = bad[0]
+        raise AssertionError(f"wide vs exhaustive walk: {bad.shape[0]} of {gpu.size} floats differ; first at pixel "
+                             f"({x}, {y}) ch {ch}: wide {gpu[y, x, ch]!r} exhaustive {ex[y, x, ch]!r}")
+
+
 @pytest.fixture(scope="module")
 def sphere6():
     sv, si = scenes.displaced_sphere(6)
@@ -78,6 +106,17 @@ def test_config3_sphere_1080p_8spp(sphere6):
     rows, _ = _check_rows(gpu, v, i, n, cam, 1920, 1080, 8, 4, stride=64, phase=29)
     # the frame has geometry in the checked rows (not only background)
     assert np.count_nonzero(gpu[rows, :, :3]) > 1000
+    _exhaustive_frame_equals(r, gpu, 1920, 1080, 8)
+
+
+def test_config3_reference_camera(sphere6):
+    v, i, n = sphere6
+    cam = scenes.DEFAULT_CAMERA
+    r, gpu = _render(v, i, n, cam, 1920, 1080, 8, 4)
+    assert r.last_kernel() == 3
+    rows, _ = _check_rows(gpu, v, i, n, cam, 1920, 1080, 8, 4, stride=24, phase=7)
+    assert np.count_nonzero(gpu[rows, :, :3]) > 1000
+    _exhaustive_frame_equals(r, gpu, 1920, 1080, 8)
 
 
 def test_config4_sphere_4k_16spp_depth8(sphere6):
@@ -87,6 +126,17 @@ def test_config4_sphere_4k_16spp_depth8(sphere6):
     assert r.last_kernel() == 3
     assert np.all(gpu[..., 3] == 1.0)
     _check_rows(gpu, v, i, n, cam, 3840, 2160, 16, 8, stride=256, phase=77)
+    _exhaustive_frame_equals(r, gpu, 3840, 2160, 16)
+
+
+def test_config4_reference_camera(sphere6):
+    v, i, n = sphere6
+    cam = scenes.DEFAULT_CAMERA
+    r, gpu = _render(v, i, n, cam, 3840, 2160, 16, 8)
+    assert r.last_kernel() == 3
+    rows, _ = _check_rows(gpu, v, i, n, cam, 3840, 2160, 16, 8, stride=96, phase=41)
+    assert np.count_nonzero(gpu[rows, :, :3]) > 1000
+    _exhaustive_frame_equals(r, gpu, 3840, 2160, 16)
 
 
 def test_config4_depth8_differs_from_depth4(sphere6):
@@ -101,23 +151,39 @@ def test_config4_depth8_differs_from_depth4(sphere6):
     assert np.array_equal(g8.reshape(-1).view(np.uint32), ref.view(np.uint32))
 
 
-def test_config5_10m_cloud_int_bits():
+@pytest.fixture(scope="module")
+def cloud10m():
     tv, ti = scenes.random_triangles(10_000_000, seed=42)
     s = ptamd.Scene.from_arrays(tv, ti).build_bvh(int_bits=True)
     v, i, n, _, _ = s.arrays()
     del tv, ti, s
     assert n.shape[0] == 19_999_999 and n.shape[0] >= (1 << 24)
+    return v, i, n
+
+
+def test_config5_10m_cloud_int_bits(cloud10m):
+    v, i, n = cloud10m
     cam = scenes.camera((0.0, 0.0, 2.2))
     r, gpu = _render(v, i, n, cam, 1920, 1080, 8, 4, int_bits=True)
     assert r.last_kernel() == 3
+    rows, st = _check_rows(gpu, v, i, n, cam, 1920, 1080, 8, 4, stride=270, phase=101, int_bits=True)
+    assert np.count_nonzero(gpu[rows, :, :3]) > 1000
+    # exhaustive traversal of the 10M tree: thousands of nodes per traceRay
+    assert st[1] / st[0] > 500
+    _exhaustive_frame_equals(r, gpu, 1920, 1080, 8)
     # the float-encoded layout of this tree is refused (indices >= 2^24 are inexact)
     nf = n.copy()
     links = nf[:, [3, 7]].view(np.int32).astype(np.float32)
     nf[:, 3], nf[:, 7] = links[:, 0], links[:, 1]
     with pytest.raises(ptamd.PTError):
         r.upload_scene(v, i, nf)
-    del nf, links
-    rows, st = _check_rows(gpu, v, i, n, cam, 1920, 1080, 8, 4, stride=270, phase=101, int_bits=True)
+
+
+def test_config5_reference_camera(cloud10m):
+    v, i, n = cloud10m
+    cam = scenes.DEFAULT_CAMERA
+    r, gpu = _render(v, i, n, cam, 1920, 1080, 8, 4, int_bits=True)
+    assert r.last_kernel() == 3
+    rows, _ = _check_rows(gpu, v, i, n, cam, 1920, 1080, 8, 4, stride=90, phase=47, int_bits=True)
     assert np.count_nonzero(gpu[rows, :, :3]) > 1000
-    # exhaustive traversal of the 10M tree: thousands of nodes per traceRay
-    assert st[1] / st[0] > 500
+    _exhaustive_frame_equals(r, gpu, 1920, 1080, 8)

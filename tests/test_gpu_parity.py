@@ -935,3 +935,30 @@ def test_wide_walk_partitioned_ranks_sum_to_oracle(case):
             r.render(0, nb)
             acc = (acc + r.read_accum()).astype(np.float32)
         _assert_same(acc, ref.reshape(-1), f"wide walk {case}, {nranks} ranks, slots {slots}")
+
+
+def test_wide_walk_reupload_deeper_scene():
+    """A context that rendered a shallow wide tree, then gets a scene whose
+    wide tree needs a deeper stack (the per-lane overflow area is sized by the
+    scene's stack bound, ADVICE r2), renders the deeper scene's oracle frame;
+    and a third upload back to the shallow scene as well."""
+    shallow = scenes.random_triangles(64, seed=4, spread=0.4, size=0.05)
+    deep = scenes.random_triangles(200000, seed=5, spread=0.6, size=0.003)
+    cam = scenes.camera((0.0, 0.1, 1.6))
+    r = None
+    depths = []
+    for sv, si in (shallow, deep, shallow):
+        v, i, n, _, _ = ptamd.Scene.from_arrays(sv, si).build_bvh().arrays()
+        if r is None:
+            r = _setup(v, i, n, cam=cam, lds=0)
+            r.set_option(ptamd.PT_OPT_KERNEL, 3)
+        else:
+            r.upload_scene(v, i, n)
+        info = r.wide_info()
+        assert info[0] > 0, info
+        depths.append(info[1])
+        r.resize_and_clear(72, 56)
+        r.render(0, 2)
+        ref, _ = _oracle(v, i, n, 72, 56, nb=2, cam=cam)
+        _assert_same(r.read_accum(), ref, f"re-upload, stack bound {info[1]}")
+    assert depths[1] > depths[0], depths
