@@ -375,6 +375,7 @@ struct pt_context {
   int n_wide = 0, wide_stack = 0;
   std::string wide_reason = "no scene";
   int opt_wide = 1;           // PT_OPT_WIDE
+  int opt_wf_fuse = 1;        // PT_OPT_WF_FUSE
   int n_nodes_full = 0;
   float4* d_tris = nullptr;
   int n_tris = 0;
@@ -811,6 +812,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.wide_ovf_lanes = 0;
   p.wide_stack = 0;
   p.wide_handback = 0;
+  p.wf_fuse = 0;
   p.nodes = c->stats_mode ? c->d_nodes_full : c->d_nodes;
   p.tris = c->d_tris;
   p.hit_tris = c->d_tris;
@@ -1006,6 +1008,8 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
       p.wide_ovf_lanes = c->wide_ovf_lanes;
       p.wide_stack = c->wide_stack;
       p.wide_handback = c->opt_wide == 2 ? 1 : 0;
+      // fused shadow walks: hit records carry the rank in 29 bits
+      p.wf_fuse = c->opt_wf_fuse && c->n_tris <= ptd::kHitRankMask && c->n_lights > 0 ? 1 : 0;
     }
     if (c->opt_wf_streams == 2 && !c->wf_stream2) {
       PT_HIP(hipStreamCreateWithFlags(&c->wf_stream2, hipStreamNonBlocking));
@@ -1497,6 +1501,10 @@ int pt_set_option(pt_context* c, int key, int value) {
     case PT_OPT_WIDE:
       if (value < 0 || value > 2) return fail(PT_ERR_INVALID, "PT_OPT_WIDE takes 0, 1 or 2");
       c->opt_wide = value;
+      return PT_OK;
+    case PT_OPT_WF_FUSE:
+      if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_WF_FUSE takes 0 or 1");
+      c->opt_wf_fuse = value;
       return PT_OK;
     case PT_OPT_WF_STREAMS:
       if (value != 1 && value != 2) return fail(PT_ERR_INVALID, "PT_OPT_WF_STREAMS takes 1 or 2");

@@ -95,6 +95,7 @@ struct RenderParams {
   long long wide_ovf_lanes;
   int wide_stack;
   int wide_handback;        // test: hand every odd list slot to the exact walk (PT_OPT_WIDE 2)
+  int wf_fuse;              // PT_OPT_WF_FUSE: the wide trace kernel also walks a closest hit's first-light shadow ray
   const float4* nodes;
   const float4* tris;
   const LightDev* lights;
@@ -187,6 +188,15 @@ struct WfBuffers {
   long long cap;     // paths the buffers hold
 };
 constexpr int kWfStateF4 = 10;
+// kind word of a listed ray (rays[cap + s].w): 0 closest, 1 shadow, 2 null
+// shadow query, plus (PT_OPT_WF_FUSE, closest rays) kRayFuse: the trace
+// kernel walks the path's first-light shadow ray after a hit (the ray's
+// limit word then holds the path's RNG state); kRayPrimary: a primary ray,
+// whose light pre-pass (raytrace_comp.comp:311-328) may end the path first
+constexpr int kRayKindMask = 3, kRayFuse = 4, kRayPrimary = 8;
+// hits[s].y of a fused closest hit: rank | kHitFused | (kHitOccluded if the
+// shadow ray was occluded)
+constexpr int kHitFused = 0x40000000, kHitOccluded = 0x20000000, kHitRankMask = 0x1fffffff;
 constexpr size_t kWfBytesPerPath = 2 * (size_t)kWfStateF4 * 16 + 16 + 2 * (4 + 32) + 8;
 // rays a path may trace in one sample: the primary ray, then per bounce the
 // light shadow rays, sss_bounces x (walk ray + light shadow rays) and the

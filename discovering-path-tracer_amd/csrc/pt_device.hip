@@ -1614,9 +1614,12 @@ __device__ __forceinline__ void wf_store_state(const WfBuffers& B, int list, lon
   for (int j = 0; j < kWfStateF4; ++j) dst[(size_t)j * (size_t)B.cap] = v[j];
 }
 
-__device__ __forceinline__ void wf_store_ray(float4* __restrict__ rays, long long cap, int slot, const Trav& T) {
-  rays[slot] = make_float4(T.o.x, T.o.y, T.o.z, T.lim);
-  rays[(size_t)cap + (size_t)slot] = make_float4(T.d.x, T.d.y, T.d.z, __int_as_float(T.shadow));
+// bits: kRayFuse / kRayPrimary (fuse_bits); the limit word of a fused
+// closest ray (whose limit is always 1e30) carries the path's RNG state
+__device__ __forceinline__ void wf_store_ray(float4* __restrict__ rays, long long cap, int slot, const Trav& T,
+                                             int bits = 0, uint32_t rng = 0u) {
+  rays[slot] = make_float4(T.o.x, T.o.y, T.o.z, bits ? __uint_as_float(rng) : T.lim);
+  rays[(size_t)cap + (size_t)slot] = make_float4(T.d.x, T.d.y, T.d.z, __int_as_float(T.shadow | bits));
 }
 
 __device__ __forceinline__ void wf_load_ray(const float4* __restrict__ rays, long long cap, int slot, float4* r0,
@@ -1638,9 +1641,21 @@ __device__ __forceinline__ int wave_slot(int* counter, bool pred) {
   return pred ? base + (int)__popcll(m & ((1ull << lane) - 1ull)) : -1;
 }
 
-__device__ __forceinline__ void wf_push(const WfBuffers& B, int list, int slot, int p, const Trav& T) {
+// PT_OPT_WF_FUSE: which closest rays the trace kernel follows with the
+// path's next shadow ray.  After the hit of a primary (unless the light
+// pre-pass ends the path), bounce or SSS ray, pathTrace's next draws sample
+// light 0 (PH_DIRECT :345-366, PH_SSS_SHADOW :383-402) from the state the
+// path holds now, and the shadow ray depends only on the hit and those draws.
+__device__ __forceinline__ int fuse_bits(const RenderParams& P, const PathSt& S, const Trav& T) {
+  if (!P.wf_fuse || T.shadow != 0) return 0;
+  if (S.phase == PH_PRIMARY) return P.max_depth > 0 ? kRayFuse | kRayPrimary : 0;
+  return (S.phase == PH_BOUNCE || S.phase == PH_SSS) ? kRayFuse : 0;
+}
+
+__device__ __forceinline__ void wf_push(const WfBuffers& B, int list, int slot, int p, const Trav& T, int bits = 0,
+                                        uint32_t rng = 0u) {
   B.ids[list][slot] = p;
-  wf_store_ray(B.rays[list], B.cap, slot, T);
+  wf_store_ray(B.rays[list], B.cap, slot, T, bits, rng);
 }
 
 // Path g of a launch: pixel (item, q) = g / n_batches, sample g % n_batches
@@ -1702,7 +1717,7 @@ __global__ __launch_bounds__(256) void wf_gen_kernel(RenderParams P, WfBuffers B
   }
   const int slot = wave_slot(&B.counters[0], need);
   if (need) {
-    wf_push(B, 0, slot, (int)g, T);
+    wf_push(B, 0, slot, (int)g, T, fuse_bits(P, S, T), S.rng);
     wf_store_state(B, 0, slot, S);
   }
   if (CNT) {
@@ -1724,7 +1739,7 @@ struct WfLane {
 // CNT: a ray handed to the traversal kernel -- closest (kind 0) or shadow
 // (kind 1) walk; a null shadow query (kind 2, trav_null) is no walk.
 __device__ __forceinline__ void count_start(float4 r1, Ctr& c) {
-  const int kind = __float_as_int(r1.w);
+  const int kind = __float_as_int(r1.w) & kRayKindMask;
   c.rays += kind == 0 ? 1u : 0u;
   c.srays += kind == 1 ? 1u : 0u;
 }
@@ -2123,6 +2138,37 @@ constexpr int kWideG = PT_WIDE_G;
 // 64 VGPRs, 60 B spilled): sphere +6.5 %, 10M cloud +5.4 %; with 7: +1 %.
 #define PT_WIDE_MIN_BLOCKS 6
 #endif
+// PT_OPT_WF_FUSE: the shadow ray pathTrace traces right after closest hit
+// (t, rank) of ray (o, d), from the path's RNG state `rng` -- light 0's
+// sample, direction, diffuse term and distance with the ops of path_step's
+// PH_DIRECT / PH_SSS_SHADOW (:345-366, :383-402; the hit point o + d t is
+// S.hp / S.cp, the normal the record's).  0: none (a primary ray's light
+// pre-pass, :311-328, ends the path); 1: answered without a walk (its answer
+// cannot change the image, shadow_needed); 2: walk (so, sd) up to lim.
+__device__ __forceinline__ int fused_shadow_ray(const RenderParams& P, v3 o, v3 d, float t, int rank, bool primary,
+                                                uint32_t rng, v3* so, v3* sd, float* lim) {
+  if (primary) {
+    for (int i = 0; i < P.n_lights; ++i) {
+      float tl;
+      if (intersect_area_light(o, d, load_light(P, i), &tl) && t > tl) return 0;   // lit: T.res >= 0 here
+    }
+  }
+  const float OFFSET = 0.001f;
+  const v3 hp = add(o, muls(d, t));
+  const v3 hn = tri_normal(P, rank);
+  const LightDev L = load_light(P, 0);
+  const v3 lp = sample_area_light(L, &rng);
+  const v3 ld = normalize(sub(lp, hp));
+  const float diff = fmax_(dot(hn, ld), 0.0f);
+  const float dist = length(sub(lp, hp));
+  if (!shadow_needed(L, diff)) return 1;
+  *so = add(hp, muls(hn, OFFSET));
+  *sd = ld;
+  *lim = dist - OFFSET;
+  return 2;
+}
+constexpr int kFuseWalk = 16;   // lane state: walking the fused shadow ray
+
 template <int G, bool CNT = false>
 __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(RenderParams P, WfBuffers B,
                                                                                 int cur) {
@@ -2145,6 +2191,11 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
   R.cur = -1;
   R.sp = R.lo = 0;
   R.nc = 0;
+  // PT_OPT_WF_FUSE: fz = the ray's kRayFuse / kRayPrimary bits, or kFuseWalk
+  // while the lane walks the fused shadow ray; aux = the path's RNG state,
+  // then the closest hit's t; cr = its rank
+  int fz = 0, cr = 0;
+  uint32_t aux = 0u;
   Ctr c = {0u, 0u, 0u, 0u, 0u};
   for (;;) {
     const unsigned long long idle = __ballot(p < 0);
@@ -2165,9 +2216,12 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
         if (slot < count) {
           float4 r0, r1;
           wf_load_ray(rays, B.cap, slot, &r0, &r1);
-          const int kind = __float_as_int(r1.w);   // 0 closest, 1 shadow, 2 null shadow (trav_null)
+          const int kbits = __float_as_int(r1.w);
+          const int kind = kbits & kRayKindMask;   // 0 closest, 1 shadow, 2 null shadow (trav_null)
           if (CNT) count_start(r1, c);
           wide_start(R, mk(r0.x, r0.y, r0.z), mk(r1.x, r1.y, r1.z), kind != 0, r0.w);
+          fz = kbits & (kRayFuse | kRayPrimary);
+          aux = __float_as_uint(r0.w);
           if (kind == 2) {
             B.hits[slot] = make_float2(R.lim, __int_as_float(0));
           } else if (!wide_ray_ok(R.o, R.d, R.inv) || (P.wide_handback && (slot & 1))) {
@@ -2198,9 +2252,13 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
                                      &c.leaves, cand);
         if (exact) {
           R.nc = 0;
-          B.hits[p] = make_float2(R.lim, __int_as_float(R.shadow ? kNeedExactShadow : kNeedExactClosest));
+          // a fused shadow ray the walk cannot take goes to the shading's next round
+          B.hits[p] = (fz & kFuseWalk) ? make_float2(__uint_as_float(aux), __int_as_float(cr))
+                                       : make_float2(R.lim, __int_as_float(R.shadow ? kNeedExactShadow
+                                                                                    : kNeedExactClosest));
           p = -1;
           fin = false;
+          fz = 0;
         }
         // wave-uniform flush: a queue that cannot take another node's four
         // leaves, or PT_WIDE_FLUSH_T finished walks waiting on their queue,
@@ -2227,10 +2285,39 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
           }
         }
         if (p >= 0 && fin && R.nc == 0) {
-          const int res = R.best;   // occluded, or the hit's rank (hit_tris = wide_tris; the record the flush just tested)
-          B.hits[p] = make_float2(R.lim, __int_as_float(res));
-          p = -1;
-          fin = false;
+          float t = R.lim;
+          int res = R.best;   // occluded, or the hit's rank (hit_tris = wide_tris; the record the flush just tested)
+          bool done = true;
+          if (fz & kFuseWalk) {   // the fused shadow ray's answer joins its closest hit
+            t = __uint_as_float(aux);
+            res = cr | kHitFused | (R.best ? kHitOccluded : 0);
+          } else if ((fz & kRayFuse) && R.best >= 0) {
+            v3 so, sd;
+            float lim;
+            const int k = fused_shadow_ray(P, R.o, R.d, R.lim, R.best, (fz & kRayPrimary) != 0, aux, &so, &sd, &lim);
+            if (k == 1) {
+              res = R.best | kHitFused;   // unoccluded without a walk
+            } else if (k == 2) {
+              cr = R.best;
+              aux = __float_as_uint(R.lim);
+              wide_start(R, so, sd, true, lim);
+              if (wide_ray_ok(R.o, R.d, R.inv)) {   // walk it in this lane now
+                fz = kFuseWalk;
+                fin = false;
+                done = false;
+                if (CNT) ++c.srays;
+              } else {   // the shading's next round hands it to the exact walk
+                t = __uint_as_float(aux);
+                res = cr;
+              }
+            }
+          }
+          if (done) {
+            B.hits[p] = make_float2(t, __int_as_float(res));
+            p = -1;
+            fin = false;
+            fz = 0;
+          }
         }
       }
     }
@@ -2294,9 +2381,14 @@ __global__ __launch_bounds__(256, PT_WF_SHADE_MIN_BLOCKS) void wf_shade_kernel(R
       const float2 h = B.hits[i];
       T.o = mk(r0.x, r0.y, r0.z);
       T.d = mk(r1.x, r1.y, r1.z);
-      T.shadow = __float_as_int(r1.w);
+      T.shadow = __float_as_int(r1.w) & kRayKindMask;
       T.lim = h.x;
       T.res = __float_as_int(h.y);
+      int fused = 0;   // PT_OPT_WF_FUSE: 1 the path's next shadow ray was walked unoccluded, 2 occluded
+      if (T.shadow == 0 && T.res >= 0 && (T.res & kHitFused)) {
+        fused = (T.res & kHitOccluded) ? 2 : 1;
+        T.res &= kHitRankMask;
+      }
       T.nc = 0;
       T.cn = T.cl = 0u;
       Ctr c = {0u, 0u, 0u, 0u, 0u};
@@ -2309,6 +2401,17 @@ __global__ __launch_bounds__(256, PT_WF_SHADE_MIN_BLOCKS) void wf_shade_kernel(R
       }
       v3 col;
       need = path_step<false>(P, F, S, T, c, &col);
+      if (fused) {
+        // the shading just derived the shadow ray the trace kernel walked
+        // (same hit, same draws, same ops): take its answer
+        if (need && T.shadow != 0) {
+          T.res = T.shadow == 2 ? 0 : fused - 1;
+          need = path_step<false>(P, F, S, T, c, &col);
+        } else {   // cannot happen; fail loudly rather than shade wrongly
+          need = false;
+          col = mk(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""));
+        }
+      }
 #if PT_WF_NULL_INLINE
       while (P.wide && need && T.shadow == 2) {   // a null shadow query (trav_null): unoccluded, answered here
         T.res = 0;
@@ -2339,14 +2442,14 @@ __global__ __launch_bounds__(256, PT_WF_SHADE_MIN_BLOCKS) void wf_shade_kernel(R
       __syncthreads();
       if (need) {
         const int slot = wg_base + bin_base[bin] + rank;
-        wf_push(B, cur ^ 1, slot, p, T);
+        wf_push(B, cur ^ 1, slot, p, T, fuse_bits(P, S, T), S.rng);
         wf_store_state(B, cur ^ 1, slot, S);
       }
       __syncthreads();   // the bins are reused by the next iteration
     } else {
       const int slot = wave_slot(&B.counters[cur ^ 1], need);
       if (need) {
-        wf_push(B, cur ^ 1, slot, p, T);
+        wf_push(B, cur ^ 1, slot, p, T, fuse_bits(P, S, T), S.rng);
         wf_store_state(B, cur ^ 1, slot, S);
       }
     }

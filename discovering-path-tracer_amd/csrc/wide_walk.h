@@ -112,7 +112,15 @@ PT_FN bool wide_ray_ok(v3 o, v3 d, v3 inv) {
 // One child box: the reference slab test (same ops as slab()), its t_near,
 // and the cull threshold th (culled iff lim < th).  kf: the node's
 // {c1, E0, E1, 0}.
-PT_FN void wide_child(const WideRay& R, float lx, float hx, float ly, float hy, float lz, float hz, float4 kf,
+// PT_WIDE_AINV_REG 0: fl(|1/d_i| + 1) is recomputed per node (3 ops shared by
+// the 4 children) instead of held in 3 registers across the walk
+#ifndef PT_WIDE_AINV_REG
+#define PT_WIDE_AINV_REG 0
+#endif
+PT_FN v3 wide_ainv(const WideRay& R) {
+  return PT_WIDE_AINV_REG ? R.ainv : mk(fabs_(R.inv.x) + 1.0f, fabs_(R.inv.y) + 1.0f, fabs_(R.inv.z) + 1.0f);
+}
+PT_FN void wide_child(const WideRay& R, v3 ainv, float lx, float hx, float ly, float hy, float lz, float hz, float4 kf,
                       bool* hit, float* tn, float* th) {
   const float dlx = lx - R.o.x, dly = ly - R.o.y, dlz = lz - R.o.z;
   const float dhx = hx - R.o.x, dhy = hy - R.o.y, dhz = hz - R.o.z;
@@ -125,9 +133,9 @@ PT_FN void wide_child(const WideRay& R, float lx, float hx, float ly, float hy, 
   const float smax = fmax_(fmax_(fmax_(fabs_(dlx), fabs_(dhx)), fmax_(fabs_(dly), fabs_(dhy))),
                            fmax_(fabs_(dlz), fabs_(dhz)));
   const float eps = fma_(kf.z, smax, kf.y);
-  const float e0 = fma_(-eps, R.ainv.x, fmin_(t0x, t1x) * (1.0f - 0x1p-20f));
-  const float e1 = fma_(-eps, R.ainv.y, fmin_(t0y, t1y) * (1.0f - 0x1p-20f));
-  const float e2 = fma_(-eps, R.ainv.z, fmin_(t0z, t1z) * (1.0f - 0x1p-20f));
+  const float e0 = fma_(-eps, ainv.x, fmin_(t0x, t1x) * (1.0f - 0x1p-20f));
+  const float e1 = fma_(-eps, ainv.y, fmin_(t0y, t1y) * (1.0f - 0x1p-20f));
+  const float e2 = fma_(-eps, ainv.z, fmin_(t0z, t1z) * (1.0f - 0x1p-20f));
   *th = kf.x * fmax_(fmax_(e0, e1), e2);
 }
 
@@ -247,14 +255,15 @@ PT_FN bool wide_step(WideRay& R, const float4* __restrict__ nodes, const float4*
   const float4* nd = nodes + (size_t)R.cur * kWideNodeF4;
   const float4 lx = nd[0], hx = nd[1], ly = nd[2], hy = nd[3], lz = nd[4], hz = nd[5], cf = nd[6], kf = nd[7];
   if (CNT) ++*cn;
+  const v3 ainv = wide_ainv(R);
   const int c0 = (int)f2u(cf.x), c1 = (int)f2u(cf.y), c2 = (int)f2u(cf.z),
             c3 = (int)f2u(cf.w);
   bool h0, h1, h2, h3;
   float n0, n1, n2, n3, th0, th1, th2, th3;
-  wide_child(R, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, kf, &h0, &n0, &th0);
-  wide_child(R, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, kf, &h1, &n1, &th1);
-  wide_child(R, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, kf, &h2, &n2, &th2);
-  wide_child(R, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, kf, &h3, &n3, &th3);
+  wide_child(R, ainv, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, kf, &h0, &n0, &th0);
+  wide_child(R, ainv, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, kf, &h1, &n1, &th1);
+  wide_child(R, ainv, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, kf, &h2, &n2, &th2);
+  wide_child(R, ainv, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, kf, &h3, &n3, &th3);
   h0 = h0 && c0 != kWideEmpty && !(R.lim < th0);
   h1 = h1 && c1 != kWideEmpty && !(R.lim < th1);
   h2 = h2 && c2 != kWideEmpty && !(R.lim < th2);

@@ -343,6 +343,14 @@ int pt_dist_finalize(pt_context* ctx);
  * 4-wide nodes.  Every child box is a reference leaf box bitwise or contains
  * the leaf boxes below it, so the walk's answers are the same. */
 #define PT_OPT_WIDE_BUILD 14
+/* PT_OPT_WF_FUSE: 1 (default) = with the culled wide walk, a lane of the
+ * wavefront traversal kernel that finds a closest hit for a primary, bounce
+ * or SSS ray also samples the path's first light (the draws pathTrace makes
+ * next, raytrace_comp.comp:345-366 / :383-402) and walks that shadow ray
+ * itself, so the path skips a ray round; the shading kernel takes both
+ * answers and runs the same shading.  0 = one ray per round.  Output is
+ * identical. */
+#define PT_OPT_WF_FUSE 15
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */

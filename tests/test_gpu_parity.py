@@ -962,3 +962,23 @@ def test_wide_walk_reupload_deeper_scene():
         ref, _ = _oracle(v, i, n, 72, 56, nb=2, cam=cam)
         _assert_same(r.read_accum(), ref, f"re-upload, stack bound {info[1]}")
     assert depths[1] > depths[0], depths
+
+
+@pytest.mark.parametrize("fuse", [0, 1])
+@pytest.mark.parametrize("case", ["sphere", "grid2lights", "cloud_int_bits"])
+def test_wide_walk_fused_shadow_rays(case, fuse):
+    """PT_OPT_WF_FUSE: the trace kernel walks a closest hit's first-light
+    shadow ray in the same lane (the shading kernel takes both answers) or
+    not; over a stale accumulator, depth 3, either way the oracle's frame."""
+    sv, si, cam, lights, int_bits = _wide_case(case)
+    v, i, n, _, _ = ptamd.Scene.from_arrays(sv, si).build_bvh(int_bits=int_bits).arrays()
+    W, H = 96, 72
+    ref, _ = _oracle(v, i, n, W, H, nb=1, depth=3, cam=cam, lights=lights, int_bits=int_bits)
+    ref, _ = _oracle(v, i, n, W, H, first=1, nb=3, depth=3, cam=cam, lights=lights, int_bits=int_bits, accum=ref)
+    r = _setup(v, i, n, cam=cam, lights=lights, int_bits=int_bits, lds=0, depth=3)
+    r.set_option(ptamd.PT_OPT_KERNEL, 3)
+    r.set_option(ptamd.PT_OPT_WF_FUSE, fuse)
+    r.resize_and_clear(W, H)
+    r.render(0, 1)
+    r.render(1, 3)
+    _assert_same(r.read_accum(), ref, f"fuse {fuse} {case}")
