@@ -179,7 +179,8 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool
 // emits the next rays; finally fold each pixel's sample colours in batch
 // order.  Buffers hold `cap` paths; larger launches run in batch chunks.
 struct WfBuffers {
-  float4* state[2];  // per list slot: the waiting path's PathSt, by component (float4 j of slot s at [j * cap + s])
+  float4* state[2];  // per list slot: the fields of the waiting path's PathSt its phase needs, by component
+                     // (chunk j of slot s at [j * cap + s], wf_store_state)
   float4* colors;    // per path radiance
   int* ids[2];       // work lists: path id per slot
   float4* rays[2];   // ... and its ray, 2 float4 per slot: {o.xyz, limit} {d.xyz, shadow}
@@ -187,7 +188,7 @@ struct WfBuffers {
   int* counters;     // [0],[1] list sizes, [2] trace fetch cursor ([4..6]: the second half's, two streams)
   long long cap;     // paths the buffers hold
 };
-constexpr int kWfStateF4 = 10;
+constexpr int kWfStateF4 = 9;   // state chunks (float4) a waiting path stores at most
 // kind word of a listed ray (rays[cap + s].w): 0 closest, 1 shadow, 2 null
 // shadow query, plus (PT_OPT_WF_FUSE, closest rays) kRayFuse: the trace
 // kernel walks the path's first-light shadow ray after a hit (the ray's

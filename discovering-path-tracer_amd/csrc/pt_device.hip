@@ -1589,29 +1589,86 @@ __global__ __launch_bounds__(256, PT_SM_MIN_BLOCKS) void render_sm_kernel(Render
 // RNG draws and traversal order are those of path_trace(); the colours are
 // folded per pixel in batch order at the end, so the image is bit-identical.
 // ===========================================================================
-static_assert(sizeof(PathSt) == kWfStateF4 * 16, "PathSt is stored as kWfStateF4 float4");
-
 // A waiting path's state travels with its ray: list slot s holds both, each
-// stored by component (float4 j of the state at state[list][j * cap + s];
-// the ray at rays[list][s] and rays[list][cap + s]).  A wave reads and writes
+// stored by component (chunk j of the state at state[list][j * cap + s]; the
+// ray at rays[list][s] and rays[list][cap + s]).  A wave reads and writes
 // consecutive slots, so every access instruction covers consecutive 16-B
 // words.  (Indexed by path, the state of a list's sparse surviving paths
 // cost 64 lines per instruction and a dependent load of the path id first;
 // by path and by component it measured +2.5 % / +4 %.)
-__device__ __forceinline__ void wf_load_state(const WfBuffers& B, int list, long long slot, PathSt* S) {
-  const float4* __restrict__ src = B.state[list] + slot;
-  float4 v[kWfStateF4];
-#pragma unroll
-  for (int j = 0; j < kWfStateF4; ++j) v[j] = src[(size_t)j * (size_t)B.cap];
-  __builtin_memcpy(S, v, sizeof(PathSt));
+//
+// Only the fields the phase the path waits in reads again are stored, in
+// chunks of 4 words, a prefix per phase (the 160-B PathSt lives in registers
+// only):
+//   c0 {s, rng, phase, depth}       c1 {thr.xyz, rad.x}
+//   c2 {rad.yz, li | sss_thr.z, k}  c3 {hp.xyz, hn.x}
+//   c4 {hn.yz, acc3.xy | sss_thr.xy}
+//   c5 {acc3.z, pend.xyz}           c6 {sss_thr.xyz, travel}
+//   c7 {cp.xyz, sn.x}               c8 {sn.yz, -, -}
+// PH_PRIMARY: c0 (thr = 1, rad = 0, depth = 0: PH_BEGIN's values); PH_BOUNCE:
+// c0-c2; PH_SSS: c0-c4 with sss_thr in the li / acc3 words (li and acc3 are
+// set again before they are read; the walk ray's origin and direction are
+// S.so / S.sd bitwise, restored from the ray record); PH_DIRECT: c0-c5;
+// PH_SSS_SHADOW: c0-c8.  With the fused shadow walks a path mostly waits in
+// PH_BOUNCE / PH_SSS: 48 / 80 B stored and loaded instead of 160.
+__device__ __forceinline__ int wf_state_chunks(int phase) {
+  return phase == PH_PRIMARY ? 1 : phase == PH_BOUNCE ? 3 : phase == PH_SSS ? 5 : phase == PH_DIRECT ? 6 : 9;
 }
 
 __device__ __forceinline__ void wf_store_state(const WfBuffers& B, int list, long long slot, const PathSt& S) {
   float4* __restrict__ dst = B.state[list] + slot;
-  float4 v[kWfStateF4];
-  __builtin_memcpy(v, &S, sizeof(PathSt));
+  const size_t cap = (size_t)B.cap;
+  const bool sss = S.phase == PH_SSS;
+  const int n = wf_state_chunks(S.phase);
+  dst[0] = make_float4(__uint_as_float(S.s), __uint_as_float(S.rng), __int_as_float(S.phase), __int_as_float(S.depth));
+  if (n > 1) {
+    dst[cap] = make_float4(S.thr.x, S.thr.y, S.thr.z, S.rad.x);
+    dst[2 * cap] = make_float4(S.rad.y, S.rad.z, sss ? S.sss_thr.z : __int_as_float(S.li), __int_as_float(S.k));
+  }
+  if (n > 3) {
+    dst[3 * cap] = make_float4(S.hp.x, S.hp.y, S.hp.z, S.hn.x);
+    dst[4 * cap] = sss ? make_float4(S.hn.y, S.hn.z, S.sss_thr.x, S.sss_thr.y)
+                       : make_float4(S.hn.y, S.hn.z, S.acc3.x, S.acc3.y);
+  }
+  if (n > 5) dst[5 * cap] = make_float4(S.acc3.z, S.pend.x, S.pend.y, S.pend.z);
+  if (n > 6) {
+    dst[6 * cap] = make_float4(S.sss_thr.x, S.sss_thr.y, S.sss_thr.z, S.travel);
+    dst[7 * cap] = make_float4(S.cp.x, S.cp.y, S.cp.z, S.sn.x);
+    dst[8 * cap] = make_float4(S.sn.y, S.sn.z, 0.0f, 0.0f);
+  }
+}
+
+// o, d: the path's waiting ray (PH_SSS: S.so, S.sd).  Every field is
+// assigned (chunks a phase does not store read as 0), so the state stays in
+// registers.
+__device__ __forceinline__ void wf_load_state(const WfBuffers& B, int list, long long slot, v3 o, v3 d, PathSt* S) {
+  const float4* __restrict__ src = B.state[list] + slot;
+  const size_t cap = (size_t)B.cap;
+  float4 c[kWfStateF4];
+  c[0] = src[0];
+  const int phase = __float_as_int(c[0].z);
+  const int n = wf_state_chunks(phase);
 #pragma unroll
-  for (int j = 0; j < kWfStateF4; ++j) dst[(size_t)j * (size_t)B.cap] = v[j];
+  for (int j = 1; j < kWfStateF4; ++j) c[j] = j < n ? src[(size_t)j * cap] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  const bool prim = n == 1, sss = phase == PH_SSS;
+  S->s = __float_as_uint(c[0].x);
+  S->rng = __float_as_uint(c[0].y);
+  S->phase = phase;
+  S->depth = __float_as_int(c[0].w);
+  S->thr = prim ? mk(1.0f, 1.0f, 1.0f) : mk(c[1].x, c[1].y, c[1].z);
+  S->rad = prim ? mk(0.0f, 0.0f, 0.0f) : mk(c[1].w, c[2].x, c[2].y);
+  S->li = __float_as_int(c[2].z);
+  S->k = __float_as_int(c[2].w);
+  S->hp = mk(c[3].x, c[3].y, c[3].z);
+  S->hn = mk(c[3].w, c[4].x, c[4].y);
+  S->acc3 = mk(c[4].z, c[4].w, c[5].x);
+  S->pend = mk(c[5].y, c[5].z, c[5].w);
+  S->sss_thr = sss ? mk(c[4].z, c[4].w, c[2].z) : mk(c[6].x, c[6].y, c[6].z);
+  S->travel = c[6].w;
+  S->so = o;
+  S->sd = d;
+  S->cp = mk(c[7].x, c[7].y, c[7].z);
+  S->sn = mk(c[7].w, c[8].x, c[8].y);
 }
 
 // bits: kRayFuse / kRayPrimary (fuse_bits); the limit word of a fused
@@ -2375,12 +2432,12 @@ __global__ __launch_bounds__(256, PT_WF_SHADE_MIN_BLOCKS) void wf_shade_kernel(R
     PathSt S;
     if (i < count) {
       p = B.ids[cur][i];
-      wf_load_state(B, cur, i, &S);
       float4 r0, r1;
       wf_load_ray(B.rays[cur], B.cap, i, &r0, &r1);
       const float2 h = B.hits[i];
       T.o = mk(r0.x, r0.y, r0.z);
       T.d = mk(r1.x, r1.y, r1.z);
+      wf_load_state(B, cur, i, T.o, T.d, &S);
       T.shadow = __float_as_int(r1.w) & kRayKindMask;
       T.lim = h.x;
       T.res = __float_as_int(h.y);
