@@ -367,6 +367,8 @@ struct pt_context {
   // culled wide walk (wide_walk.h): nodes, triangle records by rank, rank ->
   // slot, per-lane stack overflow areas (grown on demand)
   float4* d_wide = nullptr;
+  float4* d_wide_q = nullptr;        // the same wide nodes in the 64-B layout
+  float4* d_wide_leafbox = nullptr;  // the reference's leaf boxes by rank (64-B walk)
   float4* d_wide_tris = nullptr;
   int* d_wide_rank_of = nullptr;
   int2* d_wide_ovf = nullptr;
@@ -376,6 +378,7 @@ struct pt_context {
   std::string wide_reason = "no scene";
   int opt_wide = 1;           // PT_OPT_WIDE
   int opt_wf_fuse = 1;        // PT_OPT_WF_FUSE
+  int opt_wide_node = 64;     // PT_OPT_WIDE_NODE
   int n_nodes_full = 0;
   float4* d_tris = nullptr;
   int n_tris = 0;
@@ -813,6 +816,8 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.wide_stack = 0;
   p.wide_handback = 0;
   p.wf_fuse = 0;
+  p.wide_qn = 0;
+  p.wide_leafbox = nullptr;
   p.nodes = c->stats_mode ? c->d_nodes_full : c->d_nodes;
   p.tris = c->d_tris;
   p.hit_tris = c->d_tris;
@@ -1000,7 +1005,9 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
         c->wide_ovf_lanes = lanes;
         c->wide_ovf_stack = c->wide_stack;
       }
-      p.wide = c->d_wide;
+      p.wide_qn = c->opt_wide_node == 64 ? 1 : 0;
+      p.wide = p.wide_qn ? c->d_wide_q : c->d_wide;
+      p.wide_leafbox = c->d_wide_leafbox;
       p.wide_tris = c->d_wide_tris;
       p.wide_rank_of = c->d_wide_rank_of;
       p.hit_tris = c->d_wide_tris;   // closest hits come back as ranks
@@ -1093,6 +1100,8 @@ int pt_destroy(pt_context* c) {
   dev_free(c->d_nodes_full);
   dev_free(c->d_pairs);
   dev_free(c->d_wide);
+  dev_free(c->d_wide_q);
+  dev_free(c->d_wide_leafbox);
   dev_free(c->d_wide_tris);
   dev_free(c->d_wide_rank_of);
   dev_free(c->d_wide_ovf);
@@ -1176,6 +1185,8 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   dev_free(c->d_nodes_full);
   dev_free(c->d_pairs);
   dev_free(c->d_wide);
+  dev_free(c->d_wide_q);
+  dev_free(c->d_wide_leafbox);
   dev_free(c->d_wide_tris);
   dev_free(c->d_wide_rank_of);
   dev_free(c->d_tris);
@@ -1213,6 +1224,12 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   std::vector<int> rank_of_host(wide_reason.empty() ? (size_t)T : 0);
   if (wide_reason.empty()) {
     PT_HIP(hipMalloc((void**)&c->d_wide, wide.nodes.size() * sizeof(float)));
+    PT_HIP(hipMalloc((void**)&c->d_wide_q, wide.qnodes.size() * sizeof(float)));
+    PT_HIP(hipMalloc((void**)&c->d_wide_leafbox, wide.leaf_box.size() * sizeof(float)));
+    PT_HIP(hipMemcpyAsync(c->d_wide_q, wide.qnodes.data(), wide.qnodes.size() * sizeof(float), hipMemcpyHostToDevice,
+                          c->stream));
+    PT_HIP(hipMemcpyAsync(c->d_wide_leafbox, wide.leaf_box.data(), wide.leaf_box.size() * sizeof(float),
+                          hipMemcpyHostToDevice, c->stream));
     PT_HIP(hipMalloc((void**)&c->d_wide_rank_of, (size_t)T * sizeof(int)));
     PT_HIP(hipMalloc((void**)&c->d_wide_tris, (size_t)T * 3 * sizeof(float4)));
     PT_HIP(hipMemcpyAsync(c->d_wide, wide.nodes.data(), wide.nodes.size() * sizeof(float), hipMemcpyHostToDevice,
@@ -1501,6 +1518,10 @@ int pt_set_option(pt_context* c, int key, int value) {
     case PT_OPT_WIDE:
       if (value < 0 || value > 2) return fail(PT_ERR_INVALID, "PT_OPT_WIDE takes 0, 1 or 2");
       c->opt_wide = value;
+      return PT_OK;
+    case PT_OPT_WIDE_NODE:
+      if (value != 64 && value != 128) return fail(PT_ERR_INVALID, "PT_OPT_WIDE_NODE takes 64 or 128");
+      c->opt_wide_node = value;
       return PT_OK;
     case PT_OPT_WF_FUSE:
       if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_WF_FUSE takes 0 or 1");

@@ -88,7 +88,9 @@ struct RenderParams {
   // by leaf rank, triangle slot -> rank, per-lane stack overflow areas
   // (wide_ovf_lanes lanes of wide_stack entries, lane-strided)
   const float4* hit_tris;   // the records a closest hit's index refers to: wide_tris (by rank) with the wide walk, else tris
-  const float4* wide;
+  const float4* wide;        // 64-B nodes when wide_qn, else 128-B (wide_walk.h)
+  int wide_qn;
+  const float4* wide_leafbox;   // wide_qn: the reference's leaf box per rank, 2 float4
   const float4* wide_tris;
   const int* wide_rank_of;
   int2* wide_ovf;

@@ -2226,7 +2226,7 @@ __device__ __forceinline__ int fused_shadow_ray(const RenderParams& P, v3 o, v3 
 }
 constexpr int kFuseWalk = 16;   // lane state: walking the fused shadow ray
 
-template <int G, bool CNT = false>
+template <int G, bool CNT = false, bool QN = true>
 __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(RenderParams P, WfBuffers B,
                                                                                 int cur) {
   const int tid = (int)threadIdx.x;
@@ -2293,8 +2293,8 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
     for (int it = 0; it < PT_WF_STEPS; ++it) {
       bool exact = false;
       if (!PT_WIDE_QUEUE) {
-        if (p >= 0 && wide_step<CNT>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
-                                     &c.leaves)) {
+        if (p >= 0 && wide_step<CNT, false, QN>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact,
+                                                &c.nodes, &c.leaves, nullptr, P.wide_leafbox)) {
           int res;
           if (exact) res = R.shadow ? kNeedExactShadow : kNeedExactClosest;
           else if (R.shadow) res = R.best;
@@ -2305,8 +2305,8 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
       } else {
         // fin: the walk has no node left (its queue may still hold candidates)
         if (p >= 0 && !fin)
-          fin = wide_step<CNT, true>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
-                                     &c.leaves, cand);
+          fin = wide_step<CNT, true, QN>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
+                                         &c.leaves, cand, P.wide_leafbox);
         if (exact) {
           R.nc = 0;
           // a fused shadow ray the walk cannot take goes to the shading's next round
@@ -2335,7 +2335,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
 #endif
         if (__ballot(p >= 0 && R.nc > kWideQ - 4) || (int)__popcll(waiting) >= PT_WIDE_FLUSH_T ||
             (waiting && __ballot(p >= 0 && !fin) == 0ull)) {
-          if (p >= 0 && R.nc > 0 && wide_flush<CNT>(R, P.wide_tris, cand, &c.leaves)) {
+          if (p >= 0 && R.nc > 0 && wide_flush<CNT, QN>(R, P.wide_tris, cand, &c.leaves, P.wide_leafbox)) {
             fin = true;   // occluded
             R.sp = 0;
             R.cur = -1;
@@ -2650,7 +2650,8 @@ long long wide_trace_lanes() {
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
   int most = 0;
-  for (auto k : {wf_trace_wide_kernel<kWideG>, wf_trace_wide_kernel<kWideG, true>}) {
+  for (auto k : {wf_trace_wide_kernel<kWideG, false, true>, wf_trace_wide_kernel<kWideG, true, true>,
+                 wf_trace_wide_kernel<kWideG, false, false>, wf_trace_wide_kernel<kWideG, true, false>}) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess) return 0;
     most = std::max(most, per_cu);
   }
@@ -2691,7 +2692,8 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
                 : (g2 ? wf_trace_pairs_kernel<2> : wf_trace_pairs_kernel<4>);
   const bool wide = p0.wide && !lds_scene && !p0.pairs;
   if (wide)   // culled wide walk (PT_OPT_WIDE, default)
-    trace = cnt ? wf_trace_wide_kernel<kWideG, true> : wf_trace_wide_kernel<kWideG>;
+    trace = p0.wide_qn ? (cnt ? wf_trace_wide_kernel<kWideG, true, true> : wf_trace_wide_kernel<kWideG, false, true>)
+                       : (cnt ? wf_trace_wide_kernel<kWideG, true, false> : wf_trace_wide_kernel<kWideG, false, false>);
   size_t lds_t = lds;
   if (p0.pairs && !lds_scene) lds_t = (size_t)4 * 64 * p0.pair_depth * sizeof(int);   // the walk stacks
   if (wide) lds_t = 0;

@@ -29,6 +29,70 @@ float down_f(double x) {
   return f;
 }
 
+// bf16 bits of x >= 0 rounded up (toward +inf)
+uint32_t bf16_up(float x) {
+  uint32_t b;
+  memcpy(&b, &x, 4);
+  return (b >> 16) + ((b & 0xffffu) ? 1u : 0u);
+}
+
+// One 64-B node (wide_walk.h kWideQNodeF4) from a 32-float node: per axis a
+// grid origin p (the children's least lo) and step s = 2^e (the smallest
+// with fl(p + 255 s) >= the largest hi); each child's lo rounded down and hi
+// rounded up onto the grid, checked with the device's own decode
+// fmaf(q, s, p) (q s is exact, so this is fl(p + q s) on both sides).
+// Returns false if some box cannot be enclosed (it always can: the caller
+// reports it as a builder error).
+bool quantize_node(const float* rec, float* q) {
+  int32_t refs[4];
+  memcpy(refs, rec + 24, sizeof refs);
+  uint32_t packed[6] = {0, 0, 0, 0, 0, 0};   // qlo.x qhi.x qlo.y qhi.y qlo.z qhi.z
+  uint32_t meta = 0;
+  for (int a = 0; a < 3; ++a) {
+    float pmin = INFINITY, hmax = -INFINITY;
+    for (int j = 0; j < 4; ++j)
+      if (refs[j] != kEmpty) {
+        pmin = std::min(pmin, rec[8 * a + j]);
+        hmax = std::max(hmax, rec[8 * a + 4 + j]);
+      }
+    if (!(pmin <= hmax)) return false;
+    const float p = pmin;
+    const double d = (double)hmax - (double)p;
+    int e = d > 0.0 ? (int)ceil(log2(d / 255.0)) : -126;
+    e = std::max(-126, std::min(127, e));
+    while (e < 127 && fmaf(255.0f, ldexpf(1.0f, e), p) < hmax) ++e;
+    while (e > -126 && fmaf(255.0f, ldexpf(1.0f, e - 1), p) >= hmax) --e;
+    const float s = ldexpf(1.0f, e);
+    if (!(fmaf(255.0f, s, p) >= hmax)) return false;
+    meta |= (uint32_t)(e + 127) << (8 * a);
+    q[a] = p;
+    for (int j = 0; j < 4; ++j) {
+      uint32_t ql = 255, qh = 0;   // empty slot: an inverted box (the walk also checks the ref)
+      if (refs[j] != kEmpty) {
+        const float lo = rec[8 * a + j], hi = rec[8 * a + 4 + j];
+        int l = (int)std::max(0.0, std::min(255.0, floor(((double)lo - (double)p) / (double)s)));
+        while (l > 0 && fmaf((float)l, s, p) > lo) --l;
+        while (l < 255 && fmaf((float)(l + 1), s, p) <= lo) ++l;
+        int h = (int)std::max(0.0, std::min(255.0, ceil(((double)hi - (double)p) / (double)s)));
+        while (h < 255 && fmaf((float)h, s, p) < hi) ++h;
+        while (h > 0 && fmaf((float)(h - 1), s, p) >= hi) --h;
+        if (!(fmaf((float)l, s, p) <= lo && fmaf((float)h, s, p) >= hi)) return false;
+        ql = (uint32_t)l;
+        qh = (uint32_t)h;
+      }
+      packed[2 * a] |= ql << (8 * j);
+      packed[2 * a + 1] |= qh << (8 * j);
+    }
+  }
+  memcpy(&q[3], &meta, 4);
+  memcpy(&q[4], packed, sizeof packed);
+  q[10] = rec[28];   // c1 (already rounded down)
+  const uint32_t e01 = bf16_up(rec[29]) | (bf16_up(rec[30]) << 16);   // E0, E1 rounded up
+  memcpy(&q[11], &e01, 4);
+  memcpy(&q[12], refs, sizeof refs);
+  return true;
+}
+
 }  // namespace
 
 WideCoeffs coeff_max(const WideCoeffs& a, const WideCoeffs& b) {
@@ -439,6 +503,18 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
     bound[w] = std::max(0, n_inner[w] - 1) + m;
   }
   if (bound[0] > 4096) return "tree too deep for the wide walk's stack";
+  // the 64-B layout of the same nodes, and the reference's leaf boxes by rank
+  // (the walk over 64-B nodes tests a leaf's exact box before it accepts a hit)
+  out->qnodes.assign(16 * nw, 0.0f);
+  for (size_t w = 0; w < nw; ++w)
+    if (!quantize_node(&W[32 * w], &out->qnodes[16 * w])) return "a wide node's boxes cannot be quantized";
+  out->leaf_box.assign(8 * n_tris, 0.0f);
+  for (size_t v = 0; v < n; ++v)
+    if (leaf(v))
+      for (int a = 0; a < 3; ++a) {
+        out->leaf_box[8 * (size_t)rank[v] + a] = lo(v, a);
+        out->leaf_box[8 * (size_t)rank[v] + 4 + a] = hi(v, a);
+      }
   out->n_nodes = (int)nw;
   out->stack_cap = bound[0] + 1;
   return "";

@@ -19,6 +19,8 @@ namespace pt {
 
 struct WideBVH {
   std::vector<float> nodes;        // 32 floats per node, the wide_walk.h layout
+  std::vector<float> qnodes;       // the same nodes, 16 floats each: child boxes on an 8-bit grid (wide_walk.h)
+  std::vector<float> leaf_box;     // 8 floats per leaf rank: the reference's leaf box {lo.xyz, 0, hi.xyz, 0}
   std::vector<int32_t> rank_tri;   // leaf rank -> triangle slot (the reference's triIdx)
   int n_nodes = 0;
   int stack_cap = 0;               // most stack entries a walk can hold

@@ -57,6 +57,24 @@ namespace ptd {
 // stored by rank (the reference tris layout, 3 float4), with rank -> slot.
 constexpr int kWideNodeF4 = 8;
 constexpr int32_t kWideEmpty = (int32_t)0x80000000;
+// 64-B node (QN, the default layout; wide_bvh.cpp quantize_node): 4 float4
+//   [0] {p.xyz, meta}  meta byte a: biased exponent of the axis-a grid step s_a
+//   [1] {qlo.x, qhi.x, qlo.y, qhi.y}   uint32 each, byte j = child j
+//   [2] {qlo.z, qhi.z, c1, E0 | E1 << 16 (bf16, rounded up)}
+//   [3] child refs
+// Child j's box on axis a is [fma(qlo_j, s_a, p_a), fma(qhi_j, s_a, p_a)]:
+// the builder rounds every box outward onto the grid and checks these exact
+// float values enclose it, so the decoded box contains the 128-B node's box
+// (a leaf's decoded box contains the reference's leaf box, which the walk
+// then tests exactly before it accepts that leaf's hit, wide_cand).  Every
+// argument above holds for any enclosing box: a larger box passes the slab
+// test whenever the box it contains does, its entry parameter and Smax only
+// lower the cull threshold.  Half the bytes and load instructions per node
+// visit: the trace kernel is bound by its vector-memory pipeline (TD busy
+// 91-97 % with 128-B nodes, profiles/r03).
+constexpr int kWideQNodeF4 = 4;
+PT_FN float wq_scale(uint32_t meta, int a) { return u2f(((meta >> (8 * a)) & 0xffu) << 23); }
+PT_FN float wq_dec(uint32_t w, int j, float s, float p) { return fma_((float)((w >> (8 * j)) & 0xffu), s, p); }
 #ifndef PT_WIDE_LDS_STACK
 #define PT_WIDE_LDS_STACK 8
 #endif
@@ -188,16 +206,24 @@ PT_FN void wide_start(WideRay& R, v3 o, v3 d, bool shadow, float limit) {
 // rules; true when a shadow ray is occluded (its walk is over).
 // One queued candidate's test with the reference's accept rules; true when a
 // shadow ray is occluded.
-PT_FN bool wide_cand(WideRay& R, int r, float4 A, float4 B, float4 C) {
+// QN: the candidate came from a decoded (enclosing) leaf box; the reference
+// tests its triangle only if its own leaf box passes intersectAABB, so a hit
+// that would count is checked against that box first (rare: accepted hits).
+template <bool QN = false>
+PT_FN bool wide_leaf_ok(const WideRay& R, const float4* __restrict__ leaf_box, int r) {
+  return !QN || slab(R.o, R.inv, leaf_box[2 * (size_t)r], leaf_box[2 * (size_t)r + 1]);
+}
+template <bool QN = false>
+PT_FN bool wide_cand(WideRay& R, int r, float4 A, float4 B, float4 C, const float4* __restrict__ leaf_box = nullptr) {
   float t;
   if (tri_test(R.o, R.d, A, B, C, &t)) {
     if (R.shadow) {
-      if (t < 1e30f && !(t >= R.lim)) {   // :359, :398
+      if (t < 1e30f && !(t >= R.lim) && wide_leaf_ok<QN>(R, leaf_box, r)) {   // :359, :398
         R.best = 1;
         return true;
       }
-    } else if (t < R.lim || (t == R.lim && r < R.best)) {   // :185 strict '<' in visit order
-      R.lim = t;
+    } else if ((t < R.lim || (t == R.lim && r < R.best)) && wide_leaf_ok<QN>(R, leaf_box, r)) {   // :185
+      R.lim = t;   // strict '<' in visit order
       R.best = r;
     }
   }
@@ -213,8 +239,9 @@ PT_FN bool wide_cand(WideRay& R, int r, float4 A, float4 B, float4 C) {
 #ifndef PT_WIDE_FLUSH_BATCH
 #define PT_WIDE_FLUSH_BATCH 2
 #endif
-template <bool CNT>
-PT_FN bool wide_flush(WideRay& R, const float4* __restrict__ tris, const int* cand, uint32_t* cl) {
+template <bool CNT, bool QN = false>
+PT_FN bool wide_flush(WideRay& R, const float4* __restrict__ tris, const int* cand, uint32_t* cl,
+                      const float4* __restrict__ leaf_box = nullptr) {
   const int n = R.nc;
   R.nc = 0;
   constexpr int KB = PT_WIDE_FLUSH_BATCH;
@@ -233,7 +260,7 @@ PT_FN bool wide_flush(WideRay& R, const float4* __restrict__ tris, const int* ca
     for (int k = 0; k < KB; ++k) {
       if (i + k < n) {
         if (CNT) ++*cl;
-        if (wide_cand(R, r[k], A[k], B[k], C[k])) return true;
+        if (wide_cand<QN>(R, r[k], A[k], B[k], C[k], leaf_box)) return true;
       }
     }
   }
@@ -243,17 +270,35 @@ PT_FN bool wide_flush(WideRay& R, const float4* __restrict__ tris, const int* ca
 // One node of the walk; true when the ray is finished (R.lim / R.best hold
 // the answer) or must be handed to the exact walk (*exact).  stack_cap: the
 // builder's bound on entries (overflow area size per lane).
-template <bool CNT, bool QUEUE = false>
+template <bool CNT, bool QUEUE = false, bool QN = false>
 PT_FN bool wide_step(WideRay& R, const float4* __restrict__ nodes, const float4* __restrict__ tris, int2* lds,
                      int ls, int2* ovf, long long os, int stack_cap, bool* exact, uint32_t* cn, uint32_t* cl,
-                     int* cand = nullptr) {
+                     int* cand = nullptr, const float4* __restrict__ leaf_box = nullptr) {
   while (R.cur < 0) {
     if (R.sp == 0) return true;
     const int2 e = wide_pop(R, lds, ls, ovf, os);
     if (!(R.lim < u2f((uint32_t)e.y))) R.cur = e.x;   // still able to hold a winner
   }
-  const float4* nd = nodes + (size_t)R.cur * kWideNodeF4;
-  const float4 lx = nd[0], hx = nd[1], ly = nd[2], hy = nd[3], lz = nd[4], hz = nd[5], cf = nd[6], kf = nd[7];
+  float4 lx, hx, ly, hy, lz, hz, cf, kf;
+  if (QN) {
+    const float4* nd = nodes + (size_t)R.cur * kWideQNodeF4;
+    const float4 q0 = nd[0], q1 = nd[1], q2 = nd[2];
+    cf = nd[3];
+    const uint32_t meta = f2u(q0.w);
+    const float sx = wq_scale(meta, 0), sy = wq_scale(meta, 1), sz = wq_scale(meta, 2);
+    const uint32_t a0 = f2u(q1.x), a1 = f2u(q1.y), a2 = f2u(q1.z), a3 = f2u(q1.w), a4 = f2u(q2.x), a5 = f2u(q2.y);
+    lx = make_float4(wq_dec(a0, 0, sx, q0.x), wq_dec(a0, 1, sx, q0.x), wq_dec(a0, 2, sx, q0.x), wq_dec(a0, 3, sx, q0.x));
+    hx = make_float4(wq_dec(a1, 0, sx, q0.x), wq_dec(a1, 1, sx, q0.x), wq_dec(a1, 2, sx, q0.x), wq_dec(a1, 3, sx, q0.x));
+    ly = make_float4(wq_dec(a2, 0, sy, q0.y), wq_dec(a2, 1, sy, q0.y), wq_dec(a2, 2, sy, q0.y), wq_dec(a2, 3, sy, q0.y));
+    hy = make_float4(wq_dec(a3, 0, sy, q0.y), wq_dec(a3, 1, sy, q0.y), wq_dec(a3, 2, sy, q0.y), wq_dec(a3, 3, sy, q0.y));
+    lz = make_float4(wq_dec(a4, 0, sz, q0.z), wq_dec(a4, 1, sz, q0.z), wq_dec(a4, 2, sz, q0.z), wq_dec(a4, 3, sz, q0.z));
+    hz = make_float4(wq_dec(a5, 0, sz, q0.z), wq_dec(a5, 1, sz, q0.z), wq_dec(a5, 2, sz, q0.z), wq_dec(a5, 3, sz, q0.z));
+    const uint32_t e01 = f2u(q2.w);
+    kf = make_float4(q2.z, u2f(e01 << 16), u2f(e01 & 0xffff0000u), 0.0f);
+  } else {
+    const float4* nd = nodes + (size_t)R.cur * kWideNodeF4;
+    lx = nd[0]; hx = nd[1]; ly = nd[2]; hy = nd[3]; lz = nd[4]; hz = nd[5]; cf = nd[6]; kf = nd[7];
+  }
   if (CNT) ++*cn;
   const v3 ainv = wide_ainv(R);
   const int c0 = (int)f2u(cf.x), c1 = (int)f2u(cf.y), c2 = (int)f2u(cf.z),
@@ -290,19 +335,10 @@ PT_FN bool wide_step(WideRay& R, const float4* __restrict__ nodes, const float4*
     if (R.lim < thj) continue;   // culled by a hit found in this node
     if (CNT) ++*cl;
     const float4* T = tris + 3 * (size_t)r;
-    float t;
-    if (tri_test(R.o, R.d, T[0], T[1], T[2], &t)) {
-      if (R.shadow) {
-        if (t < 1e30f && !(t >= R.lim)) {   // :359, :398
-          R.best = 1;
-          R.cur = -1;
-          R.sp = 0;
-          return true;
-        }
-      } else if (t < R.lim || (t == R.lim && r < R.best)) {   // :185 strict '<' in visit order
-        R.lim = t;
-        R.best = r;
-      }
+    if (wide_cand<QN>(R, r, T[0], T[1], T[2], leaf_box)) {   // an occluded shadow ray
+      R.cur = -1;
+      R.sp = 0;
+      return true;
     }
   }
   // inner children still live: nearest first, the others onto the stack

@@ -351,6 +351,12 @@ int pt_dist_finalize(pt_context* ctx);
  * answers and runs the same shading.  0 = one ray per round.  Output is
  * identical. */
 #define PT_OPT_WF_FUSE 15
+/* PT_OPT_WIDE_NODE: byte size of the culled wide walk's nodes.  64 (default)
+ * = child boxes rounded outward onto an 8-bit grid per node (half the bytes
+ * and load instructions per node visit; a leaf's exact box is tested before
+ * its hit counts); 128 = the boxes as floats.  Both are built at upload.
+ * Output is identical. */
+#define PT_OPT_WIDE_NODE 16
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */

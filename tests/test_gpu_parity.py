@@ -849,15 +849,18 @@ def _wide_case(case):
     return v, i, scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, False
 
 
+@pytest.mark.parametrize("node", [64, 128])
 @pytest.mark.parametrize("build", [1, 0], ids=["sah", "reference_tree"])
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("case", ["sphere", "cloud_int_bits", "dense_cloud", "grid2lights", "box"])
-def test_wide_walk_matches_oracle(case, mode, build):
+def test_wide_walk_matches_oracle(case, mode, build, node):
     """The culled wide walk (wavefront pipeline, device-memory scene) gives the
     oracle's frame bit for bit, over either grouping of the reference's leaves
-    (PT_OPT_WIDE_BUILD: binned SAH, or the reference's own tree); mode 2 hands
-    every odd ray of each round to the exact threaded walk in the shading
-    kernel (the path rays with a zero direction component take)."""
+    (PT_OPT_WIDE_BUILD: binned SAH, or the reference's own tree) and either
+    node layout (PT_OPT_WIDE_NODE: 64-B nodes with grid-rounded boxes and
+    exact leaf tests, or float boxes); mode 2 hands every odd ray of each
+    round to the exact threaded walk in the shading kernel (the path rays
+    with a zero direction component take)."""
     sv, si, cam, lights, int_bits = _wide_case(case)
     v, i, n, _, _ = ptamd.Scene.from_arrays(sv, si).build_bvh(int_bits=int_bits).arrays()
     r = _setup(v, i, n, cam=cam, lights=lights, int_bits=int_bits, lds=0)
@@ -865,6 +868,7 @@ def test_wide_walk_matches_oracle(case, mode, build):
     r.upload_scene(v, i, n, int_bits=int_bits)   # the build option is read at upload
     r.set_option(ptamd.PT_OPT_KERNEL, 3)
     r.set_option(ptamd.PT_OPT_WIDE, mode)
+    r.set_option(ptamd.PT_OPT_WIDE_NODE, node)
     info = r.wide_info()
     assert info[0] > 0 and info[1] > 0, info
     r.resize_and_clear(80, 52)

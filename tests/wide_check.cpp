@@ -18,6 +18,8 @@ using namespace ptd;
 
 namespace {
 int g_mode = pt::WIDE_SAH;   // wide_set_mode
+int g_node = 128;            // wide_set_variant: node bytes (64: the quantized layout with exact leaf tests)
+int g_queue = 0;             // ... and 1: the queued leaf tests with wave-style flushes (the kernel's default)
 
 struct Built {
   pt::WideBVH w;
@@ -44,12 +46,50 @@ std::string build(const float* V, size_t nvf, const uint32_t* I, size_t nt, cons
   }
   return "";
 }
+
+// One ray's walk in the configured variant, as the trace kernel runs it:
+// QUEUE: leaf hits queued (stride 64, like one lane of the kernel's LDS
+// queue) and flushed when the queue cannot take another node's four leaves
+// or the walk has no node left (PT_WIDE_FLUSH_T 1).
+template <bool QN, bool QUEUE>
+void walk(WideRay& R, const Built& b, int2* lds, int2* ovf, bool* exact, uint32_t* cn, uint32_t* cl) {
+  const float4* nodes = (const float4*)(QN ? b.w.qnodes.data() : b.w.nodes.data());
+  const float4* leafbox = (const float4*)b.w.leaf_box.data();
+  if (!QUEUE) {
+    while (!wide_step<true, false, QN>(R, nodes, b.tris.data(), lds, 1, ovf, 1, b.w.stack_cap, exact, cn, cl, nullptr,
+                                       leafbox)) {
+    }
+    return;
+  }
+  std::vector<int> cand(kWideQ * 64, -1);
+  bool fin = false;
+  for (;;) {
+    if (!fin)
+      fin = wide_step<true, true, QN>(R, nodes, b.tris.data(), lds, 1, ovf, 1, b.w.stack_cap, exact, cn, cl,
+                                      cand.data(), leafbox);
+    if (*exact) return;
+    if (R.nc > kWideQ - 4 || (fin && R.nc > 0)) {
+      if (wide_flush<true, QN>(R, b.tris.data(), cand.data(), cl, leafbox)) {   // occluded
+        fin = true;
+        R.sp = 0;
+        R.cur = -1;
+      }
+    }
+    if (fin && R.nc == 0) return;
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
 // The wide builder the next calls use (pt::WideBuild).
 void wide_set_mode(int mode) { g_mode = mode; }
+// The walk variant the next wide_check calls run: node bytes 64 or 128, queued leaf tests or not.
+void wide_set_variant(int node_bytes, int queue) {
+  g_node = node_bytes;
+  g_queue = queue;
+}
 
 // info[0] wide nodes, info[1] stack bound.  Returns 0, or 1 with the reason in err.
 int wide_info(const float* V, size_t nvf, const uint32_t* I, size_t nt, const float* N, size_t nn, int int_bits,
@@ -101,7 +141,6 @@ int wide_check(const float* V, size_t nvf, const uint32_t* I, size_t nt, const f
   std::vector<int2> lds(kWideLds), ovf((size_t)b.w.stack_cap + 1);
   memset(stats, 0, 8 * sizeof(uint64_t));
   stats[7] = ~0ull;
-  const float4* nodes = (const float4*)b.w.nodes.data();
   for (size_t i = 0; i < n; ++i) {
     const float* r = rays + 8 * i;
     const v3 o = mk(r[0], r[1], r[2]), d = mk(r[3], r[4], r[5]);
@@ -119,9 +158,12 @@ int wide_check(const float* V, size_t nvf, const uint32_t* I, size_t nt, const f
     bool exact = !wide_ray_ok(R.o, R.d, R.inv);
     uint32_t cn = 0, cl = 0;
     if (!exact) {
-      while (!wide_step<true>(R, nodes, b.tris.data(), lds.data(), 1, ovf.data(), 1, b.w.stack_cap, &exact, &cn,
-                              &cl)) {
-      }
+      if (g_node == 64)
+        g_queue ? walk<true, true>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl)
+                : walk<true, false>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl);
+      else
+        g_queue ? walk<false, true>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl)
+                : walk<false, false>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl);
     }
     stats[3] += cn;
     stats[4] += cl;
