@@ -357,10 +357,12 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
     return out
 
 
-def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light, cam, depth, sss):
+def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light, cam, depth, sss, coll_dev):
     """RCCL communicator for pt_dist_run and a 4-frame bitwise self-check on
     the root against a single-GPU render; None (every rank) if anything
-    fails, so the caller keeps the Python step."""
+    fails, so the caller keeps the Python step.  coll_dev: where the
+    torch.distributed process group wants its tensors (the GPU for nccl, the
+    host for gloo -- the one-GPU rehearsal with PT_RCCL_LIB)."""
     import ptamd
     import torch
     ok = 1
@@ -371,7 +373,7 @@ def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light,
         except ptamd.PTError as e:
             print(f"bench: native step loop unavailable: {e}", file=sys.stderr, flush=True)
             ok = 0
-    t = torch.tensor([ok] + list(uid), dtype=torch.uint8, device=dev)
+    t = torch.tensor([ok] + list(uid), dtype=torch.uint8, device=coll_dev)
     dist.broadcast(t, 0)   # the id, and whether rank 0 could make one
     if int(t[0].item()) == 0:
         return None
@@ -402,7 +404,7 @@ def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light,
     except ptamd.PTError as e:
         print(f"bench: native step loop unavailable: {e}", file=sys.stderr, flush=True)
         ok = 0
-    flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+    flag = torch.tensor([ok], dtype=torch.int32, device=coll_dev)
     dist.all_reduce(flag, op=dist.ReduceOp.MIN)
     if int(flag.item()) == 0:
         print("bench: native step loop failed its self-check; using the Python step", file=sys.stderr, flush=True)
@@ -750,10 +752,13 @@ def main():
     # over RCCL (and PT_BENCH_FORCE_DIST=1 at N = 1) unless PT_BENCH_NATIVE=0.
     # A 4-frame self-check against a single-GPU render runs first; if the root
     # finds any bit different, every rank falls back to the Python step.
+    # With PT_RCCL_LIB (the one-GPU rehearsal's stand-in for RCCL's
+    # point-to-point calls) it runs beside a gloo process group too.
     native = None
-    if (dist is not None and backend == "nccl" and args.collective == "gather" and args.assemble == 2
-            and os.environ.get("PT_BENCH_NATIVE", "1") != "0"):
-        native = setup_native(r, dist, dev, world, rank, W, H, SPP, v, i, n, int_bits, light, cam, DEPTH, SSS)
+    if (dist is not None and (backend == "nccl" or os.environ.get("PT_RCCL_LIB")) and args.collective == "gather"
+            and args.assemble == 2 and os.environ.get("PT_BENCH_NATIVE", "1") != "0"):
+        native = setup_native(r, dist, dev, world, rank, W, H, SPP, v, i, n, int_bits, light, cam, DEPTH, SSS,
+                              dev if backend == "nccl" else "cpu")
         if native is not None:
             outs = native["outs"]
             out = outs[0]
@@ -889,7 +894,9 @@ def main():
                        "parallelism": (f"tiles{world}-" + ("sparse-gather" if args.collective == "gather" else "reduce"))
                        if world > 1 else ("single-packed" if args.packed else "single"),
                        "streams": args.streams,
-                       "step_loop": "native (pt_dist_run, RCCL from C++)" if native is not None else "python",
+                       "step_loop": ("python" if native is None else
+                                     "native (pt_dist_run, RCCL from C++)" if not os.environ.get("PT_RCCL_LIB")
+                                     else "native (pt_dist_run, PT_RCCL_LIB stand-in)"),
                        "rays_per_frame": None if rays_per_frame != rays_per_frame else int(rays_per_frame),
                        "primary_cull": True,
                        "msamples_per_s": round(W * H * SPP * args.steps / dt / 1e6, 3)},

@@ -2207,15 +2207,24 @@ struct RcclApi {
   const char* (*GetErrorString)(ncclResult_t) = nullptr;
 };
 // RCCL is loaded only when the multi-GPU loop is used: the one already in
-// the process (torch's) if there is one, else the system's.
+// the process (torch's) if there is one, else the system's.  PT_RCCL_LIB
+// names another library with the same nine entry points instead, and then
+// only that one is tried (the tests' one-GPU stand-in, tests/dist_shim.cpp,
+// which moves the point-to-point bytes between processes sharing a device).
 const RcclApi* rccl_api() {
   static RcclApi api;
   static bool tried = false;
   if (!tried) {
     tried = true;
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    const char* alt = getenv("PT_RCCL_LIB");
+    void* h = nullptr;
+    if (alt && *alt) {
+      h = dlopen(alt, RTLD_NOW | RTLD_LOCAL);
+    } else {
+      h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+      if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+      if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    }
     if (h) {
       api.GetUniqueId = (decltype(api.GetUniqueId))dlsym(h, "ncclGetUniqueId");
       api.CommInitRank = (decltype(api.CommInitRank))dlsym(h, "ncclCommInitRank");

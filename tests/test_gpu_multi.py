@@ -59,3 +59,31 @@ def test_native_step_loop_single_rank_rccl():
     out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
     assert out["config"]["step_loop"].startswith("native"), res.stderr[-2000:]
     assert out["verified_bitwise_vs_single_gpu"] is True
+
+
+SHIM = os.path.join(ROOT, "tests", "_build", "libptdistshim.so")
+
+
+@pytest.mark.parametrize("streams", [1, 2])
+def test_native_step_loop_two_ranks_grouped_send_recv(streams):
+    """pt_dist_run's N > 1 schedule with two processes on the one GPU: the
+    grouped ncclSend/ncclRecv of every frame go through the stand-in
+    (tests/dist_shim.cpp via PT_RCCL_LIB: the same bytes moved between the
+    processes over hipIpc handles), the root receives rank 1's live items
+    into its receive sets and assembles frames k-2 inside its render
+    launches.  bench.py's 4-frame self-check and --verify compare every
+    assembled frame bitwise with a single-GPU render.  (Throughput over xGMI
+    is not measured by this: the stand-in is host-synchronous.)"""
+    assert os.path.exists(SHIM), "build it first: make -C tests"
+    env = dict(os.environ, PT_BENCH_DEVICE="0", PT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1",
+               PT_RCCL_LIB=SHIM)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "3", "--verify",
+           "--streams", str(streams)]
+    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
+    out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 2
+    assert out["config"]["step_loop"] == "native (pt_dist_run, PT_RCCL_LIB stand-in)", res.stderr[-2000:]
+    assert out["verified_bitwise_vs_single_gpu"] is True
