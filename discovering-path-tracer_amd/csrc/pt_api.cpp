@@ -371,6 +371,14 @@ struct pt_context {
   float4* d_wide_leafbox = nullptr;  // the reference's leaf boxes by rank (64-B walk)
   float4* d_wide_tris = nullptr;
   int* d_wide_rank_of = nullptr;
+  // the 8-wide layout (PT_OPT_WIDE_NODE 80): nodes, triangle records and
+  // leaf boxes by leaf position, position -> rank, slot -> position
+  float4* d_w8 = nullptr;
+  float4* d_w8_tris = nullptr;
+  float4* d_w8_leafbox = nullptr;
+  int* d_w8_pos_rank = nullptr;
+  int* d_w8_pos_of = nullptr;
+  int n_w8 = 0, w8_stack = 0;
   int2* d_wide_ovf = nullptr;
   long long wide_ovf_lanes = 0;
   int wide_ovf_stack = 0;   // the stack bound d_wide_ovf was sized for
@@ -818,6 +826,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.wf_fuse = 0;
   p.wide_qn = 0;
   p.wide_leafbox = nullptr;
+  p.wide_pos_rank = nullptr;
   p.nodes = c->stats_mode ? c->d_nodes_full : c->d_nodes;
   p.tris = c->d_tris;
   p.hit_tris = c->d_tris;
@@ -996,24 +1005,36 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     } else if (c->opt_wide && c->n_wide > 0 && !lds) {
       const long long lanes = ptd::wide_trace_lanes();
       if (lanes <= 0) return fail(PT_ERR_HIP, "wide walk: occupancy query failed");
-      if (lanes > c->wide_ovf_lanes || c->wide_stack > c->wide_ovf_stack) {   // every lane of the grid gets its area
+      const bool w8 = c->opt_wide_node == 80 && c->n_w8 > 0;
+      const int stack = w8 ? c->w8_stack : c->wide_stack;
+      if (lanes > c->wide_ovf_lanes || stack > c->wide_ovf_stack) {   // every lane of the grid gets its area
         { const int rc_ = quiesce(c); if (rc_) return rc_; }
         dev_free(c->d_wide_ovf);
         c->wide_ovf_lanes = 0;
         // two sets: the two halves of a chunk trace concurrently (launch_wavefront)
-        PT_HIP(hipMalloc((void**)&c->d_wide_ovf, 2 * (size_t)lanes * (size_t)c->wide_stack * sizeof(int2)));
+        PT_HIP(hipMalloc((void**)&c->d_wide_ovf, 2 * (size_t)lanes * (size_t)stack * sizeof(int2)));
         c->wide_ovf_lanes = lanes;
-        c->wide_ovf_stack = c->wide_stack;
+        c->wide_ovf_stack = stack;
       }
-      p.wide_qn = c->opt_wide_node == 64 ? 1 : 0;
-      p.wide = p.wide_qn ? c->d_wide_q : c->d_wide;
-      p.wide_leafbox = c->d_wide_leafbox;
-      p.wide_tris = c->d_wide_tris;
-      p.wide_rank_of = c->d_wide_rank_of;
-      p.hit_tris = c->d_wide_tris;   // closest hits come back as ranks
+      if (w8) {   // closest hits come back as leaf positions
+        p.wide_qn = 2;
+        p.wide = c->d_w8;
+        p.wide_leafbox = c->d_w8_leafbox;
+        p.wide_tris = c->d_w8_tris;
+        p.wide_rank_of = c->d_w8_pos_of;
+        p.wide_pos_rank = c->d_w8_pos_rank;
+        p.hit_tris = c->d_w8_tris;
+      } else {    // ... as ranks
+        p.wide_qn = c->opt_wide_node == 64 ? 1 : 0;
+        p.wide = p.wide_qn ? c->d_wide_q : c->d_wide;
+        p.wide_leafbox = c->d_wide_leafbox;
+        p.wide_tris = c->d_wide_tris;
+        p.wide_rank_of = c->d_wide_rank_of;
+        p.hit_tris = c->d_wide_tris;
+      }
       p.wide_ovf = c->d_wide_ovf;
       p.wide_ovf_lanes = c->wide_ovf_lanes;
-      p.wide_stack = c->wide_stack;
+      p.wide_stack = stack;
       p.wide_handback = c->opt_wide == 2 ? 1 : 0;
       // fused shadow walks: hit records carry the rank in 29 bits
       p.wf_fuse = c->opt_wf_fuse && c->n_tris <= ptd::kHitRankMask && c->n_lights > 0 ? 1 : 0;
@@ -1104,6 +1125,11 @@ int pt_destroy(pt_context* c) {
   dev_free(c->d_wide_leafbox);
   dev_free(c->d_wide_tris);
   dev_free(c->d_wide_rank_of);
+  dev_free(c->d_w8);
+  dev_free(c->d_w8_tris);
+  dev_free(c->d_w8_leafbox);
+  dev_free(c->d_w8_pos_rank);
+  dev_free(c->d_w8_pos_of);
   dev_free(c->d_wide_ovf);
   dev_free(c->d_tris);
   dev_free(c->d_lights);
@@ -1189,6 +1215,11 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   dev_free(c->d_wide_leafbox);
   dev_free(c->d_wide_tris);
   dev_free(c->d_wide_rank_of);
+  dev_free(c->d_w8);
+  dev_free(c->d_w8_tris);
+  dev_free(c->d_w8_leafbox);
+  dev_free(c->d_w8_pos_rank);
+  dev_free(c->d_w8_pos_of);
   dev_free(c->d_tris);
   // the wide walk's overflow area is sized by the scene's stack bound: a
   // deeper tree needs a new one (it is reallocated at the next wide launch)
@@ -1196,6 +1227,7 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   c->wide_ovf_lanes = 0;
   c->wide_ovf_stack = 0;
   c->n_wide = 0;
+  c->n_w8 = 0;
   c->has_scene = false;
   const int T = (int)(n_indices / 3);
   struct Staging {   // vertex/index copies live only until the triangle records are built
@@ -1242,9 +1274,37 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
     PT_HIP(hipMemcpyAsync(c->d_wide_rank_of, rank_of_host.data(), (size_t)T * sizeof(int), hipMemcpyHostToDevice,
                           c->stream));
   }
+  std::vector<int> pos_slot, pos_of_host;
+  const bool w8 = wide_reason.empty() && wide.w8_reason.empty();
+  if (w8) {
+    pos_slot.resize((size_t)T);
+    pos_of_host.resize((size_t)T);
+    for (int q = 0; q < T; ++q) {
+      pos_slot[q] = wide.rank_tri[wide.w8_pos_rank[q]];
+      pos_of_host[pos_slot[q]] = q;
+    }
+    PT_HIP(hipMalloc((void**)&c->d_w8, wide.w8nodes.size() * sizeof(float)));
+    PT_HIP(hipMalloc((void**)&c->d_w8_leafbox, wide.w8_leaf_box.size() * sizeof(float)));
+    PT_HIP(hipMalloc((void**)&c->d_w8_pos_rank, (size_t)T * sizeof(int)));
+    PT_HIP(hipMalloc((void**)&c->d_w8_pos_of, (size_t)T * sizeof(int)));
+    PT_HIP(hipMalloc((void**)&c->d_w8_tris, (size_t)T * 3 * sizeof(float4)));
+    PT_HIP(hipMemcpyAsync(c->d_w8, wide.w8nodes.data(), wide.w8nodes.size() * sizeof(float), hipMemcpyHostToDevice,
+                          c->stream));
+    PT_HIP(hipMemcpyAsync(c->d_w8_leafbox, wide.w8_leaf_box.data(), wide.w8_leaf_box.size() * sizeof(float),
+                          hipMemcpyHostToDevice, c->stream));
+    PT_HIP(hipMemcpyAsync(c->d_w8_pos_rank, wide.w8_pos_rank.data(), (size_t)T * sizeof(int), hipMemcpyHostToDevice,
+                          c->stream));
+    // position -> slot first (the gather's map), then slot -> position
+    PT_HIP(hipMemcpyAsync(c->d_w8_pos_of, pos_slot.data(), (size_t)T * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    PT_HIP(ptd::launch_gather_tris(c->d_tris, c->d_w8_pos_of, T, c->d_w8_tris, c->stream));
+    PT_HIP(hipMemcpyAsync(c->d_w8_pos_of, pos_of_host.data(), (size_t)T * sizeof(int), hipMemcpyHostToDevice,
+                          c->stream));
+  }
   PT_HIP(hipStreamSynchronize(c->stream));
   c->n_wide = wide_reason.empty() ? wide.n_nodes : 0;
   c->wide_stack = wide.stack_cap;
+  c->n_w8 = w8 ? wide.w8_n_nodes : 0;
+  c->w8_stack = w8 ? wide.w8_stack_cap : 0;
   c->wide_reason = wide_reason;
   c->n_nodes = (int)(collapsed.size() / 2) - 1;
   c->n_nodes_full = (int)(threaded.size() / 2) - 1;
@@ -1520,7 +1580,8 @@ int pt_set_option(pt_context* c, int key, int value) {
       c->opt_wide = value;
       return PT_OK;
     case PT_OPT_WIDE_NODE:
-      if (value != 64 && value != 128) return fail(PT_ERR_INVALID, "PT_OPT_WIDE_NODE takes 64 or 128");
+      if (value != 64 && value != 80 && value != 128)
+        return fail(PT_ERR_INVALID, "PT_OPT_WIDE_NODE takes 64, 80 or 128");
       c->opt_wide_node = value;
       return PT_OK;
     case PT_OPT_WF_FUSE:

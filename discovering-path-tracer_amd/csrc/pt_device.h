@@ -88,9 +88,10 @@ struct RenderParams {
   // by leaf rank, triangle slot -> rank, per-lane stack overflow areas
   // (wide_ovf_lanes lanes of wide_stack entries, lane-strided)
   const float4* hit_tris;   // the records a closest hit's index refers to: wide_tris (by rank) with the wide walk, else tris
-  const float4* wide;        // 64-B nodes when wide_qn, else 128-B (wide_walk.h)
+  const float4* wide;        // 64-B nodes when wide_qn 1, 80-B 8-wide nodes when 2, else 128-B (wide_walk.h)
   int wide_qn;
-  const float4* wide_leafbox;   // wide_qn: the reference's leaf box per rank, 2 float4
+  const float4* wide_leafbox;   // wide_qn: the reference's leaf box per rank (8-wide: per position), 2 float4
+  const int* wide_pos_rank;     // wide_qn 2: leaf position -> rank (exact ties); the indices below are positions
   const float4* wide_tris;
   const int* wide_rank_of;
   int2* wide_ovf;

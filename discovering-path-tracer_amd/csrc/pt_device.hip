@@ -2226,9 +2226,12 @@ __device__ __forceinline__ int fused_shadow_ray(const RenderParams& P, v3 o, v3 
 }
 constexpr int kFuseWalk = 16;   // lane state: walking the fused shadow ray
 
-template <int G, bool CNT = false, bool QN = true>
+// LAYOUT: 0 128-B 4-wide nodes, 1 64-B 4-wide nodes (QN), 2 80-B 8-wide
+// nodes (w8_step; leaf indices are positions, ties go by pos_rank)
+template <int G, bool CNT = false, int LAYOUT = 1>
 __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(RenderParams P, WfBuffers B,
                                                                                 int cur) {
+  constexpr bool QN = LAYOUT >= 1;
   const int tid = (int)threadIdx.x;
   if (blockIdx.x == 0 && tid == 0) B.counters[cur ^ 1] = 0;   // filled by the shading that follows
   const int count = B.counters[cur];
@@ -2293,6 +2296,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
     for (int it = 0; it < PT_WF_STEPS; ++it) {
       bool exact = false;
       if (!PT_WIDE_QUEUE) {
+        static_assert(!PT_WIDE_QUEUE ? LAYOUT != 2 : true, "the 8-wide walk runs with PT_WIDE_QUEUE");
         if (p >= 0 && wide_step<CNT, false, QN>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact,
                                                 &c.nodes, &c.leaves, nullptr, P.wide_leafbox)) {
           int res;
@@ -2304,9 +2308,14 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
         }
       } else {
         // fin: the walk has no node left (its queue may still hold candidates)
-        if (p >= 0 && !fin)
-          fin = wide_step<CNT, true, QN>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
-                                         &c.leaves, cand, P.wide_leafbox);
+        if (p >= 0 && !fin) {
+          if (LAYOUT == 2)
+            fin = w8_step<CNT, true>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
+                                     &c.leaves, cand, P.wide_leafbox, P.wide_pos_rank);
+          else
+            fin = wide_step<CNT, true, QN>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
+                                           &c.leaves, cand, P.wide_leafbox);
+        }
         if (exact) {
           R.nc = 0;
           // a fused shadow ray the walk cannot take goes to the shading's next round
@@ -2335,7 +2344,9 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
 #endif
         if (__ballot(p >= 0 && R.nc > kWideQ - 4) || (int)__popcll(waiting) >= PT_WIDE_FLUSH_T ||
             (waiting && __ballot(p >= 0 && !fin) == 0ull)) {
-          if (p >= 0 && R.nc > 0 && wide_flush<CNT, QN>(R, P.wide_tris, cand, &c.leaves, P.wide_leafbox)) {
+          if (p >= 0 && R.nc > 0 &&
+              wide_flush<CNT, QN>(R, P.wide_tris, cand, &c.leaves, P.wide_leafbox,
+                                  LAYOUT == 2 ? P.wide_pos_rank : nullptr)) {
             fin = true;   // occluded
             R.sp = 0;
             R.cur = -1;
@@ -2650,8 +2661,9 @@ long long wide_trace_lanes() {
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
   int most = 0;
-  for (auto k : {wf_trace_wide_kernel<kWideG, false, true>, wf_trace_wide_kernel<kWideG, true, true>,
-                 wf_trace_wide_kernel<kWideG, false, false>, wf_trace_wide_kernel<kWideG, true, false>}) {
+  for (auto k : {wf_trace_wide_kernel<kWideG, false, 2>, wf_trace_wide_kernel<kWideG, true, 2>,
+                 wf_trace_wide_kernel<kWideG, false, 1>, wf_trace_wide_kernel<kWideG, true, 1>,
+                 wf_trace_wide_kernel<kWideG, false, 0>, wf_trace_wide_kernel<kWideG, true, 0>}) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess) return 0;
     most = std::max(most, per_cu);
   }
@@ -2692,8 +2704,9 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
                 : (g2 ? wf_trace_pairs_kernel<2> : wf_trace_pairs_kernel<4>);
   const bool wide = p0.wide && !lds_scene && !p0.pairs;
   if (wide)   // culled wide walk (PT_OPT_WIDE, default)
-    trace = p0.wide_qn ? (cnt ? wf_trace_wide_kernel<kWideG, true, true> : wf_trace_wide_kernel<kWideG, false, true>)
-                       : (cnt ? wf_trace_wide_kernel<kWideG, true, false> : wf_trace_wide_kernel<kWideG, false, false>);
+    trace = p0.wide_qn == 2 ? (cnt ? wf_trace_wide_kernel<kWideG, true, 2> : wf_trace_wide_kernel<kWideG, false, 2>)
+            : p0.wide_qn ? (cnt ? wf_trace_wide_kernel<kWideG, true, 1> : wf_trace_wide_kernel<kWideG, false, 1>)
+                         : (cnt ? wf_trace_wide_kernel<kWideG, true, 0> : wf_trace_wide_kernel<kWideG, false, 0>);
   size_t lds_t = lds;
   if (p0.pairs && !lds_scene) lds_t = (size_t)4 * 64 * p0.pair_depth * sizeof(int);   // the walk stacks
   if (wide) lds_t = 0;

@@ -849,7 +849,7 @@ def _wide_case(case):
     return v, i, scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, False
 
 
-@pytest.mark.parametrize("node", [64, 128])
+@pytest.mark.parametrize("node", [64, 80, 128])
 @pytest.mark.parametrize("build", [1, 0], ids=["sah", "reference_tree"])
 @pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("case", ["sphere", "cloud_int_bits", "dense_cloud", "grid2lights", "box"])
@@ -858,7 +858,7 @@ def test_wide_walk_matches_oracle(case, mode, build, node):
     oracle's frame bit for bit, over either grouping of the reference's leaves
     (PT_OPT_WIDE_BUILD: binned SAH, or the reference's own tree) and either
     node layout (PT_OPT_WIDE_NODE: 64-B nodes with grid-rounded boxes and
-    exact leaf tests, or float boxes); mode 2 hands every odd ray of each
+    exact leaf tests, 80-B 8-wide nodes likewise, or float boxes); mode 2 hands every odd ray of each
     round to the exact threaded walk in the shading kernel (the path rays
     with a zero direction component take)."""
     sv, si, cam, lights, int_bits = _wide_case(case)
