@@ -2186,6 +2186,9 @@ __global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_ker
 #define PT_WIDE_REFILL 24
 #endif
 constexpr int kWideG = PT_WIDE_G;
+#ifndef PT_WIDE_DEFER_DONE
+#define PT_WIDE_DEFER_DONE 1
+#endif
 #ifndef PT_WIDE_FLUSH_T
 #define PT_WIDE_FLUSH_T 1
 #endif
@@ -2257,7 +2260,50 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
   int fz = 0, cr = 0;
   uint32_t aux = 0u;
   Ctr c = {0u, 0u, 0u, 0u, 0u};
+  // A lane whose walk is over (fin, queue empty): its answer goes to the
+  // hit list -- or, after a closest hit whose first-light shadow ray the
+  // trace kernel walks (PT_OPT_WF_FUSE), that ray starts in the lane.
+  auto finish = [&]() {
+    float t = R.lim;
+    int res = R.best;   // occluded, or the hit's rank (hit_tris = wide_tris; the record the flush just tested)
+    bool done = true;
+    if (fz & kFuseWalk) {   // the fused shadow ray's answer joins its closest hit
+      t = __uint_as_float(aux);
+      res = cr | kHitFused | (R.best ? kHitOccluded : 0);
+    } else if ((fz & kRayFuse) && R.best >= 0) {
+      v3 so, sd;
+      float lim;
+      const int k = fused_shadow_ray(P, R.o, R.d, R.lim, R.best, (fz & kRayPrimary) != 0, aux, &so, &sd, &lim);
+      if (k == 1) {
+        res = R.best | kHitFused;   // unoccluded without a walk
+      } else if (k == 2) {
+        cr = R.best;
+        aux = __float_as_uint(R.lim);
+        wide_start(R, so, sd, true, lim);
+        if (wide_ray_ok(R.o, R.d, R.inv)) {   // walk it in this lane now
+          fz = kFuseWalk;
+          fin = false;
+          done = false;
+          if (CNT) ++c.srays;
+        } else {   // the shading's next round hands it to the exact walk
+          t = __uint_as_float(aux);
+          res = cr;
+        }
+      }
+    }
+    if (done) {
+      B.hits[p] = make_float2(t, __int_as_float(res));
+      p = -1;
+      fin = false;
+      fz = 0;
+    }
+  };
   for (;;) {
+    // PT_WIDE_DEFER_DONE: the lanes whose walks ended since the last check
+    // finish here together, not in the step their walk ended in (where the
+    // wave ran the finishing code -- the fused shadow ray's light sample,
+    // normalisations and start -- for one or two lanes at a time)
+    if (PT_WIDE_DEFER_DONE && p >= 0 && fin && R.nc == 0) finish();
     const unsigned long long idle = __ballot(p < 0);
     unsigned long long gm = idle;
 #pragma unroll
@@ -2352,41 +2398,9 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
             R.cur = -1;
           }
         }
-        if (p >= 0 && fin && R.nc == 0) {
-          float t = R.lim;
-          int res = R.best;   // occluded, or the hit's rank (hit_tris = wide_tris; the record the flush just tested)
-          bool done = true;
-          if (fz & kFuseWalk) {   // the fused shadow ray's answer joins its closest hit
-            t = __uint_as_float(aux);
-            res = cr | kHitFused | (R.best ? kHitOccluded : 0);
-          } else if ((fz & kRayFuse) && R.best >= 0) {
-            v3 so, sd;
-            float lim;
-            const int k = fused_shadow_ray(P, R.o, R.d, R.lim, R.best, (fz & kRayPrimary) != 0, aux, &so, &sd, &lim);
-            if (k == 1) {
-              res = R.best | kHitFused;   // unoccluded without a walk
-            } else if (k == 2) {
-              cr = R.best;
-              aux = __float_as_uint(R.lim);
-              wide_start(R, so, sd, true, lim);
-              if (wide_ray_ok(R.o, R.d, R.inv)) {   // walk it in this lane now
-                fz = kFuseWalk;
-                fin = false;
-                done = false;
-                if (CNT) ++c.srays;
-              } else {   // the shading's next round hands it to the exact walk
-                t = __uint_as_float(aux);
-                res = cr;
-              }
-            }
-          }
-          if (done) {
-            B.hits[p] = make_float2(t, __int_as_float(res));
-            p = -1;
-            fin = false;
-            fz = 0;
-          }
-        }
+        if (!PT_WIDE_DEFER_DONE && p >= 0 && fin && R.nc == 0) finish();
+        // every lane idle or done (PT_WIDE_DEFER_DONE): back to the refill check
+        if (PT_WIDE_DEFER_DONE && __ballot(p >= 0 && !(fin && R.nc == 0)) == 0ull) break;
       }
     }
   }

@@ -168,3 +168,22 @@ def test_negative_zero_is_the_additive_identity():
     assert np.array_equal(s.view(np.uint32), x.view(np.uint32))
     # +0 is not: -0 + +0 = +0
     assert (np.float32(-0.0) + np.float32(0.0)).view(np.uint32) == 0
+
+
+def test_rccl_standin_exports_the_entry_points_pt_dist_resolves():
+    """tests/dist_shim.cpp (loaded by libptamd through PT_RCCL_LIB in the
+    two-process GPU test of pt_dist_run) defines every RCCL entry point
+    rccl_api() resolves (pt_api.cpp), and libptamd names that variable."""
+    import ctypes
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    so = os.path.join(root, "tests", "_build", "libptdistshim.so")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(root, "tests")])
+    lib = ctypes.CDLL(so)
+    for name in ("ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclCommAbort", "ncclGroupStart",
+                 "ncclGroupEnd", "ncclSend", "ncclRecv", "ncclGetErrorString"):
+        assert hasattr(lib, name), name
+    api = open(os.path.join(root, "discovering-path-tracer_amd", "csrc", "pt_api.cpp")).read()
+    assert 'getenv("PT_RCCL_LIB")' in api
+    uid = ctypes.create_string_buffer(128)
+    assert lib.ncclGetUniqueId(uid) == 0 and uid.value.startswith(b"/ptshim-")
