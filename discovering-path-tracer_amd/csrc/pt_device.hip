@@ -1740,6 +1740,9 @@ __device__ __forceinline__ bool pixel_live(const RenderParams& P, float ndcX0, f
   return live;
 }
 
+#ifndef PT_WF_GEN_BLOCK_SLOTS
+#define PT_WF_GEN_BLOCK_SLOTS 1
+#endif
 // Ray generation + shading up to the primary trace (path_step from PH_BEGIN).
 template <bool CNT>
 __global__ __launch_bounds__(256) void wf_gen_kernel(RenderParams P, WfBuffers B, long long n, long long g0) {
@@ -1772,7 +1775,29 @@ __global__ __launch_bounds__(256) void wf_gen_kernel(RenderParams P, WfBuffers B
       if (!need) B.colors[g] = make_float4(col.x, col.y, col.z, 1.0f);
     }
   }
-  const int slot = wave_slot(&B.counters[0], need);
+  // list slots: one atomic per workgroup (PT_WF_GEN_BLOCK_SLOTS) instead of
+  // one per wave -- the generation is otherwise short, and every wave of the
+  // launch adding to the same counter queued on that one address
+  int slot;
+  if (PT_WF_GEN_BLOCK_SLOTS) {
+    __shared__ int wave_n[4], wave_base[4];
+    const unsigned long long m = __ballot(need);
+    const int w = (int)threadIdx.x >> 6, lane = (int)threadIdx.x & 63;
+    if (lane == 0) wave_n[w] = (int)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int tot = wave_n[0] + wave_n[1] + wave_n[2] + wave_n[3];
+      const int base = tot ? atomicAdd(&B.counters[0], tot) : 0;
+      wave_base[0] = base;
+      wave_base[1] = base + wave_n[0];
+      wave_base[2] = base + wave_n[0] + wave_n[1];
+      wave_base[3] = base + wave_n[0] + wave_n[1] + wave_n[2];
+    }
+    __syncthreads();
+    slot = wave_base[w] + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  } else {
+    slot = wave_slot(&B.counters[0], need);
+  }
   if (need) {
     wf_push(B, 0, slot, (int)g, T, fuse_bits(P, S, T), S.rng);
     wf_store_state(B, 0, slot, S);
@@ -2183,7 +2208,7 @@ __global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_ker
 // refill threshold of the wide walk: 24 idle lanes (sphere -0.9 %, 10M cloud
 // -0.35 % against 32, repeated; 16: +3 %)
 #ifndef PT_WIDE_REFILL
-#define PT_WIDE_REFILL 24
+#define PT_WIDE_REFILL 16
 #endif
 constexpr int kWideG = PT_WIDE_G;
 #ifndef PT_WIDE_DEFER_DONE
