@@ -56,6 +56,8 @@ def lib():
         L.wide_dump8.argtypes = [F32P, sz, U32P, sz, F32P, sz, ctypes.c_int, F32P, sz, I32P, F32P, ctypes.c_char_p,
                                  sz]
         L.wide_dump8.restype = ctypes.c_longlong
+        L.wide_counts.argtypes = [F32P, sz, U32P, sz, F32P, sz, ctypes.c_int, F32P, sz, I32P, I32P, ctypes.c_char_p,
+                                  sz]
         _LIB = L
     return _LIB
 

@@ -263,6 +263,40 @@ int wide_check(const float* V, size_t nvf, const uint32_t* I, size_t nt, const f
   return 0;
 }
 
+// Per-ray work of the configured walk: nodes[i] node visits and tris[i]
+// triangle tests of ray i (rays as for wide_check; -1 for a hand-back).
+int wide_counts(const float* V, size_t nvf, const uint32_t* I, size_t nt, const float* N, size_t nn, int int_bits,
+                const float* rays, size_t n, int32_t* nodes, int32_t* tris, char* err, size_t errlen) {
+  Built b;
+  const std::string why = build(V, nvf, I, nt, N, nn, int_bits, &b);
+  if (!why.empty()) {
+    snprintf(err, errlen, "%s", why.c_str());
+    return 1;
+  }
+  std::vector<int2> lds(kWideLds), ovf((size_t)std::max(b.w.stack_cap, b.w.w8_stack_cap) + 1);
+  for (size_t i = 0; i < n; ++i) {
+    const float* r = rays + 8 * i;
+    WideRay R;
+    wide_start(R, mk(r[0], r[1], r[2]), mk(r[3], r[4], r[5]), r[6] != 0.0f, r[7]);
+    bool exact = !wide_ray_ok(R.o, R.d, R.inv);
+    uint32_t cn = 0, cl = 0;
+    if (!exact) {
+      if (g_node == 80)
+        g_queue ? walk8<true>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl)
+                : walk8<false>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl);
+      else if (g_node == 64)
+        g_queue ? walk<true, true>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl)
+                : walk<true, false>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl);
+      else
+        g_queue ? walk<false, true>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl)
+                : walk<false, false>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl);
+    }
+    nodes[i] = exact ? -1 : (int32_t)cn;
+    tris[i] = exact ? -1 : (int32_t)cl;
+  }
+  return 0;
+}
+
 // The per-triangle cull coefficients (wide_tri_coeffs) {k1, k2, eps0, eps1}
 // and the node constants {c1, E0, E1, 0} a node over that one triangle gets.
 int wide_coeffs(const float* e1, const float* e2, double* co, float* node) {
