@@ -30,9 +30,13 @@ effective_GBps: on box.obj the scene is staged in LDS, so that figure is far
 above the HBM peak and is not a bandwidth.
 
 At N = 1 the line also carries `configs`: config 3 (the level-6 displaced
-icosphere standing in for the missing Sylveon.obj) and config 5 (10M random
-triangles) at 1920x1080x8spp, each timed, counted and roofline-priced the
-same way (--no-scene-legs skips them).
+icosphere standing in for the missing Sylveon.obj) at 1920x1080x8spp,
+config 4 (the same mesh at 3840x2160x16spp, 8 bounces) and config 5 (10M
+random triangles, 1920x1080x8spp), each timed, counted and roofline-priced
+the same way.  At N > 1 `configs` holds configs 4 and 5 split across the N
+GPUs (screen tiles, RCCL SUM reduce of the accumulation buffer), each
+checked bitwise against a one-GPU render of the same frame on rank 0
+(--no-scene-legs skips the legs).
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
 torch.distributed.run, one process per GPU.  Rank 0 prints one JSON line.
@@ -66,6 +70,12 @@ def algorithmic_bytes(st):
     return 32 * st["nodes"] + 48 * st["leaf_tests"] + 32 * st["samples"]
 
 
+def build_threads():
+    """Host threads for one process's BVH build: its usable CPUs shared by
+    the processes of this node (LOCAL_WORLD_SIZE ranks build at once)."""
+    return max(1, cpu_threads() // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1"))))
+
+
 def load_scene(name):
     import ptamd
     import scenes
@@ -74,14 +84,14 @@ def load_scene(name):
         return s, scenes.DEFAULT_CAMERA, False, "box.obj, camera (0,0,5) fov 60"
     if name == "sphere":
         v, i = scenes.displaced_sphere(6)
-        s = ptamd.Scene.from_arrays(v, i).build_bvh()
+        s = ptamd.Scene.from_arrays(v, i).build_bvh(threads=build_threads())
         return (s, scenes.camera((0.0, 0.5, 3.0)), False,
                 f"displaced icosphere ({i.size // 3} tris, Sylveon substitute), camera (0,0.5,3) fov 60")
     if name.startswith("synthetic:"):
         t = int(name.split(":")[1])
         v, i = scenes.random_triangles(t, seed=42)
         big = 2 * t - 1 >= (1 << 24)
-        s = ptamd.Scene.from_arrays(v, i).build_bvh(int_bits=big)
+        s = ptamd.Scene.from_arrays(v, i).build_bvh(int_bits=big, threads=build_threads())
         return s, scenes.camera((0.0, 0.0, 2.2)), big, f"synthetic {t} random triangles, camera (0,0,2.2) fov 60"
     raise SystemExit(f"unknown scene {name}")
 
@@ -357,6 +367,133 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
     return out
 
 
+# the BASELINE configs that name a multi-GPU run (configs[3]: the Sylveon
+# substitute at 4K 16 spp D8 tile-split with an RCCL accumulation reduce;
+# configs[4]: the 10M cloud's 8-GPU report), timed at N > 1 beside the box
+DIST_SCENE_LEGS = (("config4", "sphere", 3840, 2160, 16, 8, 3),
+                   ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5))
+
+
+def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, depth, sss, steps):
+    """One multi-GPU BASELINE config at N = world: every rank renders its
+    screen tiles (pt_set_partition) of the frame with the kernel the library
+    picks for its share, then one RCCL SUM reduce of the accumulation buffer
+    to rank 0 (owned pixels +0-cleared, the others -0: the sum is bit-exact,
+    DESIGN §5).  `steps` frames after one warmup, each bracketed by barrier +
+    synchronize on every rank, the median of the per-frame max over ranks.
+    Rank 0 then renders the whole frame alone with the same context and
+    checks the reduced frame against it bit for bit.  Returns the leg's dict
+    on rank 0 (None elsewhere), or {"error": ...} if any rank failed its
+    setup (then no rank runs a collective of the leg)."""
+    import ptamd
+    import scenes
+    import torch
+    t_setup = time.perf_counter()
+    dev = torch.device("cuda", device)
+    coll = dev if backend == "nccl" else "cpu"
+    err = ""
+    r = None
+    try:
+        scene, cam, int_bits, desc = load_scene(scene_name)
+        v, i, n, _, _ = scene.arrays()
+        del scene
+        r = ptamd.Renderer(device)
+        r.upload_scene(v, i, n, int_bits=int_bits)
+        ntri = i.size // 3
+        del v, i, n
+        r.upload_lights(scenes.REFERENCE_LIGHT)
+        r.set_camera(cam)
+        r.set_params(depth, sss)
+        stream = torch.cuda.Stream(dev)
+        torch.cuda.set_stream(stream)
+        r.set_stream(stream.cuda_stream)
+        r.set_partition(world, rank)
+        frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+        r.bind_accum(frame.data_ptr(), W, H)
+    except Exception as e:   # noqa: BLE001 -- reported in the line, never a hang of the other ranks
+        err = f"rank {rank}: {type(e).__name__}: {e}"
+    ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=coll)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        if err:
+            print(f"bench: {scene_name} leg: {err}", file=sys.stderr, flush=True)
+        return {"error": err or "another rank failed its setup"} if rank == 0 else None
+    setup_s = time.perf_counter() - t_setup
+
+    def reduce_sum(t):
+        if backend == "nccl":
+            dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+        else:
+            c = t.cpu()
+            dist.reduce(c, dst=0, op=dist.ReduceOp.SUM)
+            if rank == 0:
+                t.copy_(c)
+
+    def allreduce(vals, op):
+        t = torch.tensor(np.asarray(vals, np.float64), dtype=torch.float64, device=coll)
+        dist.all_reduce(t, op=op)
+        return t.cpu().numpy()
+
+    # reference traceRay calls of the whole frame: each rank counts its share
+    t0 = time.perf_counter()
+    mine, traced = reference_and_traced_counts(r, spp)
+    ref = allreduce(mine, dist.ReduceOp.SUM)
+    traced = dict(zip(TRACED_KEYS, (int(x) for x in allreduce([traced[k] for k in TRACED_KEYS],
+                                                                 dist.ReduceOp.SUM))))
+    counts_s = time.perf_counter() - t0
+
+    def frame_once():
+        r.clear()          # +0 owned, -0 elsewhere
+        r.render(0, spp)
+        reduce_sum(frame)
+
+    frame_once()           # warmup
+    torch.cuda.synchronize(dev)
+    walls, own = [], []
+    for _ in range(steps):
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        r.reset_launch_times()
+        t0 = time.perf_counter()
+        frame_once()
+        r.synchronize()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        walls.append((time.perf_counter() - t0) * 1e3)
+        kt = r.launch_times_ms()
+        own.append(float(np.sum(kt)) if kt.size else float("nan"))
+    wmax = allreduce(walls, dist.ReduceOp.MAX)
+    kmax = allreduce(own, dist.ReduceOp.MAX)
+    kmin = allreduce(own, dist.ReduceOp.MIN)
+    out = None
+    if rank == 0:
+        got = frame.cpu().numpy().reshape(-1).copy()
+        # the whole frame on this GPU alone, same context and kernels
+        r.set_partition(1, 0)
+        r.clear()
+        r.render(0, spp)
+        r.synchronize()
+        want = r.read_accum()
+        same = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+        dt = float(np.median(wmax)) * 1e-3
+        cfg = {"workload": f"{desc} {W}x{H} {spp}spp {depth} bounces {sss} sss", "triangles": int(ntri),
+               "int_bits_nodes": bool(int_bits), "rays_per_frame": int(ref[0]),
+               "parallelism": f"tiles{world}-reduce (RCCL SUM of the accumulation buffer to rank 0)"}
+        add_traced(cfg, traced, dt)
+        out = {"metric": "Mrays/s (reference-equivalent traceRay calls)", "value": round(ref[0] / dt / 1e6, 3),
+               "unit": "Mrays/s", "n_gpus": world, "ms_per_step": round(dt * 1e3, 2), "steps": steps, "warmup": 1,
+               "ms_per_frame": spread(wmax),
+               "rank_render_ms": {"max": spread(kmax), "min": spread(kmin),
+                                  "note": "each rank's render launches (HIP events), slowest and fastest rank"},
+               "kernel": KERNEL_NAMES.get(r.last_kernel(), "?"), "config": cfg,
+               "verified_bitwise_vs_single_gpu": same,
+               "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
+    del r
+    torch.cuda.synchronize(dev)
+    dist.barrier()
+    return out
+
+
 def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light, cam, depth, sss, coll_dev):
     """RCCL communicator for pt_dist_run and a 4-frame bitwise self-check on
     the root against a single-GPU render; None (every rank) if anything
@@ -466,7 +603,8 @@ def main():
                     help="N=1: also time the same steps with primary-ray culling off (reported as "
                          "primary_cull_off); default on for the box headline at N=1")
     ap.add_argument("--no-scene-legs", action="store_true",
-                    help="N=1: skip the config-3 and config-5 legs (`configs` in the JSON line)")
+                    help="skip the scene legs (`configs` in the JSON line): configs 3, 4 and 5 on one GPU at "
+                         "N=1, configs 4 and 5 across the N GPUs at N>1")
     ap.add_argument("--profile-run", action="store_true",
                     help="only the warmup and timed frames (no stats/counting passes, legs or CPU baseline): "
                          "the command tools/gpu_*profile.sh runs under rocprofv3")
@@ -866,6 +1004,26 @@ def main():
             raise SystemExit(f"bench --verify: assembled frame differs from the single-GPU frame in {bad.size} "
                              f"floats; first at pixel {bad[0] // 4} ch {bad[0] % 4}: {got[bad[0]]} vs {want[bad[0]]}")
 
+    box_kernel = KERNEL_NAMES.get(r.last_kernel(), "?")
+    dist_legs = None
+    if dist is not None and default_cfg and not (args.no_scene_legs or args.profile_run):
+        # configs 4 and 5 across the same N GPUs (every rank takes part)
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        del r
+        dist_legs = {}
+        legs = DIST_SCENE_LEGS
+        if os.environ.get("PT_BENCH_DIST_LEGS"):
+            # smaller legs for the GPU tests: "key scene W H spp depth steps;..."
+            legs = [tuple(f if k < 2 else int(f) for k, f in enumerate(e.split()))
+                    for e in os.environ["PT_BENCH_DIST_LEGS"].split(";")]
+        for key, scene_name, lw, lh, lspp, ldepth, lsteps in legs:
+            if rank == 0:
+                print(f"bench: {key} leg on {world} GPUs ({scene_name} {lw}x{lh} {lspp}spp D{ldepth})",
+                      file=sys.stderr, flush=True)
+            dist_legs[key] = dist_scene_leg(dist, backend, device, world, rank, scene_name, lw, lh, lspp, ldepth,
+                                            SSS, lsteps)
+
     if rank == 0:
         ms_per_step = dt / args.steps * 1e3
         value = rays_per_frame * args.steps / dt / 1e6
@@ -900,7 +1058,7 @@ def main():
                        "rays_per_frame": None if rays_per_frame != rays_per_frame else int(rays_per_frame),
                        "primary_cull": True,
                        "msamples_per_s": round(W * H * SPP * args.steps / dt / 1e6, 3)},
-            "roofline": roofline_block(prof, roof_ms, own_bytes, KERNEL_NAMES.get(r.last_kernel(), "?"),
+            "roofline": roofline_block(prof, roof_ms, own_bytes, box_kernel,
                                        kernel_ms, interval_ms, int(kt.size),
                                        "launch_interval_ms (busy span / launches; launches overlap on "
                                        f"{args.streams} streams)" if args.streams > 1 else "kernel_ms"),
@@ -935,6 +1093,8 @@ def main():
             out_line["verified_bitwise_vs_single_gpu"] = verified
         if world == 1 and emu == 1 and not args.no_cpu_baseline and not args.profile_run:
             out_line["cpu_baseline"] = cpu_baseline(v, i, n, cam, light, W, H, SPP, DEPTH, SSS)
+        if dist_legs is not None:
+            out_line["configs"] = dist_legs
         if world == 1 and emu == 1 and default_cfg and not (args.no_scene_legs or args.profile_run or args.packed):
             del r
             out_line["configs"] = {}

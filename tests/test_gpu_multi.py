@@ -34,7 +34,7 @@ def test_two_rank_bench_verifies_bitwise(collective, extra):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2", "--verify",
-           "--collective", collective] + extra
+           "--no-scene-legs", "--collective", collective] + extra
     res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
     lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
@@ -80,10 +80,34 @@ def test_native_step_loop_two_ranks_grouped_send_recv(streams):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "3", "--verify",
-           "--streams", str(streams)]
+           "--no-scene-legs", "--streams", str(streams)]
     res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
     out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
     assert out["n_gpus"] == 2
     assert out["config"]["step_loop"] == "native (pt_dist_run, PT_RCCL_LIB stand-in)", res.stderr[-2000:]
     assert out["verified_bitwise_vs_single_gpu"] is True
+
+
+def test_two_rank_scene_legs_reduce_bitwise():
+    """bench.py's N > 1 scene legs (configs 4 and 5 across the GPUs, here at
+    reduced size): each rank renders its tiles of the large-scene frame on
+    the wavefront pipeline, one SUM reduce of the -0/+0-cleared
+    accumulators, and rank 0 checks the reduced frame bitwise against its own
+    whole-frame render.  The 2^24-node int encoding is exercised by the
+    full-size run (the driver's multi-GPU bench)."""
+    env = dict(os.environ, PT_BENCH_DEVICE="0", PT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1",
+               PT_BENCH_DIST_LEGS="config4 sphere 640 360 4 8 2;config5 synthetic:300000 480 270 2 4 2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1"]
+    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
+    out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
+    legs = out["configs"]
+    assert set(legs) == {"config4", "config5"}, legs
+    for key, leg in legs.items():
+        assert "error" not in leg, leg
+        assert leg["n_gpus"] == 2
+        assert leg["verified_bitwise_vs_single_gpu"] is True, key
+        assert leg["config"]["rays_per_frame"] > 0 and leg["config"]["rays_traced"] > 0
