@@ -386,6 +386,7 @@ struct pt_context {
   std::string wide_reason = "no scene";
   int opt_wide = 1;           // PT_OPT_WIDE
   int opt_wf_fuse = 1;        // PT_OPT_WF_FUSE
+  int opt_wf_tail = -1;       // PT_OPT_WF_TAIL (-1 auto)
   int opt_wide_node = 64;     // PT_OPT_WIDE_NODE
   int n_nodes_full = 0;
   float4* d_tris = nullptr;
@@ -824,6 +825,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.wide_stack = 0;
   p.wide_handback = 0;
   p.wf_fuse = 0;
+  p.wf_tail = 0;
   p.wide_qn = 0;
   p.wide_leafbox = nullptr;
   p.wide_pos_rank = nullptr;
@@ -1038,6 +1040,15 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
       p.wide_handback = c->opt_wide == 2 ? 1 : 0;
       // fused shadow walks: hit records carry the rank in 29 bits
       p.wf_fuse = c->opt_wf_fuse && c->n_tris <= ptd::kHitRankMask && c->n_lights > 0 ? 1 : 0;
+      // wf_tail_kernel (4-wide layouts).  Auto: a list of < 2^20 rays when the
+      // scene is below 2^20 triangles (its tree cache-resident, walks short)
+      // and the launch holds at most 2^22 paths (a few rays per traversal lane
+      // per round, so each round's drain dominates).  Emulated 1/8 tile share
+      // of config 3 (2M paths): 14.9 -> 12.4 ms; 1/8 shares of config 4 (16.6M
+      // paths) and of the 10M cloud: +2 % (not taken); whole frames: +-0.3 %.
+      const long long paths = std::min(chunk_paths, items * (256 / p.spl) * (long long)n_batches);
+      const int tail_auto = c->n_tris < (1 << 20) && paths <= (1ll << 22) ? (1 << 20) : 0;
+      p.wf_tail = w8 ? 0 : c->opt_wf_tail >= 0 ? c->opt_wf_tail : tail_auto;
     }
     if (c->opt_wf_streams == 2 && !c->wf_stream2) {
       PT_HIP(hipStreamCreateWithFlags(&c->wf_stream2, hipStreamNonBlocking));
@@ -1587,6 +1598,10 @@ int pt_set_option(pt_context* c, int key, int value) {
     case PT_OPT_WF_FUSE:
       if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_WF_FUSE takes 0 or 1");
       c->opt_wf_fuse = value;
+      return PT_OK;
+    case PT_OPT_WF_TAIL:
+      if (value < -1) return fail(PT_ERR_INVALID, "PT_OPT_WF_TAIL takes -1 (auto) or a ray count >= 0");
+      c->opt_wf_tail = value;
       return PT_OK;
     case PT_OPT_WF_STREAMS:
       if (value != 1 && value != 2) return fail(PT_ERR_INVALID, "PT_OPT_WF_STREAMS takes 1 or 2");

@@ -2263,7 +2263,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
   const int tid = (int)threadIdx.x;
   if (blockIdx.x == 0 && tid == 0) B.counters[cur ^ 1] = 0;   // filled by the shading that follows
   const int count = B.counters[cur];
-  if (count == 0) return;
+  if (count == 0 || count < P.wf_tail) return;   // PT_OPT_WF_TAIL: wf_tail_kernel finishes the list
   const int wave = tid >> 6, lane = tid & 63;
   __shared__ int2 stk[4][kWideLds][64];
   int2* lds = &stk[wave][0][lane];
@@ -2470,6 +2470,7 @@ constexpr int kWfBins = 16;
 __global__ __launch_bounds__(256, PT_WF_SHADE_MIN_BLOCKS) void wf_shade_kernel(RenderParams P, WfBuffers B, int cur) {
   if (blockIdx.x == 0 && threadIdx.x == 0) B.counters[2] = 0;   // the next traversal's cursor
   const int count = B.counters[cur];
+  if (count < P.wf_tail) return;   // PT_OPT_WF_TAIL: wf_tail_kernel has finished these paths
   CamFrame F = {};   // camera frame: used by PH_BEGIN only
   __shared__ int bin_cnt[kWfBins], bin_base[kWfBins], wg_base;
   __shared__ int cand_buf[4][kCand][64];   // exact walks of handed-back rays
@@ -2561,6 +2562,160 @@ __global__ __launch_bounds__(256, PT_WF_SHADE_MIN_BLOCKS) void wf_shade_kernel(R
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// PT_OPT_WF_TAIL: the last paths of a chunk in one launch.  Every ray round
+// of the pipeline ends when its longest walk ends, and a path needs a round
+// per ray it traces (up to 33 at MAX_DEPTH 4, 65 at 8).  Late rounds hold few
+// rays -- on a 1/8 tile share only a few per traversal lane from the start --
+// so each costs about one long walk's latency plus three launches while most
+// of the GPU idles.  Once a round's list holds fewer than P.wf_tail rays, this
+// kernel takes the whole list instead of the trace and shading kernels: each
+// lane claims a waiting path (its list slot) and runs it to the end -- walk
+// (the culled wide walk with the trace kernel's queued leaf tests and
+// wave-wide flushes), then path_step, then the next ray's walk in the same
+// lane -- and stores the path's colour; the lanes whose walks have ended
+// shade together at the check every PT_WF_STEPS steps, as the trace kernel
+// finishes its walks.  The path's state waits in its own list slot
+// (wf_store_state / wf_load_state) while the lane walks, so the walk keeps
+// the trace kernel's registers.  The rays, draws, float operations and their
+// order per path are those of the rounds (path_step on each returned hit,
+// null shadow queries answered unoccluded, rays the wide walk does not take
+// walked exactly): the image is bit-identical; the trace and shading kernels
+// of that round and every later round find nothing to do.  No fused shadow
+// walks here: path_step derives each shadow ray itself.
+#ifndef PT_WF_TAIL_MIN_BLOCKS
+#define PT_WF_TAIL_MIN_BLOCKS 4
+#endif
+static_assert(kCand <= kWideQ, "wf_tail_kernel runs its exact walks in the leaf queue's LDS");
+template <bool CNT, bool QN>
+__global__ __launch_bounds__(256, PT_WF_TAIL_MIN_BLOCKS) void wf_tail_kernel(RenderParams P, WfBuffers B, int cur) {
+  const int count = B.counters[cur];
+  if (count == 0 || count >= P.wf_tail) return;
+  const int tid = (int)threadIdx.x;
+  const int wave = tid >> 6, lane = tid & 63;
+  __shared__ int2 stk[4][kWideLds][64];
+  int2* lds = &stk[wave][0][lane];
+  __shared__ int cq[4][kWideQ][64];   // leaf queue; an exact walk's candidates (the queue is empty then)
+  int* cand = &cq[wave][0][lane];
+  const long long os = (long long)gridDim.x * 256;
+  int2* ovf = P.wide_ovf + ((long long)blockIdx.x * 256 + tid);
+  const float4* __restrict__ rays = B.rays[cur];
+  const CamFrame F = {};   // no path begins here
+  int p = -1;              // list slot of the lane's path
+  bool fin = false;        // the lane's walk is over (its queue may still hold candidates)
+  bool more = true;
+  WideRay R;
+  R.cur = -1;
+  R.sp = R.lo = 0;
+  R.nc = 0;
+  R.shadow = 0;
+  R.lim = 0.0f;
+  R.best = 0;
+  Ctr c = {0u, 0u, 0u, 0u, 0u};
+  // the reference's traversal of the lane's ray by the exact threaded walk
+  // (a ray the wide walk does not take, wide_ray_ok, or a stack bound hit)
+  auto exact_walk = [&]() {
+    Ctr cx = {0u, 0u, 0u, 0u, 0u};
+    if (!R.shadow) {
+      const Hit e = trace_closest<false, false, true, false>(P, R.o, R.d, cx, cand);
+      R.lim = e.t;
+      R.best = e.tri >= 0 ? P.wide_rank_of[e.tri] : e.tri;   // a slot; hit_tris is by rank
+    } else {
+      R.best = occluded<false, false>(P, R.o, R.d, R.lim, cx) ? 1 : 0;
+    }
+    R.nc = 0;
+    fin = true;
+  };
+  // the lane's next ray: kind 0 closest, 1 shadow, 2 null shadow query (its
+  // answer cannot change the image: unoccluded, no walk)
+  auto begin = [&](v3 o, v3 d, int kind, float lim) {
+    wide_start(R, o, d, kind != 0, lim);
+    fin = true;
+    if (kind == 2) {
+      R.best = 0;
+      return;
+    }
+    if (CNT) {
+      c.rays += kind == 0 ? 1u : 0u;
+      c.srays += kind == 1 ? 1u : 0u;
+    }
+    if (!wide_ray_ok(R.o, R.d, R.inv)) {
+      exact_walk();
+      return;
+    }
+    fin = false;
+  };
+  for (;;) {
+    // lanes whose walk is over shade together: path_step on the answer, then
+    // the path's next ray starts in the lane, or its colour is stored
+    while (p >= 0 && fin && R.nc == 0) {
+      Trav T;
+      T.o = R.o;
+      T.d = R.d;
+      T.shadow = R.shadow;
+      T.lim = R.lim;
+      T.res = R.best;
+      T.nc = 0;
+      T.cn = T.cl = 0u;
+      PathSt S;
+      wf_load_state(B, cur, p, R.o, R.d, &S);   // PH_SSS: the walk ray is S.so / S.sd
+      v3 col;
+      bool need = path_step<false>(P, F, S, T, c, &col);
+      while (need && T.shadow == 2) {   // null shadow queries (trav_null)
+        T.res = 0;
+        need = path_step<false>(P, F, S, T, c, &col);
+      }
+      if (need) {
+        wf_store_state(B, cur, p, S);
+        begin(T.o, T.d, T.shadow, T.lim);
+      } else {
+        B.colors[B.ids[cur][p]] = make_float4(col.x, col.y, col.z, 1.0f);
+        p = -1;
+        fin = false;
+      }
+    }
+    const unsigned long long idle = __ballot(p < 0);
+    const int ng = (int)__popcll(idle);
+    if (more && ng >= PT_WIDE_REFILL) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&B.counters[2], ng);
+      base = __shfl(base, 0);
+      if (base + ng >= count) more = false;
+      if (p < 0) {
+        const int slot = base + (int)__popcll(idle & ((1ull << lane) - 1ull));
+        if (slot < count) {
+          float4 r0, r1;
+          wf_load_ray(rays, B.cap, slot, &r0, &r1);
+          p = slot;
+          // a closest ray's limit word may carry fuse bits' RNG state: unused
+          // here (wide_start ignores a closest ray's limit)
+          begin(mk(r0.x, r0.y, r0.z), mk(r1.x, r1.y, r1.z), __float_as_int(r1.w) & kRayKindMask, r0.w);
+        }
+      }
+    }
+    if (!more && __ballot(p >= 0) == 0ull) break;
+    if (__ballot(p >= 0 && fin && R.nc == 0)) continue;   // shade first (a walk answered at its start)
+    for (int it = 0; it < PT_WF_STEPS; ++it) {
+      bool exact = false;
+      if (p >= 0 && !fin)
+        fin = wide_step<CNT, true, QN>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
+                                       &c.leaves, cand, P.wide_leafbox);
+      if (exact) exact_walk();   // the builder's stack bound rules this out; stay exact anyway
+      const unsigned long long waiting = __ballot(p >= 0 && fin && R.nc > 0);
+      if (__ballot(p >= 0 && R.nc > kWideQ - 4) || (int)__popcll(waiting) >= PT_WIDE_FLUSH_T ||
+          (waiting && __ballot(p >= 0 && !fin) == 0ull)) {
+        if (p >= 0 && R.nc > 0 && wide_flush<CNT, QN>(R, P.wide_tris, cand, &c.leaves, P.wide_leafbox)) {
+          fin = true;   // occluded
+          R.sp = 0;
+          R.cur = -1;
+        }
+      }
+      if (__ballot(p >= 0 && !(fin && R.nc == 0)) == 0ull) break;
+    }
+  }
+  if (CNT) flush_traced(P, c, lane);
 }
 
 // Running mean (:467-469) of each pixel's samples, in batch order.
@@ -2751,11 +2906,21 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
   if (wide) lds_t = 0;
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, trace, 256, lds_t);
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, wf_shade_kernel, 256, 0);
+  // PT_OPT_WF_TAIL (the 4-wide layouts of the wide walk): wf_tail_kernel after each round's trace
+  const bool tail = wide && p0.wf_tail > 0 && p0.wide_qn != 2;
+  void (*tailk)(RenderParams, WfBuffers, int) =
+      p0.wide_qn ? (cnt ? wf_tail_kernel<true, true> : wf_tail_kernel<false, true>)
+                 : (cnt ? wf_tail_kernel<true, false> : wf_tail_kernel<false, false>);
+  if (p0.wf_tail > 0 && !tail) return hipErrorInvalidValue;   // the trace and shading kernels would skip its lists
+  int per_cu_x = 0;
+  if (e == hipSuccess && tail) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_x, tailk, 256, 0);
   if (e != hipSuccess) return e;
   unsigned grid_t = (unsigned)(cus * (per_cu_t > 0 ? per_cu_t : 1));
+  unsigned grid_x = (unsigned)(cus * (per_cu_x > 0 ? per_cu_x : 1));
   if (wide) {   // every lane needs its overflow stack area
     if (p0.wide_ovf_lanes < 256) return hipErrorInvalidValue;
     grid_t = std::min<unsigned>(grid_t, (unsigned)(p0.wide_ovf_lanes / 256));
+    grid_x = std::min<unsigned>(grid_x, (unsigned)(p0.wide_ovf_lanes / 256));
   }
   const unsigned grid_s = (unsigned)(cus * (per_cu_s > 0 ? per_cu_s : 1));
   const uint32_t chunk = (uint32_t)std::min<long long>((long long)p0.n_batches, b.cap / px);
@@ -2804,6 +2969,8 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
     int cur = 0;
     for (int it = 0; it < iters; ++it) {
       for (int h = 0; h < H; ++h) hipLaunchKernelGGL(trace, dim3(grid_t), dim3(256), lds_t, sh[h], ph[h], bh[h], cur);
+      if (tail)
+        for (int h = 0; h < H; ++h) hipLaunchKernelGGL(tailk, dim3(grid_x), dim3(256), 0, sh[h], ph[h], bh[h], cur);
       for (int h = 0; h < H; ++h) wf_shade_kernel<<<grid_s, 256, 0, sh[h]>>>(ph[h], bh[h], cur);
 #ifdef PT_WF_ROUND_LOG   // A/B builds only: rays per round (synchronous)
       {

@@ -33,6 +33,7 @@ PT_OPT_WF_STREAMS = 13
 PT_OPT_WIDE_BUILD = 14
 PT_OPT_WF_FUSE = 15
 PT_OPT_WIDE_NODE = 16
+PT_OPT_WF_TAIL = 17
 KERNEL_AUTO, KERNEL_RECURSIVE, KERNEL_STATE_MACHINE, KERNEL_WAVEFRONT = 0, 1, 2, 3
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).

@@ -359,6 +359,14 @@ int pt_dist_finalize(pt_context* ctx);
  * twice the box tests per visit: measured slower, an option).  All are built
  * at upload.  Output is identical. */
 #define PT_OPT_WIDE_NODE 16
+/* PT_OPT_WF_TAIL: with the culled wide walk (4-wide nodes), once a ray
+ * round's list holds fewer than this many rays, one persistent launch runs
+ * every remaining path to its end (each lane walks a ray, shades it and walks
+ * the path's next ray) instead of a trace and a shading launch per remaining
+ * round; 0 = never; -1 (default) = auto: 2^20 for scenes below 2^20
+ * triangles rendering at most 2^22 paths per launch (small tile shares),
+ * else never.  Output is identical. */
+#define PT_OPT_WF_TAIL 17
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */

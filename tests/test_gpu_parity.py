@@ -896,6 +896,65 @@ def test_wide_walk_refused_tree_keeps_exact_walk():
     _assert_same(r.read_accum(), ref, "refused wide tree")
 
 
+@pytest.mark.parametrize("tail", [1 << 30, 3000, 1])
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("node", [64, 128])
+@pytest.mark.parametrize("case", ["sphere", "cloud_int_bits", "dense_cloud", "grid2lights", "box"])
+def test_wavefront_tail_kernel_matches_oracle(case, node, mode, tail):
+    """PT_OPT_WF_TAIL: once a round's list is shorter than `tail` rays,
+    wf_tail_kernel runs every remaining path to its end in one launch (walk,
+    path_step, the next walk in the same lane).  2^30: the whole frame in the
+    tail kernel from the first list; 3000: the late rounds; 1: never (the
+    rounds alone).  Over a stale accumulator, with mode 2 handing every odd
+    ray of the rounds to the exact walk: the oracle's frame bit for bit, and
+    the counting mode's walks equal to the rounds' own."""
+    sv, si, cam, lights, int_bits = _wide_case(case)
+    v, i, n, _, _ = ptamd.Scene.from_arrays(sv, si).build_bvh(int_bits=int_bits).arrays()
+    W, H = 80, 52
+    ref, _ = _oracle(v, i, n, W, H, nb=2, cam=cam, lights=lights, int_bits=int_bits)
+    ref, _ = _oracle(v, i, n, W, H, first=2, nb=3, cam=cam, lights=lights, int_bits=int_bits, accum=ref)
+    r = _setup(v, i, n, cam=cam, lights=lights, int_bits=int_bits, lds=0)
+    r.set_option(ptamd.PT_OPT_KERNEL, 3)
+    r.set_option(ptamd.PT_OPT_WIDE, mode)
+    r.set_option(ptamd.PT_OPT_WIDE_NODE, node)
+    r.set_option(ptamd.PT_OPT_WF_TAIL, tail)
+    r.resize_and_clear(W, H)
+    r.render(0, 2)
+    r.render(2, 3)
+    _assert_same(r.read_accum(), ref, f"tail kernel {case} node {node} mode {mode} tail {tail}")
+
+
+@pytest.mark.parametrize("case", ["sphere", "cloud_int_bits"])
+def test_wavefront_tail_kernel_counts_and_two_streams(case):
+    """The tail kernel's counting variant starts the same closest-hit walks as
+    the rounds (shadow walks differ only by the fused walks' bookkeeping:
+    both count each walk once), and with two streams (each half's own lists
+    and counters) the frame is still the oracle's."""
+    sv, si, cam, lights, int_bits = _wide_case(case)
+    v, i, n, _, _ = ptamd.Scene.from_arrays(sv, si).build_bvh(int_bits=int_bits).arrays()
+    W, H, nb = 120, 72, 2
+    ref, _ = _oracle(v, i, n, W, H, nb=nb, cam=cam, lights=lights, int_bits=int_bits)
+    got = {}
+    for tail in (0, 1 << 30, 5000):
+        r = _setup(v, i, n, cam=cam, lights=lights, int_bits=int_bits, lds=0)
+        r.set_option(ptamd.PT_OPT_KERNEL, 3)
+        r.set_option(ptamd.PT_OPT_WF_TAIL, tail)
+        r.set_option(ptamd.PT_OPT_COUNT_TRACED, 1)
+        r.reset_stats()
+        r.resize_and_clear(W, H)
+        r.render(0, nb)
+        _assert_same(r.read_accum(), ref, f"counting tail {tail} {case}")
+        got[tail] = r.traced()
+        r.set_option(ptamd.PT_OPT_COUNT_TRACED, 0)
+        r.set_option(ptamd.PT_OPT_WF_STREAMS, 2)
+        r.resize_and_clear(W, H)
+        r.render(0, nb)
+        _assert_same(r.read_accum(), ref, f"two streams tail {tail} {case}")
+    for tail in (1 << 30, 5000):
+        assert got[tail]["closest_walks"] == got[0]["closest_walks"], (tail, got)
+        assert got[tail]["primaries"] == got[0]["primaries"], (tail, got)
+
+
 @pytest.mark.parametrize("case", ["sphere", "cloud_int_bits"])
 def test_wavefront_two_streams(case):
     """PT_OPT_WF_STREAMS 2: the chunk's pixels as two halves on two streams
