@@ -2254,6 +2254,95 @@ __device__ __forceinline__ int fused_shadow_ray(const RenderParams& P, v3 o, v3 
 }
 constexpr int kFuseWalk = 16;   // lane state: walking the fused shadow ray
 
+// PT_WIDE_FLUSH_WAVE: the wave's queued leaf candidates tested one per lane.
+// wide_flush runs a lane's queue in its own lane, so a flush takes as many
+// loop trips as the longest queue while the others idle: a probe of the trace
+// kernel (tools/flush_probe.py) measured 67 candidates per flush on the
+// displaced sphere and 38 on the 10M cloud, against a longest queue of 5.8 /
+// 4.7 -- 18 % / 13 % of the flush loop's lane slots in use.  Here the
+// candidates are numbered across the wave (a prefix sum of the queue
+// lengths), and lane j of each window of 64 tests candidate j: it finds the
+// owner by a binary search over the prefix sums, reads the rank from the
+// owner's queue column, the owner's ray by lane shuffles, and runs the same
+// triangle test and accept rules.  The owner's answer is a lexicographic
+// minimum of (t, rank) -- an LDS atomic min of (t bits << 32 | rank), t > 0
+// (tri_test accepts t > 1e-6), so its bits order as its value -- merged with
+// the owner's best by wide_cand's own rule; a shadow ray is occluded if any
+// of its candidates is an accepted hit below its limit.  Neither answer
+// depends on the order the candidates are tested in (ties go to the lower
+// rank, the reference's visit order): the same hits as wide_flush.  Call with
+// every lane of the wave active; keys: the wave's 64 LDS words; returns true
+// for a shadow ray found occluded.
+#ifndef PT_WIDE_FLUSH_WAVE
+#define PT_WIDE_FLUSH_WAVE 1
+#endif
+template <bool CNT, bool QN>
+__device__ __forceinline__ bool wide_flush_wave(WideRay& R, bool mine, const float4* __restrict__ tris, const int* cand,
+                                                unsigned long long* keys, int lane, uint32_t* cl,
+                                                const float4* __restrict__ leaf_box) {
+  const int n = mine ? R.nc : 0;
+  int incl = n;   // inclusive prefix sum of the queue lengths
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const int v = __shfl_up(incl, (unsigned)s);
+    if (lane >= s) incl += v;
+  }
+  const int total = __shfl(incl, 63);
+  const int off = incl - n;
+  keys[lane] = ~0ull;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int* qbase = cand - lane;   // the wave's queue: [k][lane]
+  for (int base = 0; base < total; base += 64) {
+    const int target = base + lane;
+    int L = 0;   // the owner: lanes whose inclusive sum is <= target
+#pragma unroll
+    for (int s = 32; s >= 1; s >>= 1) {
+      const int v = __shfl(incl, L + s - 1);
+      if (v <= target) L += s;
+    }
+    L = min(L, 63);
+    const int offL = __shfl(off, L);
+    const v3 o = mk(__shfl(R.o.x, L), __shfl(R.o.y, L), __shfl(R.o.z, L));
+    const v3 d = mk(__shfl(R.d.x, L), __shfl(R.d.y, L), __shfl(R.d.z, L));
+    const float lim = __shfl(R.lim, L);
+    const int shadow = __shfl(R.shadow, L);
+    if (target < total) {
+      const int r = qbase[(target - offL) * 64 + L];
+      const float4* T = tris + 3 * (size_t)r;
+      const float4 A = T[0], B = T[1], C = T[2];
+      if (CNT) ++*cl;
+      float t;
+      // shadow: :359 / :398; closest: a hit that can still win (t == lim may
+      // tie with a lower rank)
+      if (tri_test(o, d, A, B, C, &t) && t < 1e30f && (shadow ? !(t >= lim) : t <= lim)) {
+        bool ok = true;
+        if (QN) ok = slab(o, mk(rcp_(d.x), rcp_(d.y), rcp_(d.z)), leaf_box[2 * (size_t)r], leaf_box[2 * (size_t)r + 1]);
+        if (ok) atomicMin(&keys[L], shadow ? 0ull : ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)r);
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (n == 0) return false;
+  R.nc = 0;
+  const unsigned long long k = keys[lane];
+  if (k == ~0ull) return false;
+  if (R.shadow) {
+    R.best = 1;
+    return true;
+  }
+  const float tm = __uint_as_float((uint32_t)(k >> 32));
+  const int rm = (int)(uint32_t)k;
+  if (tm < R.lim || (tm == R.lim && R.best >= 0 && rm < R.best)) {   // wide_cand's rule
+    R.lim = tm;
+    R.best = rm;
+  }
+  return false;
+}
+
 // LAYOUT: 0 128-B 4-wide nodes, 1 64-B 4-wide nodes (QN), 2 80-B 8-wide
 // nodes (w8_step; leaf indices are positions, ties go by pos_rank)
 template <int G, bool CNT = false, int LAYOUT = 1>
@@ -2269,6 +2358,8 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
   int2* lds = &stk[wave][0][lane];
   __shared__ int cq[PT_WIDE_QUEUE ? 4 : 1][PT_WIDE_QUEUE ? kWideQ : 1][64];
   int* cand = PT_WIDE_QUEUE ? &cq[wave][0][lane] : nullptr;
+  constexpr bool FW = PT_WIDE_FLUSH_WAVE && PT_WIDE_QUEUE && LAYOUT != 2;
+  __shared__ unsigned long long fkeys[FW ? 4 : 1][64];
   bool fin = false;
   const long long os = (long long)gridDim.x * 256;
   int2* ovf = P.wide_ovf + ((long long)blockIdx.x * 256 + tid);
@@ -2401,6 +2492,10 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
         // leaves, or PT_WIDE_FLUSH_T finished walks waiting on their queue,
         // or nothing left walking
         const unsigned long long waiting = __ballot(p >= 0 && fin && R.nc > 0);
+#ifdef PT_WIDE_PROBE_FLUSH
+        if (lane == 0) atomicAdd(&P.stats[7], 1ull);
+        if (lane == 0) atomicAdd(&P.stats[8], (unsigned long long)__popcll(__ballot(p >= 0 && !fin)));
+#endif
 #ifdef PT_WIDE_PROBE   // lane-state census per step (traced counters 0-4: walking, idle with rays left
                        // in the list, idle in the drain, steps, waiting on the leaf queue)
         {
@@ -2415,9 +2510,26 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
 #endif
         if (__ballot(p >= 0 && R.nc > kWideQ - 4) || (int)__popcll(waiting) >= PT_WIDE_FLUSH_T ||
             (waiting && __ballot(p >= 0 && !fin) == 0ull)) {
-          if (p >= 0 && R.nc > 0 &&
-              wide_flush<CNT, QN>(R, P.wide_tris, cand, &c.leaves, P.wide_leafbox,
-                                  LAYOUT == 2 ? P.wide_pos_rank : nullptr)) {
+#ifdef PT_WIDE_PROBE_FLUSH   // flush loop use: [4] flushes, [5] sum of candidates, [6] sum of the largest queue, [7] steps
+          {
+            int mx = p >= 0 ? R.nc : 0, sm = mx;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+              mx = max(mx, __shfl_xor(mx, o));
+              sm += __shfl_xor(sm, o);
+            }
+            if (lane == 0) {
+              atomicAdd(&P.stats[4], 1ull);
+              atomicAdd(&P.stats[5], (unsigned long long)sm);
+              atomicAdd(&P.stats[6], (unsigned long long)mx);
+            }
+          }
+#endif
+          if (FW ? wide_flush_wave<CNT, QN>(R, p >= 0, P.wide_tris, cand, fkeys[FW ? wave : 0], lane, &c.leaves,
+                                            P.wide_leafbox)
+                 : (p >= 0 && R.nc > 0 &&
+                    wide_flush<CNT, QN>(R, P.wide_tris, cand, &c.leaves, P.wide_leafbox,
+                                        LAYOUT == 2 ? P.wide_pos_rank : nullptr))) {
             fin = true;   // occluded
             R.sp = 0;
             R.cur = -1;
@@ -2599,6 +2711,7 @@ __global__ __launch_bounds__(256, PT_WF_TAIL_MIN_BLOCKS) void wf_tail_kernel(Ren
   int2* lds = &stk[wave][0][lane];
   __shared__ int cq[4][kWideQ][64];   // leaf queue; an exact walk's candidates (the queue is empty then)
   int* cand = &cq[wave][0][lane];
+  __shared__ unsigned long long fkeys[PT_WIDE_FLUSH_WAVE ? 4 : 1][64];
   const long long os = (long long)gridDim.x * 256;
   int2* ovf = P.wide_ovf + ((long long)blockIdx.x * 256 + tid);
   const float4* __restrict__ rays = B.rays[cur];
@@ -2706,7 +2819,9 @@ __global__ __launch_bounds__(256, PT_WF_TAIL_MIN_BLOCKS) void wf_tail_kernel(Ren
       const unsigned long long waiting = __ballot(p >= 0 && fin && R.nc > 0);
       if (__ballot(p >= 0 && R.nc > kWideQ - 4) || (int)__popcll(waiting) >= PT_WIDE_FLUSH_T ||
           (waiting && __ballot(p >= 0 && !fin) == 0ull)) {
-        if (p >= 0 && R.nc > 0 && wide_flush<CNT, QN>(R, P.wide_tris, cand, &c.leaves, P.wide_leafbox)) {
+        if (PT_WIDE_FLUSH_WAVE ? wide_flush_wave<CNT, QN>(R, p >= 0, P.wide_tris, cand, fkeys[PT_WIDE_FLUSH_WAVE ? wave : 0],
+                                                        lane, &c.leaves, P.wide_leafbox)
+                               : (p >= 0 && R.nc > 0 && wide_flush<CNT, QN>(R, P.wide_tris, cand, &c.leaves, P.wide_leafbox))) {
           fin = true;   // occluded
           R.sp = 0;
           R.cur = -1;
