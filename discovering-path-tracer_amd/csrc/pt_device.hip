@@ -2700,7 +2700,6 @@ __global__ __launch_bounds__(256, PT_WF_SHADE_MIN_BLOCKS) void wf_shade_kernel(R
 #ifndef PT_WF_TAIL_MIN_BLOCKS
 #define PT_WF_TAIL_MIN_BLOCKS 4
 #endif
-static_assert(kCand <= kWideQ, "wf_tail_kernel runs its exact walks in the leaf queue's LDS");
 template <bool CNT, bool QN>
 __global__ __launch_bounds__(256, PT_WF_TAIL_MIN_BLOCKS) void wf_tail_kernel(RenderParams P, WfBuffers B, int cur) {
   const int count = B.counters[cur];
@@ -2709,7 +2708,8 @@ __global__ __launch_bounds__(256, PT_WF_TAIL_MIN_BLOCKS) void wf_tail_kernel(Ren
   const int wave = tid >> 6, lane = tid & 63;
   __shared__ int2 stk[4][kWideLds][64];
   int2* lds = &stk[wave][0][lane];
-  __shared__ int cq[4][kWideQ][64];   // leaf queue; an exact walk's candidates (the queue is empty then)
+  // leaf queue; an exact walk's candidates (the queue is empty then)
+  __shared__ int cq[4][kWideQ > kCand ? kWideQ : kCand][64];
   int* cand = &cq[wave][0][lane];
   __shared__ unsigned long long fkeys[PT_WIDE_FLUSH_WAVE ? 4 : 1][64];
   const long long os = (long long)gridDim.x * 256;
