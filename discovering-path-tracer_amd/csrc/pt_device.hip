@@ -2210,6 +2210,11 @@ __global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_ker
 #ifndef PT_WIDE_REFILL
 #define PT_WIDE_REFILL 16
 #endif
+// steps between the wide walk's refill checks: 12 (with the wave-wide flush,
+// item 39): 10M cloud -1.7 %, sphere -0.1 % against 8; 16: -0.5 % / +0.6 %
+#ifndef PT_WIDE_STEPS
+#define PT_WIDE_STEPS 12
+#endif
 constexpr int kWideG = PT_WIDE_G;
 #ifndef PT_WIDE_DEFER_DONE
 #define PT_WIDE_DEFER_DONE 1
@@ -2455,7 +2460,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
       }
     }
     if (!more && __ballot(p >= 0) == 0ull) break;
-    for (int it = 0; it < PT_WF_STEPS; ++it) {
+    for (int it = 0; it < PT_WIDE_STEPS; ++it) {
       bool exact = false;
       if (!PT_WIDE_QUEUE) {
         static_assert(!PT_WIDE_QUEUE ? LAYOUT != 2 : true, "the 8-wide walk runs with PT_WIDE_QUEUE");
@@ -2688,7 +2693,7 @@ __global__ __launch_bounds__(256, PT_WF_SHADE_MIN_BLOCKS) void wf_shade_kernel(R
 // (the culled wide walk with the trace kernel's queued leaf tests and
 // wave-wide flushes), then path_step, then the next ray's walk in the same
 // lane -- and stores the path's colour; the lanes whose walks have ended
-// shade together at the check every PT_WF_STEPS steps, as the trace kernel
+// shade together at the check every PT_WIDE_STEPS steps, as the trace kernel
 // finishes its walks.  The path's state waits in its own list slot
 // (wf_store_state / wf_load_state) while the lane walks, so the walk keeps
 // the trace kernel's registers.  The rays, draws, float operations and their
@@ -2810,7 +2815,7 @@ __global__ __launch_bounds__(256, PT_WF_TAIL_MIN_BLOCKS) void wf_tail_kernel(Ren
     }
     if (!more && __ballot(p >= 0) == 0ull) break;
     if (__ballot(p >= 0 && fin && R.nc == 0)) continue;   // shade first (a walk answered at its start)
-    for (int it = 0; it < PT_WF_STEPS; ++it) {
+    for (int it = 0; it < PT_WIDE_STEPS; ++it) {
       bool exact = false;
       if (p >= 0 && !fin)
         fin = wide_step<CNT, true, QN>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
