@@ -1040,14 +1040,13 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
       p.wide_handback = c->opt_wide == 2 ? 1 : 0;
       // fused shadow walks: hit records carry the rank in 29 bits
       p.wf_fuse = c->opt_wf_fuse && c->n_tris <= ptd::kHitRankMask && c->n_lights > 0 ? 1 : 0;
-      // wf_tail_kernel (4-wide layouts).  Auto: a list of < 2^20 rays when the
-      // scene is below 2^20 triangles (its tree cache-resident, walks short)
-      // and the launch holds at most 2^22 paths (a few rays per traversal lane
-      // per round, so each round's drain dominates).  Emulated 1/8 tile share
-      // of config 3 (2M paths): 14.9 -> 12.4 ms; 1/8 shares of config 4 (16.6M
-      // paths) and of the 10M cloud: +2 % (not taken); whole frames: +-0.3 %.
-      const long long paths = std::min(chunk_paths, items * (256 / p.spl) * (long long)n_batches);
-      const int tail_auto = c->n_tris < (1 << 20) && paths <= (1ll << 22) ? (1 << 20) : 0;
+      // wf_tail_kernel (4-wide layouts).  Auto: once a list holds fewer than
+      // 400K rays (with the wave-wide flush, item 39; ab_bench device time):
+      // emulated 1/8 tile shares of configs 3 / 4 / 5 13.48 -> 11.31, 64.68 ->
+      // 64.26, 22.36 -> 21.91 ms; whole frames 44.28 -> 43.77, 384.41 ->
+      // 384.89, 117.72 -> 117.39 ms.  (2^20: 11.17 / 65.31 / 22.39; from the
+      // first list: +28-57 % on whole frames.)
+      const int tail_auto = 400000;
       p.wf_tail = w8 ? 0 : c->opt_wf_tail >= 0 ? c->opt_wf_tail : tail_auto;
     }
     if (c->opt_wf_streams == 2 && !c->wf_stream2) {

@@ -363,9 +363,8 @@ int pt_dist_finalize(pt_context* ctx);
  * round's list holds fewer than this many rays, one persistent launch runs
  * every remaining path to its end (each lane walks a ray, shades it and walks
  * the path's next ray) instead of a trace and a shading launch per remaining
- * round; 0 = never; -1 (default) = auto: 2^20 for scenes below 2^20
- * triangles rendering at most 2^22 paths per launch (small tile shares),
- * else never.  Output is identical. */
+ * round; 0 = never; -1 (default) = auto (400000 rays).  Output is
+ * identical. */
 #define PT_OPT_WF_TAIL 17
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
