@@ -23,7 +23,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BOX_KERNEL = "render_kernel<false, true, false>"
 KERNEL_SOURCES = ("pt_device.hip", "pt_device.h", "pt_isect.h", "wide_walk.h", "pt_math.h", "scene/wide_bvh.cpp")   # == bench.py
-WF_KERNELS = ("wf_gen_kernel", "wf_trace_kernel", "wf_trace_wide_kernel", "wf_trace_pairs_kernel", "wf_shade_kernel",
+WF_KERNELS = ("wf_gen_kernel", "wf_trace_kernel", "wf_trace_wide_kernel", "wf_trace_pairs_kernel", "wf_tail_kernel", "wf_shade_kernel",
               "wf_fold_kernel", "fill_culled_kernel")
 
 
