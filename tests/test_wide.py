@@ -70,15 +70,16 @@ def _scene(v, i):
 # the two ways the wide nodes group the reference's leaves (scene/wide_bvh.h)
 WIDE_FROM_REFERENCE, WIDE_SAH = 0, 1
 # (grouping, node bytes, queued leaf tests): the kernel's default is (SAH, 64,
-# queued); 64-B nodes hold boxes rounded outward onto an 8-bit grid and test a
+# 2: queued, flushed wave-wide); 64-B nodes hold boxes rounded outward onto an 8-bit grid and test a
 # leaf's exact box before its hit counts (wide_walk.h); queued: leaf hits are
 # tested in flushes, as one lane of the trace kernel does (PT_WIDE_QUEUE)
 BUILDS = pytest.mark.parametrize(
     "build", [(WIDE_SAH, 80, 1), (WIDE_SAH, 80, 0), (WIDE_SAH, 64, 1), (WIDE_SAH, 64, 0), (WIDE_SAH, 128, 1),
               (WIDE_SAH, 128, 0), (WIDE_FROM_REFERENCE, 80, 1), (WIDE_FROM_REFERENCE, 64, 1),
-              (WIDE_FROM_REFERENCE, 128, 0)],
+              (WIDE_FROM_REFERENCE, 128, 0), (WIDE_SAH, 64, 2), (WIDE_SAH, 128, 2), (WIDE_FROM_REFERENCE, 64, 2)],
     ids=["sah-w8-queue", "sah-w8", "sah-64-queue", "sah-64", "sah-128-queue", "sah-128", "reference_tree-w8-queue",
-         "reference_tree-64-queue", "reference_tree-128"])
+         "reference_tree-64-queue", "reference_tree-128", "sah-64-waveflush", "sah-128-waveflush",
+         "reference_tree-64-waveflush"])
 
 
 def check(v, idx, nodes, rays, build=(WIDE_SAH, 64, 1)):

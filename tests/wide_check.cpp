@@ -20,7 +20,8 @@ using namespace ptd;
 namespace {
 int g_mode = pt::WIDE_SAH;   // wide_set_mode
 int g_node = 128;            // wide_set_variant: node bytes (64: the quantized layout with exact leaf tests)
-int g_queue = 0;             // ... and 1: the queued leaf tests with wave-style flushes (the kernel's default)
+int g_queue = 0;             // ... and 1: the queued leaf tests with per-lane flushes; 2: with the wave-wide flush's
+                             // merge (flush_lexmin, the trace kernel's default)
 
 struct Built {
   pt::WideBVH w;
@@ -83,6 +84,45 @@ void walk8(WideRay& R, const Built& b, int2* lds, int2* ovf, bool* exact, uint32
 // QUEUE: leaf hits queued (stride 64, like one lane of the kernel's LDS
 // queue) and flushed when the queue cannot take another node's four leaves
 // or the walk has no node left (PT_WIDE_FLUSH_T 1).
+// The wave-wide flush of the trace kernel (pt_device.hip wide_flush_wave),
+// restated for one lane: every queued candidate is tested (here in reverse
+// queue order, as another lane of the wave could), the accepted ones reduce
+// to the lexicographic least (t, rank) -- the kernel's LDS atomic min of
+// (t bits << 32 | rank) -- which is merged with the ray's best by
+// wide_cand's rule; a shadow ray is occluded by any accepted candidate.
+template <bool QN>
+bool flush_lexmin(WideRay& R, const float4* tris, const int* cand, uint32_t* cl, const float4* leaf_box) {
+  const int n = R.nc;
+  R.nc = 0;
+  bool any = false;
+  unsigned long long key = ~0ull;
+  for (int i = n - 1; i >= 0; --i) {
+    const int r = cand[i * 64];
+    const float4* T = tris + 3 * (size_t)r;
+    ++*cl;
+    float t;
+    if (tri_test(R.o, R.d, T[0], T[1], T[2], &t) && t < 1e30f && (R.shadow ? !(t >= R.lim) : t <= R.lim) &&
+        (!QN || slab(R.o, mk(rcp_(R.d.x), rcp_(R.d.y), rcp_(R.d.z)), leaf_box[2 * (size_t)r],
+                     leaf_box[2 * (size_t)r + 1]))) {
+      any = true;
+      const unsigned long long k = ((unsigned long long)f2u(t) << 32) | (uint32_t)r;
+      if (k < key) key = k;
+    }
+  }
+  if (!any) return false;
+  if (R.shadow) {
+    R.best = 1;
+    return true;
+  }
+  const float tm = u2f((uint32_t)(key >> 32));
+  const int rm = (int)(uint32_t)key;
+  if (tm < R.lim || (tm == R.lim && R.best >= 0 && rm < R.best)) {
+    R.lim = tm;
+    R.best = rm;
+  }
+  return false;
+}
+
 template <bool QN, bool QUEUE>
 void walk(WideRay& R, const Built& b, int2* lds, int2* ovf, bool* exact, uint32_t* cn, uint32_t* cl) {
   const float4* nodes = (const float4*)(QN ? b.w.qnodes.data() : b.w.nodes.data());
@@ -101,7 +141,8 @@ void walk(WideRay& R, const Built& b, int2* lds, int2* ovf, bool* exact, uint32_
                                       cand.data(), leafbox);
     if (*exact) return;
     if (R.nc > kWideQ - 4 || (fin && R.nc > 0)) {
-      if (wide_flush<true, QN>(R, b.tris.data(), cand.data(), cl, leafbox)) {   // occluded
+      if (g_queue == 2 ? flush_lexmin<QN>(R, b.tris.data(), cand.data(), cl, leafbox)
+                       : wide_flush<true, QN>(R, b.tris.data(), cand.data(), cl, leafbox)) {   // occluded
         fin = true;
         R.sp = 0;
         R.cur = -1;

@@ -20,7 +20,7 @@ done <<< "$GROUPS_LIST"
 python3 - $OUT <<'PY'
 import csv, glob, sys, collections
 out = sys.argv[1]
-fam = lambda n: next((k for k in ("wf_trace", "wf_shade", "wf_gen", "wf_fold", "render_kernel") if k in n), None)
+fam = lambda n: next((k for k in ("wf_trace", "wf_tail", "wf_shade", "wf_gen", "wf_fold", "render_kernel") if k in n), None)
 agg = collections.defaultdict(float)
 for f in sorted(glob.glob(out + "/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
