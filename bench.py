@@ -330,6 +330,16 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
                                       kernel_ms, int(kt.size), "median kernel_ms (HIP events around each "
                                                                "frame's launches on the render stream)"),
            "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
+    if prof is not None and prof[1].get("sq_per_launch", {}).get("SQ_INSTS_VALU"):
+        # the same frame against the VALU issue peak (committed PMC profile):
+        # the traversal of an L2/MALL-resident tree is bound by issue and
+        # dependent latency, not by HBM
+        valu = prof[1]["sq_per_launch"]["SQ_INSTS_VALU"]
+        gi = valu / (kernel_ms * 1e-3) / 1e9
+        out["roofline_valu"] = {"achieved": round(gi, 2), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
+                                "frac": round(gi / VALU_PEAK_GINST, 4), "valu_wave_instr_per_frame": int(valu),
+                                "source": prof[0],
+                                "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 f32 instruction"}
     if exhaustive_too:
         r.set_option(ptamd.PT_OPT_WIDE, 0)
         r.reset_launch_times()

@@ -14,7 +14,7 @@ f=$(find $OUT -name '*kernel_trace.csv' | head -1)
 python3 - "$f" <<'PY'
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
-rows = [r for r in rows if any(k in r["Kernel_Name"] for k in ("wf_trace", "wf_shade", "wf_gen", "wf_fold"))]
+rows = [r for r in rows if any(k in r["Kernel_Name"] for k in ("wf_trace", "wf_tail", "wf_shade", "wf_gen", "wf_fold"))]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 n = len(rows) // 2   # the last frame
 last = rows[n:]
