@@ -621,8 +621,12 @@ def main():
     args = ap.parse_args()
     W, H, SPP = args.width, args.height, args.spp
     if args.streams is None:
+        # N = 1: the box's 0.27-ms frames alternate between two contexts
+        # (double-buffered accumulation, one stream each), so frame k+1 starts
+        # while frame k's last workgroups drain (-5.4 %, tools/box_streams.py);
+        # the long large-scene frames gain nothing from it and keep one
         args.streams = 2 if (int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.packed
-                             or int(os.environ.get("PT_BENCH_EMULATE_RANKS", "1")) > 1) else 1
+                             or int(os.environ.get("PT_BENCH_EMULATE_RANKS", "1")) > 1 or args.scene == "box") else 1
     if args.collective == "reduce":
         args.streams = 1   # the reduce path runs on one stream
     if args.timing_every is None:
@@ -782,9 +786,33 @@ def main():
     finish = None
     ingest = None   # the emulated root's stand-in for the gather's receive traffic
     nparts = max(world, emu)
+    ctxs = [r]   # N = 1: the contexts frames alternate between
     if dist is None and emu == 1 and not args.packed:
+        # args.streams > 1: frames alternate between that many contexts, each
+        # with its own stream and accumulation buffer (the same scene, camera
+        # and options), so consecutive frames overlap on the GPU; every frame
+        # is still a whole frame from batch 0 (bitwise checked after timing)
+        for _ in range(args.streams - 1):
+            x = ptamd.Renderer(device)
+            x.upload_scene(v, i, n, int_bits=int_bits)
+            x.upload_lights(light)
+            x.set_camera(cam)
+            x.set_params(DEPTH, SSS)
+            x.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+            x.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 0)
+            for kv in args.opt:
+                k, _, val = kv.partition("=")
+                x.set_option(int(k), int(val))
+            xs = torch.cuda.Stream(dev)
+            x.set_stream(xs.cuda_stream)
+            x.resize_and_clear(W, H)
+            ctxs.append(x)
+        state1 = {"k": 0}
+
         def step():
-            r.render(0, SPP)
+            c = ctxs[state1["k"] % len(ctxs)]
+            state1["k"] += 1
+            c.render(0, SPP)
     elif args.collective == "reduce":
         r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 0)
         frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
@@ -969,6 +997,17 @@ def main():
         t = allreduce_max(torch.tensor([dt, kernel_ms, interval_ms], dtype=torch.float64, device=dev))
         dt, kernel_ms, interval_ms = float(t[0]), float(t[1]), float(t[2])
     roof_ms = interval_ms if args.streams > 1 else kernel_ms
+    pipelined = len(ctxs) > 1
+    if pipelined:
+        # frames overlap across the contexts: the GPU time per frame is the
+        # wall time per step (the launch events of one context span two frames)
+        roof_ms = dt / args.steps * 1e3
+        for c in ctxs[1:]:
+            c.synchronize()
+        want = ctxs[0].read_accum().view(np.uint32)
+        for c in ctxs[1:]:
+            if not np.array_equal(c.read_accum().view(np.uint32), want):
+                raise SystemExit("bench: the pipelined contexts' frames differ")
 
     no_cull = None
     default_cfg = args.scene == "box" and (W, H, SPP, DEPTH, SSS) == (1920, 1080, 8, 4, 3)
@@ -978,16 +1017,18 @@ def main():
     if world == 1 and args.compare_no_cull:
         # the same frames with primary-ray culling off (every pixel generated
         # and traced), for reference next to the default
-        r.set_option(ptamd.PT_OPT_PRIMARY_CULL, 0)
+        for c in ctxs:
+            c.set_option(ptamd.PT_OPT_PRIMARY_CULL, 0)
         for _ in range(args.warmup):
             step()
-        r.synchronize()
+        torch.cuda.synchronize(dev)
         t1 = time.perf_counter()
         for _ in range(args.steps):
             step()
-        r.synchronize()
+        torch.cuda.synchronize(dev)
         dt_nc = time.perf_counter() - t1
-        r.set_option(ptamd.PT_OPT_PRIMARY_CULL, 1)
+        for c in ctxs:
+            c.set_option(ptamd.PT_OPT_PRIMARY_CULL, 1)
         no_cull = {"ms_per_step": round(dt_nc / args.steps * 1e3, 4),
                    "value": round(rays_per_frame * args.steps / dt_nc / 1e6, 3)}
 
@@ -1060,7 +1101,9 @@ def main():
                        "sss_bounces": SSS,
                        "partition_slots": slots,
                        "parallelism": (f"tiles{world}-" + ("sparse-gather" if args.collective == "gather" else "reduce"))
-                       if world > 1 else ("single-packed" if args.packed else "single"),
+                       if world > 1 else ("single-packed" if args.packed else
+                                          f"single, frames alternating over {len(ctxs)} contexts (one stream and "
+                                          "accumulation buffer each)" if pipelined else "single"),
                        "streams": args.streams,
                        "step_loop": ("python" if native is None else
                                      "native (pt_dist_run, RCCL from C++)" if not os.environ.get("PT_RCCL_LIB")
@@ -1070,8 +1113,9 @@ def main():
                        "msamples_per_s": round(W * H * SPP * args.steps / dt / 1e6, 3)},
             "roofline": roofline_block(prof, roof_ms, own_bytes, box_kernel,
                                        kernel_ms, interval_ms, int(kt.size),
-                                       "launch_interval_ms (busy span / launches; launches overlap on "
-                                       f"{args.streams} streams)" if args.streams > 1 else "kernel_ms"),
+                                       ("wall ms per frame (frames overlap across the N=1 contexts)" if pipelined
+                                        else "launch_interval_ms (busy span / launches; launches overlap on "
+                                        f"{args.streams} streams)" if args.streams > 1 else "kernel_ms")),
         }
         if traced is not None:
             add_traced(out_line["config"], traced, dt / args.steps)
