@@ -261,9 +261,13 @@ def roofline_block(prof, time_ms, alg_bytes, kernel, kernel_ms, interval_ms, n_t
 
 # the BASELINE configs the default run reports beside the headline, one GPU
 # each: (key, scene, W, H, spp, MAX_DEPTH, timed frames, profile workload)
-SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 5, "sphere_1080p8"),
-              ("config4", "sphere", 3840, 2160, 16, 8, 3, "sphere_4k16_d8"),
-              ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5, "synthetic10M_1080p8"))
+# (key, scene, W, H, spp, MAX_DEPTH, timed frames, profile workload,
+# contexts): config 3's frames alternate between two contexts (one frame's
+# ray rounds run beside the other's drains: 44.0 -> 39.1 ms per frame,
+# tools/scene_streams.py); configs 4 and 5 gain nothing from it (+-0.5 %)
+SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 6, "sphere_1080p8", 2),
+              ("config4", "sphere", 3840, 2160, 16, 8, 3, "sphere_4k16_d8", 1),
+              ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5, "synthetic10M_1080p8", 1))
 
 
 def time_frames(r, spp, steps):
@@ -279,18 +283,38 @@ def time_frames(r, spp, steps):
     return np.array(walls), r.launch_times_ms()
 
 
+def time_frames_pipelined(ctxs, spp, steps, groups=3):
+    """`groups` runs of `steps` frames alternating between the contexts with
+    no wait in between (frames overlap on the GPU): wall ms per frame of each
+    run."""
+    import torch
+    walls = []
+    for _ in range(groups):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            ctxs[k % len(ctxs)].render(0, spp)
+        torch.cuda.synchronize()
+        walls.append((time.perf_counter() - t0) * 1e3 / steps)
+    return np.array(walls)
+
+
 def spread(ms):
     return {"min": round(float(np.min(ms)), 3), "median": round(float(np.median(ms)), 3),
             "max": round(float(np.max(ms)), 3), "frames": int(ms.size)}
 
 
-def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaustive_too=False):
+def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaustive_too=False, contexts=1):
     """One BASELINE config on one GPU (N = 1 only): the reference rays of a
     stats-mode frame, the walks of a counting frame, `steps` timed frames
     after one warmup, and the roofline priced from the committed profile of
     this workload (tools/profile_workload.sh).  exhaustive_too: one more frame
     with PT_OPT_WIDE 0 -- the threaded exhaustive walk, the reference's own
-    traversal shape -- reported as `exhaustive_walk` (workload + "_exhaustive")."""
+    traversal shape -- reported as `exhaustive_walk` (workload + "_exhaustive").
+    contexts > 1: the timed frames alternate between that many contexts
+    (own stream, accumulation and wavefront buffers each), two frames in
+    flight; ms per frame is then the wall time of a run over its frames, and
+    the contexts' frames are checked bitwise equal."""
     import ptamd
     import scenes
     import torch
@@ -298,23 +322,40 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
     scene, cam, int_bits, desc = load_scene(scene_name)
     v, i, n, _, _ = scene.arrays()
     del scene
-    r = ptamd.Renderer(device)
-    r.upload_scene(v, i, n, int_bits=int_bits)
+    ctxs = []
+    for _ in range(contexts):
+        x = ptamd.Renderer(device)
+        x.upload_scene(v, i, n, int_bits=int_bits)
+        x.upload_lights(scenes.REFERENCE_LIGHT)
+        x.set_camera(cam)
+        x.set_params(depth, sss)
+        if ctxs:
+            xs = torch.cuda.Stream(torch.device("cuda", device))
+            x.set_stream(xs.cuda_stream)
+            x.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+            x.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 0)
+        x.resize_and_clear(W, H)
+        ctxs.append(x)
+    r = ctxs[0]
     ntri = i.size // 3
     del v, i, n
-    r.upload_lights(scenes.REFERENCE_LIGHT)
-    r.set_camera(cam)
-    r.set_params(depth, sss)
-    r.resize_and_clear(W, H)
     setup_s = time.perf_counter() - t_setup
     t0 = time.perf_counter()
     ref, traced = reference_and_traced_counts(r, spp)
     counts_s = time.perf_counter() - t0
     r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
-    r.render(0, spp)
-    r.synchronize()
+    for x in ctxs:
+        x.render(0, spp)
     torch.cuda.synchronize()
-    walls, kt = time_frames(r, spp, steps)
+    if contexts > 1:
+        walls = time_frames_pipelined(ctxs, spp, steps)
+        kt = walls
+        want = r.read_accum().view(np.uint32)
+        for x in ctxs[1:]:
+            if not np.array_equal(x.read_accum().view(np.uint32), want):
+                raise SystemExit(f"bench: {scene_name} leg: the pipelined contexts' frames differ")
+    else:
+        walls, kt = time_frames(r, spp, steps)
     dt = float(np.median(walls)) * 1e-3   # the median frame (min/max beside it)
     kernel_ms = float(np.median(kt)) if kt.size else float("nan")
     alg = algorithmic_bytes({"nodes": ref[1], "leaf_tests": ref[2], "samples": ref[3]})
@@ -327,8 +368,12 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
            "ms_per_frame": spread(walls), "kernel_ms_per_frame": spread(kt) if kt.size else None,
            "kernel": KERNEL_NAMES.get(r.last_kernel(), "?"), "config": cfg,
            "roofline": roofline_block(prof, kernel_ms, alg, KERNEL_NAMES.get(r.last_kernel(), "?"), kernel_ms,
-                                      kernel_ms, int(kt.size), "median kernel_ms (HIP events around each "
-                                                               "frame's launches on the render stream)"),
+                                      kernel_ms, int(kt.size),
+                                      f"median wall ms per frame of runs of {steps} frames alternating over "
+                                      f"{contexts} contexts (frames overlap)" if contexts > 1 else
+                                      "median kernel_ms (HIP events around each frame's launches on the render "
+                                      "stream)"),
+           "contexts": contexts,
            "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
     if prof is not None and prof[1].get("sq_per_launch", {}).get("SQ_INSTS_VALU"):
         # the same frame against the VALU issue peak (committed PMC profile):
@@ -363,9 +408,16 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
     r.set_camera(scenes.DEFAULT_CAMERA)
     ref2, traced2 = reference_and_traced_counts(r, spp)
     r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
-    r.render(0, spp)
-    r.synchronize()
-    walls2, kt2 = time_frames(r, spp, steps)
+    for x in ctxs[1:]:
+        x.set_camera(scenes.DEFAULT_CAMERA)
+    for x in ctxs:
+        x.render(0, spp)
+    torch.cuda.synchronize()
+    if contexts > 1:
+        walls2 = time_frames_pipelined(ctxs, spp, steps)
+        kt2 = walls2
+    else:
+        walls2, kt2 = time_frames(r, spp, steps)
     dt2 = float(np.median(walls2)) * 1e-3
     cfg2 = {"workload": cfg["workload"].replace(desc, desc.split(", camera")[0] + ", camera (0,0,5) fov 60"),
             "rays_per_frame": int(ref2[0])}
@@ -373,28 +425,33 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
     out["reference_camera"] = {"value": round(ref2[0] / dt2 / 1e6, 3), "unit": "Mrays/s",
                                "ms_per_step": round(dt2 * 1e3, 2), "ms_per_frame": spread(walls2),
                                "kernel_ms_per_frame": spread(kt2) if kt2.size else None, "config": cfg2}
-    del r
+    del r, ctxs
     return out
 
 
 # the BASELINE configs that name a multi-GPU run (configs[3]: the Sylveon
 # substitute at 4K 16 spp D8 tile-split with an RCCL accumulation reduce;
 # configs[4]: the 10M cloud's 8-GPU report), timed at N > 1 beside the box
-DIST_SCENE_LEGS = (("config4", "sphere", 3840, 2160, 16, 8, 3),
-                   ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5))
+DIST_SCENE_LEGS = (("config4", "sphere", 3840, 2160, 16, 8, 4),
+                   ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 6))
 
 
-def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, depth, sss, steps):
+def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, depth, sss, steps, contexts=2):
     """One multi-GPU BASELINE config at N = world: every rank renders its
     screen tiles (pt_set_partition) of the frame with the kernel the library
     picks for its share, then one RCCL SUM reduce of the accumulation buffer
     to rank 0 (owned pixels +0-cleared, the others -0: the sum is bit-exact,
-    DESIGN §5).  `steps` frames after one warmup, each bracketed by barrier +
-    synchronize on every rank, the median of the per-frame max over ranks.
-    Rank 0 then renders the whole frame alone with the same context and
-    checks the reduced frame against it bit for bit.  Returns the leg's dict
-    on rank 0 (None elsewhere), or {"error": ...} if any rank failed its
-    setup (then no rank runs a collective of the leg)."""
+    DESIGN §5).  Frames alternate between `contexts` contexts per rank (own
+    stream, accumulation and wavefront buffers each), so a frame's ray rounds
+    run beside the previous frame's drains and its reduce (a 1/8 tile share
+    of config 4 takes 64.2 ms per frame alone, 56.0 ms two in flight,
+    tools/scene_streams.py).  Timed: runs of `steps` frames after one warmup
+    frame per context, each run bracketed by barrier + synchronize on every
+    rank; ms per frame = the run's wall time over its frames, the maximum over
+    ranks, median over runs.  Rank 0 then renders the whole frame alone and
+    checks every context's last reduced frame against it bit for bit.
+    Returns the leg's dict on rank 0 (None elsewhere), or {"error": ...} if
+    any rank failed its setup (then no rank runs a collective of the leg)."""
     import ptamd
     import scenes
     import torch
@@ -402,24 +459,27 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
     dev = torch.device("cuda", device)
     coll = dev if backend == "nccl" else "cpu"
     err = ""
-    r = None
+    ctxs = []   # (renderer, stream, accumulation buffer)
     try:
         scene, cam, int_bits, desc = load_scene(scene_name)
         v, i, n, _, _ = scene.arrays()
         del scene
-        r = ptamd.Renderer(device)
-        r.upload_scene(v, i, n, int_bits=int_bits)
+        for _ in range(contexts):
+            r = ptamd.Renderer(device)
+            r.upload_scene(v, i, n, int_bits=int_bits)
+            r.upload_lights(scenes.REFERENCE_LIGHT)
+            r.set_camera(cam)
+            r.set_params(depth, sss)
+            stream = torch.cuda.Stream(dev)
+            r.set_stream(stream.cuda_stream)
+            r.set_partition(world, rank)
+            if ctxs:
+                r.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 0)
+            frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+            r.bind_accum(frame.data_ptr(), W, H)
+            ctxs.append((r, stream, frame))
         ntri = i.size // 3
         del v, i, n
-        r.upload_lights(scenes.REFERENCE_LIGHT)
-        r.set_camera(cam)
-        r.set_params(depth, sss)
-        stream = torch.cuda.Stream(dev)
-        torch.cuda.set_stream(stream)
-        r.set_stream(stream.cuda_stream)
-        r.set_partition(world, rank)
-        frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
-        r.bind_accum(frame.data_ptr(), W, H)
     except Exception as e:   # noqa: BLE001 -- reported in the line, never a hang of the other ranks
         err = f"rank {rank}: {type(e).__name__}: {e}"
     ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=coll)
@@ -429,10 +489,11 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
             print(f"bench: {scene_name} leg: {err}", file=sys.stderr, flush=True)
         return {"error": err or "another rank failed its setup"} if rank == 0 else None
     setup_s = time.perf_counter() - t_setup
+    r0 = ctxs[0][0]
 
     def reduce_sum(t):
         if backend == "nccl":
-            dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
+            dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)   # the current stream waits for it
         else:
             c = t.cpu()
             dist.reduce(c, dst=0, op=dist.ReduceOp.SUM)
@@ -445,60 +506,61 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
         return t.cpu().numpy()
 
     # reference traceRay calls of the whole frame: each rank counts its share
+    torch.cuda.set_stream(ctxs[0][1])
     t0 = time.perf_counter()
-    mine, traced = reference_and_traced_counts(r, spp)
+    mine, traced = reference_and_traced_counts(r0, spp)
     ref = allreduce(mine, dist.ReduceOp.SUM)
     traced = dict(zip(TRACED_KEYS, (int(x) for x in allreduce([traced[k] for k in TRACED_KEYS],
                                                                  dist.ReduceOp.SUM))))
     counts_s = time.perf_counter() - t0
 
-    def frame_once():
-        r.clear()          # +0 owned, -0 elsewhere
+    def frame_once(j):
+        r, stream, frame = ctxs[j % len(ctxs)]
+        torch.cuda.set_stream(stream)   # the reduce follows this context's render
+        r.clear()                       # +0 owned, -0 elsewhere
         r.render(0, spp)
         reduce_sum(frame)
 
-    frame_once()           # warmup
+    for j in range(len(ctxs)):   # warmup
+        frame_once(j)
     torch.cuda.synchronize(dev)
-    walls, own = [], []
-    for _ in range(steps):
+    walls = []
+    for _ in range(3):
         dist.barrier()
         torch.cuda.synchronize(dev)
-        r.reset_launch_times()
         t0 = time.perf_counter()
-        frame_once()
-        r.synchronize()
+        for j in range(steps):
+            frame_once(j)
         torch.cuda.synchronize(dev)
         dist.barrier()
-        walls.append((time.perf_counter() - t0) * 1e3)
-        kt = r.launch_times_ms()
-        own.append(float(np.sum(kt)) if kt.size else float("nan"))
+        walls.append((time.perf_counter() - t0) * 1e3 / steps)
     wmax = allreduce(walls, dist.ReduceOp.MAX)
-    kmax = allreduce(own, dist.ReduceOp.MAX)
-    kmin = allreduce(own, dist.ReduceOp.MIN)
+    wmin = allreduce(walls, dist.ReduceOp.MIN)
     out = None
     if rank == 0:
-        got = frame.cpu().numpy().reshape(-1).copy()
+        got = [f.cpu().numpy().reshape(-1).copy() for _, _, f in ctxs]
         # the whole frame on this GPU alone, same context and kernels
-        r.set_partition(1, 0)
-        r.clear()
-        r.render(0, spp)
-        r.synchronize()
-        want = r.read_accum()
-        same = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+        r0.set_partition(1, 0)
+        r0.clear()
+        r0.render(0, spp)
+        r0.synchronize()
+        want = r0.read_accum().view(np.uint32)
+        same = all(bool(np.array_equal(g.view(np.uint32), want)) for g in got)
         dt = float(np.median(wmax)) * 1e-3
         cfg = {"workload": f"{desc} {W}x{H} {spp}spp {depth} bounces {sss} sss", "triangles": int(ntri),
                "int_bits_nodes": bool(int_bits), "rays_per_frame": int(ref[0]),
-               "parallelism": f"tiles{world}-reduce (RCCL SUM of the accumulation buffer to rank 0)"}
+               "parallelism": f"tiles{world}-reduce (RCCL SUM of the accumulation buffer to rank 0); "
+                              f"{len(ctxs)} frames in flight per rank"}
         add_traced(cfg, traced, dt)
         out = {"metric": "Mrays/s (reference-equivalent traceRay calls)", "value": round(ref[0] / dt / 1e6, 3),
-               "unit": "Mrays/s", "n_gpus": world, "ms_per_step": round(dt * 1e3, 2), "steps": steps, "warmup": 1,
-               "ms_per_frame": spread(wmax),
-               "rank_render_ms": {"max": spread(kmax), "min": spread(kmin),
-                                  "note": "each rank's render launches (HIP events), slowest and fastest rank"},
-               "kernel": KERNEL_NAMES.get(r.last_kernel(), "?"), "config": cfg,
+               "unit": "Mrays/s", "n_gpus": world, "ms_per_step": round(dt * 1e3, 2), "steps": steps,
+               "warmup": len(ctxs), "ms_per_frame": spread(wmax),
+               "rank_ms_per_frame": {"slowest": spread(wmax), "fastest": spread(wmin),
+                                     "note": "per run of frames, the slowest and the fastest rank"},
+               "kernel": KERNEL_NAMES.get(r0.last_kernel(), "?"), "config": cfg, "contexts": len(ctxs),
                "verified_bitwise_vs_single_gpu": same,
                "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
-    del r
+    del r0, ctxs
     torch.cuda.synchronize(dev)
     dist.barrier()
     return out
@@ -1152,10 +1214,10 @@ def main():
         if world == 1 and emu == 1 and default_cfg and not (args.no_scene_legs or args.profile_run or args.packed):
             del r
             out_line["configs"] = {}
-            for key, scene_name, lw, lh, lspp, ldepth, steps, workload in SCENE_LEGS:
+            for key, scene_name, lw, lh, lspp, ldepth, steps, workload, nctx in SCENE_LEGS:
                 print(f"bench: {key} leg ({scene_name} {lw}x{lh} {lspp}spp D{ldepth})", file=sys.stderr, flush=True)
                 out_line["configs"][key] = scene_leg(scene_name, lw, lh, lspp, ldepth, SSS, steps, device, workload,
-                                                     exhaustive_too=key == "config5")
+                                                     exhaustive_too=key == "config5", contexts=nctx)
         out_line["bench_wall_s"] = round(time.perf_counter() - T_START, 1)
         print(json.dumps(out_line), flush=True)
     if dist is not None:
