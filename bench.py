@@ -436,16 +436,16 @@ DIST_SCENE_LEGS = (("config4", "sphere", 3840, 2160, 16, 8, 4),
                    ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 6))
 
 
-def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, depth, sss, steps, contexts=2):
+def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, depth, sss, steps, contexts=3):
     """One multi-GPU BASELINE config at N = world: every rank renders its
     screen tiles (pt_set_partition) of the frame with the kernel the library
     picks for its share, then one RCCL SUM reduce of the accumulation buffer
     to rank 0 (owned pixels +0-cleared, the others -0: the sum is bit-exact,
     DESIGN §5).  Frames alternate between `contexts` contexts per rank (own
     stream, accumulation and wavefront buffers each), so a frame's ray rounds
-    run beside the previous frame's drains and its reduce (a 1/8 tile share
-    of config 4 takes 64.2 ms per frame alone, 56.0 ms two in flight,
-    tools/scene_streams.py).  Timed: runs of `steps` frames after one warmup
+    run beside the previous frames' drains and reduces (a 1/8 tile share of
+    config 4 takes 64.0 ms per frame alone, 56.7 ms two in flight, 55.3
+    three; config 5 21.9 / 18.7 / 17.7; tools/scene_streams.py).  Timed: runs of `steps` frames after one warmup
     frame per context, each run bracketed by barrier + synchronize on every
     rank; ms per frame = the run's wall time over its frames, the maximum over
     ranks, median over runs.  Rank 0 then renders the whole frame alone and

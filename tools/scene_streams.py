@@ -26,7 +26,7 @@ def main():
     W, H, spp, depth = (3840, 2160, 16, 8) if name.endswith("4k") else (1920, 1080, 8, 4)
     scene, cam = ab_bench.load_scene(name.replace("_4k", ""))
     rs = []
-    for _ in range(2):
+    for _ in range(3):
         r = ptamd.Renderer(0)
         r.upload(scene)
         r.upload_lights(scenes.REFERENCE_LIGHT)
@@ -50,9 +50,11 @@ def main():
         return (time.perf_counter() - t0) / k * 1e3
 
     for rep in range(2):
-        print(f"{name} nr={nr}: one context {run(rs[:1]):.2f} ms/frame, two {run(rs):.2f}", flush=True)
-    a, b = rs[0][0].read_accum(), rs[1][0].read_accum()
-    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+        print(f"{name} nr={nr}: one context {run(rs[:1]):.2f} ms/frame, two {run(rs[:2]):.2f}, "
+              f"three {run(rs):.2f}", flush=True)
+    a = rs[0][0].read_accum()
+    for x in rs[1:]:
+        assert np.array_equal(a.view(np.uint32), x[0].read_accum().view(np.uint32))
     print("frames bitwise equal")
 
 
