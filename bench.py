@@ -854,6 +854,18 @@ def main():
         # with its own stream and accumulation buffer (the same scene, camera
         # and options), so consecutive frames overlap on the GPU; every frame
         # is still a whole frame from batch 0 (bitwise checked after timing)
+        if args.streams > 1:
+            # with frames in flight the tail of a frame is filled by the next
+            # one, so the work granularity that shortened it no longer pays:
+            # one lane per pixel (its samples in order, no colour hand-off
+            # between lanes) and items in scan order, unless --opt says
+            # otherwise.  Box 1080p8 on two contexts: 0.2466 -> 0.2176 ms
+            # (one frame at a time the same options take 0.351 against 0.263)
+            given = {int(kv.partition("=")[0]) for kv in args.opt}
+            for key, val in ((ptamd.PT_OPT_SAMPLE_LANES, 1), (ptamd.PT_OPT_ITEM_ORDER, 0)):
+                if key not in given:
+                    args.opt.append(f"{key}={val}")
+                    r.set_option(key, val)
         for _ in range(args.streams - 1):
             x = ptamd.Renderer(device)
             x.upload_scene(v, i, n, int_bits=int_bits)
@@ -1167,6 +1179,7 @@ def main():
                                           f"single, frames alternating over {len(ctxs)} contexts (one stream and "
                                           "accumulation buffer each)" if pipelined else "single"),
                        "streams": args.streams,
+                       "kernel_options": list(args.opt),
                        "step_loop": ("python" if native is None else
                                      "native (pt_dist_run, RCCL from C++)" if not os.environ.get("PT_RCCL_LIB")
                                      else "native (pt_dist_run, PT_RCCL_LIB stand-in)"),
