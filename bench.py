@@ -262,10 +262,11 @@ def roofline_block(prof, time_ms, alg_bytes, kernel, kernel_ms, interval_ms, n_t
 # the BASELINE configs the default run reports beside the headline, one GPU
 # each: (key, scene, W, H, spp, MAX_DEPTH, timed frames, profile workload)
 # (key, scene, W, H, spp, MAX_DEPTH, timed frames, profile workload,
-# contexts): config 3's frames alternate between two contexts (one frame's
-# ray rounds run beside the other's drains: 44.0 -> 39.1 ms per frame,
-# tools/scene_streams.py); configs 4 and 5 gain nothing from it (+-0.5 %)
-SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 6, "sphere_1080p8", 2),
+# contexts): config 3's frames alternate between three contexts (a frame's
+# ray rounds run beside the others' drains: 43.7 -> 39.4 (two) -> 38.2 ms
+# per frame, tools/scene_streams.py); configs 4 and 5 gain nothing from it
+# (10M cloud: 117.2 / 116.6 / 119.1)
+SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 6, "sphere_1080p8", 3),
               ("config4", "sphere", 3840, 2160, 16, 8, 3, "sphere_4k16_d8", 1),
               ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5, "synthetic10M_1080p8", 1))
 
