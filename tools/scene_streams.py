@@ -33,6 +33,9 @@ def main():
         r.set_camera(cam)
         r.set_params(depth, 3)
         r.set_partition(nr, 0)
+        for kv in filter(None, os.environ.get("PT_SS_OPTS", "").split(",")):   # e.g. "17=0,2=1"
+            key, _, val = kv.partition("=")
+            r.set_option(int(key), int(val))
         r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
         s = torch.cuda.Stream()
         r.set_stream(s.cuda_stream)
