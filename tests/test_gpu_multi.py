@@ -20,19 +20,31 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+# torchrun --standalone binds its rendezvous store to a port of its own
+# choosing (a port picked here and handed over could be taken in between:
+# EADDRINUSE); the single-rank native test sets MASTER_PORT itself.
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A free port below the ephemeral range (32768+), so no client socket
+    of an earlier run can be holding it."""
+    import random
+    for _ in range(200):
+        p = random.randrange(20000, 30000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
+    raise RuntimeError("no free port in 20000-29999")
 
 
 @pytest.mark.parametrize("collective,extra", [("gather", []), ("reduce", []), ("gather", ["--assemble", "0"])])
 def test_two_rank_bench_verifies_bitwise(collective, extra):
     env = dict(os.environ, PT_BENCH_DEVICE="0", PT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "--standalone", "--local-addr", "127.0.0.1",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2", "--verify",
            "--no-scene-legs", "--collective", collective] + extra
     res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
@@ -78,7 +90,7 @@ def test_native_step_loop_two_ranks_grouped_send_recv(streams):
     env = dict(os.environ, PT_BENCH_DEVICE="0", PT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1",
                PT_RCCL_LIB=SHIM)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "--standalone", "--local-addr", "127.0.0.1",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "3", "--verify",
            "--no-scene-legs", "--streams", str(streams)]
     res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
@@ -99,7 +111,7 @@ def test_two_rank_scene_legs_reduce_bitwise():
     env = dict(os.environ, PT_BENCH_DEVICE="0", PT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1",
                PT_BENCH_DIST_LEGS="config4 sphere 640 360 4 8 2;config5 synthetic:300000 480 270 2 4 2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "--standalone", "--local-addr", "127.0.0.1",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1"]
     res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]

@@ -106,11 +106,21 @@ def _reduce_worker(rank, world, port, slots, q):
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A free port below the ephemeral range (32768+), so no client socket
+    of an earlier run can be holding it (a port picked in that range can be
+    taken before the store binds it: EADDRINUSE)."""
+    import random
+    for _ in range(200):
+        p = random.randrange(20000, 30000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
+    raise RuntimeError("no free port in 20000-29999")
 
 
 def _run(worker, world, slots):
