@@ -266,7 +266,7 @@ def roofline_block(prof, time_ms, alg_bytes, kernel, kernel_ms, interval_ms, n_t
 # ray rounds run beside the others' drains: 43.7 -> 39.4 (two) -> 38.2 ms
 # per frame, tools/scene_streams.py); configs 4 and 5 gain nothing from it
 # (10M cloud: 117.2 / 116.6 / 119.1)
-SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 6, "sphere_1080p8", 3),
+SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 12, "sphere_1080p8", 3),
               ("config4", "sphere", 3840, 2160, 16, 8, 3, "sphere_4k16_d8", 1),
               ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5, "synthetic10M_1080p8", 1))
 
@@ -437,8 +437,10 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
 # the BASELINE configs that name a multi-GPU run (configs[3]: the Sylveon
 # substitute at 4K 16 spp D8 tile-split with an RCCL accumulation reduce;
 # configs[4]: the 10M cloud's 8-GPU report), timed at N > 1 beside the box
-DIST_SCENE_LEGS = (("config4", "sphere", 3840, 2160, 16, 8, 4),
-                   ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 6))
+# runs of 9 / 12 frames: with three in flight, the first frame of a run
+# starts alone and the last drains alone
+DIST_SCENE_LEGS = (("config4", "sphere", 3840, 2160, 16, 8, 9),
+                   ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 12))
 
 
 def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, depth, sss, steps, contexts=3):
