@@ -284,6 +284,36 @@ def time_frames(r, spp, steps):
     return np.array(walls), r.launch_times_ms()
 
 
+class HipStream:
+    """A HIP stream made for one context of a frames-in-flight run
+    (hipStreamCreateWithFlags, non-blocking), with a torch view of it
+    (ExternalStream) for collectives that must follow its work.  Streams are
+    given hardware queues as they are created (GPU_MAX_HW_QUEUES, 4 here);
+    torch's pool streams, handed out round-robin, were seen to put two busy
+    contexts on one queue in later legs of a run (config 3: 38.3 ms per frame
+    in the first leg, 40.5 in a later one; two contexts 38.9 vs 43.6), so each
+    context of a leg gets a stream created for it, released with the leg."""
+
+    def __init__(self, device):
+        import ctypes
+        import torch
+        self._hip = ctypes.CDLL("libamdhip64.so")
+        self._hip.hipSetDevice(ctypes.c_int(device))
+        h = ctypes.c_void_p()
+        rc = self._hip.hipStreamCreateWithFlags(ctypes.byref(h), ctypes.c_uint(1))
+        if rc != 0:
+            raise RuntimeError(f"hipStreamCreateWithFlags: error {rc}")
+        self.handle = h.value
+        self.torch = torch.cuda.ExternalStream(self.handle, device=torch.device("cuda", device))
+
+    def close(self):
+        import ctypes
+        if self.handle:
+            self._hip.hipStreamSynchronize(ctypes.c_void_p(self.handle))
+            self._hip.hipStreamDestroy(ctypes.c_void_p(self.handle))
+            self.handle = None
+
+
 def time_frames_pipelined(ctxs, spp, steps, groups=3):
     """`groups` runs of `steps` frames alternating between the contexts with
     no wait in between (frames overlap on the GPU): wall ms per frame of each
@@ -324,6 +354,7 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
     v, i, n, _, _ = scene.arrays()
     del scene
     ctxs = []
+    hip_streams = []
     for _ in range(contexts):
         x = ptamd.Renderer(device)
         x.upload_scene(v, i, n, int_bits=int_bits)
@@ -334,9 +365,11 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
             # the other frames fill a frame's last ray rounds: the tail kernel
             # (PT_OPT_WF_TAIL, for a frame alone) then costs more than it saves
             x.set_option(ptamd.PT_OPT_WF_TAIL, 0)
+        if contexts > 1:
+            hs = HipStream(device)
+            hip_streams.append(hs)
+            x.set_stream(hs.handle)
         if ctxs:
-            xs = torch.cuda.Stream(torch.device("cuda", device))
-            x.set_stream(xs.cuda_stream)
             x.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
             x.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 0)
         x.resize_and_clear(W, H)
@@ -431,6 +464,9 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
                                "ms_per_step": round(dt2 * 1e3, 2), "ms_per_frame": spread(walls2),
                                "kernel_ms_per_frame": spread(kt2) if kt2.size else None, "config": cfg2}
     del r, ctxs
+    torch.cuda.synchronize()
+    for hs in hip_streams:
+        hs.close()
     return out
 
 
@@ -467,6 +503,7 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
     coll = dev if backend == "nccl" else "cpu"
     err = ""
     ctxs = []   # (renderer, stream, accumulation buffer)
+    hip_streams = []
     try:
         scene, cam, int_bits, desc = load_scene(scene_name)
         v, i, n, _, _ = scene.arrays()
@@ -477,8 +514,10 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
             r.upload_lights(scenes.REFERENCE_LIGHT)
             r.set_camera(cam)
             r.set_params(depth, sss)
-            stream = torch.cuda.Stream(dev)
-            r.set_stream(stream.cuda_stream)
+            hs = HipStream(device)   # released with the leg (HipStream)
+            hip_streams.append(hs)
+            stream = hs.torch
+            r.set_stream(hs.handle)
             r.set_partition(world, rank)
             if contexts > 1:
                 # frames in flight fill each other's last ray rounds: no tail
@@ -574,6 +613,9 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
                "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
     del r0, ctxs
     torch.cuda.synchronize(dev)
+    torch.cuda.set_stream(torch.cuda.default_stream(dev))
+    for hs in hip_streams:
+        hs.close()
     dist.barrier()
     return out
 
@@ -889,8 +931,8 @@ def main():
             for kv in args.opt:
                 k, _, val = kv.partition("=")
                 x.set_option(int(k), int(val))
-            xs = torch.cuda.Stream(dev)
-            x.set_stream(xs.cuda_stream)
+            xs = HipStream(device)
+            x.set_stream(xs.handle)
             x.resize_and_clear(W, H)
             ctxs.append(x)
         state1 = {"k": 0}
