@@ -286,23 +286,30 @@ def time_frames(r, spp, steps):
 
 class HipStream:
     """A HIP stream made for one context of a frames-in-flight run
-    (hipStreamCreateWithFlags, non-blocking), with a torch view of it
-    (ExternalStream) for collectives that must follow its work.  Streams are
-    given hardware queues as they are created (GPU_MAX_HW_QUEUES, 4 here);
+    (non-blocking, the least priority), with a torch view of it
+    (ExternalStream) for collectives that must follow its work.  The HIP
+    runtime gives streams hardware queues as they are created, up to
+    GPU_MAX_HW_QUEUES (4 here) per priority, then shares the least-used one;
     torch's pool streams, handed out round-robin, were seen to put two busy
     contexts on one queue in later legs of a run (config 3: 38.3 ms per frame
-    in the first leg, 40.5 in a later one; two contexts 38.9 vs 43.6), so each
-    context of a leg gets a stream created for it, released with the leg."""
+    in the first leg, 40.5 in a later one; two contexts 38.9 vs 43.6).  Each
+    context of a leg gets a stream of the least priority created for it --
+    a queue pool no other stream of the process uses -- released with the
+    leg, so a leg's (at most three) streams get queues of their own."""
 
     def __init__(self, device):
         import ctypes
         import torch
         self._hip = ctypes.CDLL("libamdhip64.so")
         self._hip.hipSetDevice(ctypes.c_int(device))
+        least, greatest = ctypes.c_int(0), ctypes.c_int(0)
+        self._hip.hipDeviceGetStreamPriorityRange(ctypes.byref(least), ctypes.byref(greatest))
         h = ctypes.c_void_p()
-        rc = self._hip.hipStreamCreateWithFlags(ctypes.byref(h), ctypes.c_uint(1))
+        # the least priority: a queue pool of its own, away from torch's
+        # (normal) and RCCL's (high-priority) streams
+        rc = self._hip.hipStreamCreateWithPriority(ctypes.byref(h), ctypes.c_uint(1), least)
         if rc != 0:
-            raise RuntimeError(f"hipStreamCreateWithFlags: error {rc}")
+            raise RuntimeError(f"hipStreamCreateWithPriority: error {rc}")
         self.handle = h.value
         self.torch = torch.cuda.ExternalStream(self.handle, device=torch.device("cuda", device))
 
@@ -903,6 +910,7 @@ def main():
     ingest = None   # the emulated root's stand-in for the gather's receive traffic
     nparts = max(world, emu)
     ctxs = [r]   # N = 1: the contexts frames alternate between
+    box_streams = []   # HipStreams of the N = 1 contexts, closed before the legs
     if dist is None and emu == 1 and not args.packed:
         # args.streams > 1: frames alternate between that many contexts, each
         # with its own stream and accumulation buffer (the same scene, camera
@@ -920,6 +928,12 @@ def main():
                 if key not in given:
                     args.opt.append(f"{key}={val}")
                     r.set_option(key, val)
+            if os.environ.get("PT_BENCH_R_HIPSTREAM", "1") == "1":
+                # every context on a stream of the same (least) priority:
+                # one queue pool, a queue each, none favoured by the dispatcher
+                rs = HipStream(device)
+                box_streams.append(rs)
+                r.set_stream(rs.handle)
         for _ in range(args.streams - 1):
             x = ptamd.Renderer(device)
             x.upload_scene(v, i, n, int_bits=int_bits)
@@ -932,6 +946,7 @@ def main():
                 k, _, val = kv.partition("=")
                 x.set_option(int(k), int(val))
             xs = HipStream(device)
+            box_streams.append(xs)
             x.set_stream(xs.handle)
             x.resize_and_clear(W, H)
             ctxs.append(x)
@@ -1279,7 +1294,13 @@ def main():
         if dist_legs is not None:
             out_line["configs"] = dist_legs
         if world == 1 and emu == 1 and default_cfg and not (args.no_scene_legs or args.profile_run or args.packed):
+            torch.cuda.synchronize(dev)
             del r
+            for c in ctxs:   # the N = 1 contexts go before the legs make theirs
+                c.close()
+            ctxs.clear()
+            for bs in box_streams:
+                bs.close()
             out_line["configs"] = {}
             for key, scene_name, lw, lh, lspp, ldepth, steps, workload, nctx in SCENE_LEGS:
                 print(f"bench: {key} leg ({scene_name} {lw}x{lh} {lspp}spp D{ldepth})", file=sys.stderr, flush=True)
