@@ -890,9 +890,12 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     // 1M cloud 968/930/927/923.  Never more lanes than samples.
     // With frames alternating between two streams (bench.py N > 1), the
     // 1/2 and 1/4 shares favour 4 lanes (0.187 vs 0.210, 0.101 vs 0.110 ms
-    // per step) and the 1/8 share 8 (0.062 vs 0.069).
+    // per step) and the 1/8 share 8 (0.062 vs 0.069).  Round 3's kernels,
+    // the emulated root step on the native loop (tools/r03_share_opts.sh,
+    // two runs each): 1/2 share spl 2/4 = 0.1175/0.1225 ms, 1/4 share 4/8 =
+    // 0.069/0.082, 1/8 share 4/8 = 0.046/0.042.
     const bool small = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
-    int want = (c->nranks >= 8 || !small) ? 8 : 4;
+    int want = (c->nranks >= 8 || !small) ? 8 : (c->nranks == 2 || c->nranks == 3) ? 2 : 4;
     while (want > 1 && (uint32_t)want > n_batches) want >>= 1;
     p.spl = want;
   }
@@ -2392,7 +2395,11 @@ int pt_dist_init(pt_context* c, const void* id, int nranks, int rank) {
   int lo = 0, hi = 0;
   PT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
   PT_HIP(hipStreamCreateWithPriority(&d->own[2], hipStreamNonBlocking, hi));   // gathers take CUs first
-  for (int b = 0; b < 2; ++b) PT_HIP(hipStreamCreateWithFlags(&d->own[b], hipStreamNonBlocking));
+  // the two render streams at the least priority: the HIP runtime gives each
+  // priority its own pool of GPU_MAX_HW_QUEUES hardware queues, so these two
+  // get a queue each instead of sharing one with the process's other streams
+  // (two frames on one queue do not overlap)
+  for (int b = 0; b < 2; ++b) PT_HIP(hipStreamCreateWithPriority(&d->own[b], hipStreamNonBlocking, lo));
   d->streams[0] = d->own[0];
   d->streams[1] = d->own[1];
   d->comm_stream = d->own[2];
