@@ -627,8 +627,9 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
     return out
 
 
-def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light, cam, depth, sss, coll_dev):
-    """RCCL communicator for pt_dist_run and a 4-frame bitwise self-check on
+def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light, cam, depth, sss, coll_dev,
+                 n_streams=2):
+    """RCCL communicator for pt_dist_run and a 6-frame bitwise self-check on
     the root against a single-GPU render; None (every rank) if anything
     fails, so the caller keeps the Python step.  coll_dev: where the
     torch.distributed process group wants its tensors (the GPU for nccl, the
@@ -650,8 +651,10 @@ def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light,
     frames = None
     try:
         r.dist_init(bytes(t[1:].cpu().tolist()), world, rank)
-        frames = torch.full((2, H, W, 4), float("nan"), dtype=torch.float32, device=dev)
-        r.dist_run(spp, 4, frames.data_ptr(), 2, n_streams=1)
+        frames = torch.full((3, H, W, 4), float("nan"), dtype=torch.float32, device=dev)   # up to 3 in flight
+        # six frames on the streams the timed run uses; the last three land in
+        # buffers 0-2 and are each checked below
+        r.dist_run(spp, 6, frames.data_ptr(), 3, n_streams=n_streams)
         try:
             r.dist_wait(30000)   # a hung gather must not hang the bench: abort and fall back
         except ptamd.PTError:
@@ -668,7 +671,7 @@ def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light,
             ref.render(0, spp)
             want = ref.read_accum().view(np.uint32)
             del ref
-            for f in range(2):
+            for f in range(3):
                 if not np.array_equal(frames[f].cpu().numpy().reshape(-1).view(np.uint32), want):
                     ok = 0
     except ptamd.PTError as e:
@@ -683,7 +686,7 @@ def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light,
         except ptamd.PTError:
             pass
         return None
-    return {"frames": frames, "outs": [frames[0], frames[1]]}
+    return {"frames": frames, "outs": list(frames)}
 
 
 class _StreamWork:
@@ -747,9 +750,13 @@ def main():
         # N = 1: the box's 0.27-ms frames alternate between two contexts
         # (double-buffered accumulation, one stream each), so frame k+1 starts
         # while frame k's last workgroups drain (-5.4 %, tools/box_streams.py);
-        # the long large-scene frames gain nothing from it and keep one
-        args.streams = 2 if (int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.packed
-                             or int(os.environ.get("PT_BENCH_EMULATE_RANKS", "1")) > 1 or args.scene == "box") else 1
+        # the long large-scene frames gain nothing from it and keep one.
+        # N > 1: three frames in flight on the native loop's three render
+        # streams (emulated root step, tools/r03_native3.sh: N=8 0.0417 ->
+        # 0.0369 ms, N=4 0.0685 -> 0.0648, N=2 0.119 -> 0.1145 against two)
+        multi = (int(os.environ.get("WORLD_SIZE", "1")) > 1
+                 or int(os.environ.get("PT_BENCH_EMULATE_RANKS", "1")) > 1)
+        args.streams = 3 if multi and not args.packed else 2 if (multi or args.packed or args.scene == "box") else 1
     if args.collective == "reduce":
         args.streams = 1   # the reduce path runs on one stream
     if args.timing_every is None:
@@ -998,7 +1005,7 @@ def main():
         outs = [torch.empty((H, W, 4), dtype=torch.float32, device=dev) for _ in range(args.streams)] if root else None
         out = outs[0] if root else None
         streams = [stream] + [torch.cuda.Stream(dev) for _ in range(args.streams - 1)]
-        state = {"k": 0}
+        state = {"k": 0, "written": set()}   # written: outs indices holding an assembled frame
         # Emulated root (PT_BENCH_EMULATE_RANKS): the other ranks' slots
         # still have to arrive.  A high-priority side stream copies N-1 whole
         # slots into the receive buffer after each render, in one copy as an
@@ -1016,6 +1023,7 @@ def main():
                 work.wait()
             if root:
                 r.items_unpack_all(recv_all[buf].data_ptr(), slot, out.data_ptr())
+                state["written"].add(0)
 
         def step():
             buf = state["k"] % nbuf
@@ -1032,6 +1040,7 @@ def main():
                         work.wait()   # gather of frame k-depth: ran during the frames since
                     if root:
                         fused = (recv_all[pbuf].data_ptr(), slot, outs[sid].data_ptr())
+                        state["written"].add(sid)
                 else:
                     finish(work, pbuf)
             # emulation: the root's own slot is written in place, no transfer
@@ -1069,7 +1078,7 @@ def main():
     # Native step loop (pt_dist_*): the same pipelined sparse gather with the
     # RCCL send/recv issued from C++ -- no Python per frame.  Used for N > 1
     # over RCCL (and PT_BENCH_FORCE_DIST=1 at N = 1) unless PT_BENCH_NATIVE=0.
-    # A 4-frame self-check against a single-GPU render runs first; if the root
+    # A 6-frame self-check against a single-GPU render runs first; if the root
     # finds any bit different, every rank falls back to the Python step.
     # With PT_RCCL_LIB (the one-GPU rehearsal's stand-in for RCCL's
     # point-to-point calls) it runs beside a gloo process group too.
@@ -1077,6 +1086,7 @@ def main():
     if (dist is not None and (backend == "nccl" or os.environ.get("PT_RCCL_LIB")) and args.collective == "gather"
             and args.assemble == 2 and os.environ.get("PT_BENCH_NATIVE", "1") != "0"):
         native = setup_native(r, dist, dev, world, rank, W, H, SPP, v, i, n, int_bits, light, cam, DEPTH, SSS,
+                              n_streams=min(3, args.streams), coll_dev=
                               dev if backend == "nccl" else "cpu")
         if native is not None:
             outs = native["outs"]
@@ -1087,17 +1097,17 @@ def main():
         # N-way partition; the other ranks' slots arrive as a device copy of
         # the same bytes on the high-priority stream (pt_dist_init, emulation)
         r.dist_init(ptamd.Renderer.dist_unique_id(), 1, 0)
-        frames_t = torch.empty((2, H, W, 4), dtype=torch.float32, device=dev)
-        native = {"frames": frames_t, "outs": [frames_t[0], frames_t[1]], "emulated": True}
+        frames_t = torch.empty((3, H, W, 4), dtype=torch.float32, device=dev)   # up to 3 frames in flight
+        native = {"frames": frames_t, "outs": list(frames_t), "emulated": True}
 
     def run_steps(k):
         if native is not None:
-            r.dist_run(SPP, k, native["frames"].data_ptr(), 2, n_streams=min(2, args.streams))
+            r.dist_run(SPP, k, native["frames"].data_ptr(), native["frames"].shape[0], n_streams=min(3, args.streams))
         else:
             for _ in range(k):
                 step()
 
-    if native is not None and os.environ.get("PT_BENCH_NATIVE_TORCH_STREAMS", "1") == "1":
+    if native is not None and os.environ.get("PT_BENCH_NATIVE_TORCH_STREAMS", "0") == "1":
         # the native loop on torch's streams (the Python step's, whose frames
         # measured to overlap), the gather on a high-priority one
         gs = torch.cuda.Stream(dev, priority=-1)
@@ -1188,6 +1198,10 @@ def main():
         want = ref.read_accum()
         # --assemble 2 assembles frames into outs[stream]; 0 and 1 into outs[0]
         frames = (outs if args.assemble == 2 else [out]) if args.collective == "gather" else [frame]
+        if native is None and args.collective == "gather" and args.assemble == 2:
+            # the Python step: only the buffers a fused or trailing assembly wrote
+            frames = [outs[x] for x in sorted(state["written"])]
+            assert frames, "bench --verify: no frame was assembled"
         for f in frames:
             got = f.cpu().numpy().reshape(-1)
             verified = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))

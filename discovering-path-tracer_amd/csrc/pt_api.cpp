@@ -339,15 +339,17 @@ int cull_rects(const float cam[16], int W, int H, const float* lo, const float* 
 // Native multi-GPU step loop state (pt_dist_*): an RCCL communicator of its
 // own, a high-priority stream for the gathers, two render streams (frames
 // alternate), and double-buffered send / receive slots.
-constexpr int kDistSets = 4;   // frame k uses buffer set k % 4 (see pt_dist_run)
+constexpr int kDistStreams = 3;                 // render streams: frames k, k+1, .. in flight
+constexpr int kDistSets = 2 * kDistStreams;     // frame k uses buffer set k % (2 D) (see pt_dist_run)
 struct DistState {
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0;
   hipStream_t comm_stream = nullptr;
-  hipStream_t streams[2] = {nullptr, nullptr};
-  hipStream_t own[3] = {nullptr, nullptr, nullptr};   // created here (pt_dist_set_streams may override)
+  hipStream_t streams[kDistStreams] = {};
+  hipStream_t own[kDistStreams + 1] = {};   // created here: render streams, then the gather stream
+                                            // (pt_dist_set_streams may override)
   hipEvent_t render_done[kDistSets] = {}, gather_done[kDistSets] = {};
-  float* send[2] = {nullptr, nullptr};   // non-root ranks: frame k's live items (k % 2)
+  float* send[kDistStreams] = {};        // non-root ranks: frame k's live items (k % D)
   float* recv[kDistSets] = {};           // root: one slot per rank of the partition; slot 0 its own
   float* ingest = nullptr;               // emulated root: stand-in for the other ranks' slots
   size_t slot_floats = 0, cap_floats = 0;
@@ -2341,13 +2343,13 @@ int dist_layout(pt_context* c) {
   const size_t slot = std::max<size_t>(4, live_max * (size_t)(256 / c->last.spl) * 4);
   const size_t nslots = (size_t)c->nranks;   // the partition's ranks (emulation: > d->nranks)
   if (slot > d->cap_floats) {
-    for (int b = 0; b < 2; ++b)
+    for (int b = 0; b < kDistStreams; ++b)
       for (hipStream_t s : {d->streams[b], d->comm_stream}) PT_HIP(hipStreamSynchronize(s));
-    for (int b = 0; b < 2; ++b) dev_free(d->send[b]);
+    for (int b = 0; b < kDistStreams; ++b) dev_free(d->send[b]);
     for (int b = 0; b < kDistSets; ++b) dev_free(d->recv[b]);
     dev_free(d->ingest);
     d->cap_floats = 0;
-    for (int b = 0; b < 2 && d->rank != 0; ++b) {
+    for (int b = 0; b < kDistStreams && d->rank != 0; ++b) {
       PT_HIP(hipMalloc((void**)&d->send[b], slot * sizeof(float)));
       PT_HIP(hipMemset(d->send[b], 0, slot * sizeof(float)));
     }
@@ -2394,15 +2396,16 @@ int pt_dist_init(pt_context* c, const void* id, int nranks, int rank) {
   d->rank = rank;
   int lo = 0, hi = 0;
   PT_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  PT_HIP(hipStreamCreateWithPriority(&d->own[2], hipStreamNonBlocking, hi));   // gathers take CUs first
+  PT_HIP(hipStreamCreateWithPriority(&d->own[kDistStreams], hipStreamNonBlocking, hi));   // gathers take CUs first
   // the two render streams at the least priority: the HIP runtime gives each
   // priority its own pool of GPU_MAX_HW_QUEUES hardware queues, so these two
   // get a queue each instead of sharing one with the process's other streams
   // (two frames on one queue do not overlap)
-  for (int b = 0; b < 2; ++b) PT_HIP(hipStreamCreateWithPriority(&d->own[b], hipStreamNonBlocking, lo));
-  d->streams[0] = d->own[0];
-  d->streams[1] = d->own[1];
-  d->comm_stream = d->own[2];
+  for (int b = 0; b < kDistStreams; ++b) {
+    PT_HIP(hipStreamCreateWithPriority(&d->own[b], hipStreamNonBlocking, lo));
+    d->streams[b] = d->own[b];
+  }
+  d->comm_stream = d->own[kDistStreams];
   for (int b = 0; b < kDistSets; ++b) {
     PT_HIP(hipEventCreateWithFlags(&d->render_done[b], hipEventDisableTiming));
     PT_HIP(hipEventCreateWithFlags(&d->gather_done[b], hipEventDisableTiming));
@@ -2421,7 +2424,7 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, 
   if (n_frames < 0 || n_batches == 0) return fail(PT_ERR_INVALID, "pt_dist_run: bad frame or batch count");
   if (d->rank == 0 && (!frames || n_frame_bufs < 1 || (((uintptr_t)frames) & 15)))
     return fail(PT_ERR_INVALID, "pt_dist_run: the root needs 16-B aligned frame buffers");
-  if (n_streams != 1 && n_streams != 2) return fail(PT_ERR_INVALID, "pt_dist_run: 1 or 2 streams");
+  if (n_streams < 1 || n_streams > kDistStreams) return fail(PT_ERR_INVALID, "pt_dist_run: 1 to 3 streams");
   const bool emulated = d->nranks == 1 && c->nranks > 1;
   if ((d->nranks != c->nranks && !emulated) || d->rank != c->rank)
     return fail(PT_ERR_INVALID, "partition changed since pt_dist_init");
@@ -2436,29 +2439,31 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, 
   const size_t frame_f = (size_t)c->width * c->height * 4;
   hipStream_t saved = c->stream;
   int rc = PT_OK;
-  // Frame k runs on stream k % 2 (or the one stream) with buffer set k % 4.
-  // Its launch (pt_render_packed) writes this rank's live items -- on the root
-  // straight into its own slot of receive set k % 4, elsewhere into send
-  // slot k % 2 -- and, on the root, assembles frame k-2 from receive set
-  // (k-2) % 4, after waiting for that frame's gather.  Hazards: the gather of
-  // frame k (comm stream, after frame k's launch) overwrites set k % 4, which
-  // frame k-2's launch read -- earlier on frame k's own stream; a send slot
-  // is read by the gather of frame k-2, which frame k's launch waits for.
+  // D = max(2, streams) frames in flight.  Frame k runs on stream k % S
+  // with buffer set k % 2D.  Its launch (pt_render_packed) writes this rank's
+  // live items -- on the root straight into its own slot of receive set
+  // k % 2D, elsewhere into send slot k % D -- and, on the root, assembles
+  // frame k-D from receive set (k-D) % 2D, after waiting for that frame's
+  // gather.  Hazards: the gather of frame k (comm stream, after frame k's
+  // launch) overwrites set k % 2D, which frame k-D's launch read -- earlier
+  // on frame k's own stream (S divides D: S = 1 or D); a send slot is read by
+  // the gather of frame k-D, which frame k's launch waits for.
+  const int D = std::max(2, n_streams), nsets = 2 * D;
   c->in_dist = true;
   for (int k = 0; k < n_frames && rc == PT_OK; ++k) {
-    const int b = k % kDistSets;
-    c->stream = d->streams[n_streams == 2 ? (k & 1) : 0];
+    const int b = k % nsets;
+    c->stream = d->streams[k % n_streams];
     Assembly as;
-    if (k >= 2) {
-      const int pb = (k - 2) % kDistSets;
+    if (k >= D) {
+      const int pb = (k - D) % nsets;
       PT_HIP(hipStreamWaitEvent(c->stream, d->gather_done[pb], 0));
       if (d->rank == 0) {
         as.src = d->recv[pb];
         as.slot_floats = slot;
-        as.frame = (float*)frames + (size_t)((k - 2) % n_frame_bufs) * frame_f;
+        as.frame = (float*)frames + (size_t)((k - D) % n_frame_bufs) * frame_f;
       }
     }
-    rc = render_impl(c, 0, n_batches, (float4*)(d->rank == 0 ? d->recv[b] : d->send[k & 1]), as);
+    rc = render_impl(c, 0, n_batches, (float4*)(d->rank == 0 ? d->recv[b] : d->send[k % D]), as);
     if (rc) break;
     PT_HIP(hipEventRecord(d->render_done[b], c->stream));
     PT_HIP(hipStreamWaitEvent(d->comm_stream, d->render_done[b], 0));
@@ -2471,19 +2476,19 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, 
         for (int r = 1; r < d->nranks; ++r)
           PT_NCCL(R->Recv(d->recv[b] + (size_t)r * slot, slot, ncclFloat32, r, d->comm, d->comm_stream));
       else
-        PT_NCCL(R->Send(d->send[k & 1], slot, ncclFloat32, 0, d->comm, d->comm_stream));
+        PT_NCCL(R->Send(d->send[k % D], slot, ncclFloat32, 0, d->comm, d->comm_stream));
       PT_NCCL(R->GroupEnd());
     }
     PT_HIP(hipEventRecord(d->gather_done[b], d->comm_stream));
   }
   c->in_dist = false;
-  // the root assembles the last (up to) two frames in launches of their own
+  // the root assembles the last (up to) D frames in launches of their own
   if (rc == PT_OK && d->rank == 0) {
     frame_key(c, c->last, &c->key_scratch);
     rc = unpack_table(c, c->last, c->key_scratch);
-    for (int k = std::max(0, n_frames - 2); k < n_frames && rc == PT_OK; ++k) {
-      const int b = k % kDistSets;
-      c->stream = d->streams[n_streams == 2 ? (k & 1) : 0];
+    for (int k = std::max(0, n_frames - D); k < n_frames && rc == PT_OK; ++k) {
+      const int b = k % nsets;
+      c->stream = d->streams[k % n_streams];
       PT_HIP(hipStreamWaitEvent(c->stream, d->gather_done[b], 0));
       float4* out = (float4*)((float*)frames + (size_t)(k % n_frame_bufs) * frame_f);
       PT_HIP(ptd::launch_items_unpack(c->last, out, (const float4*)d->recv[b], slot / 4, c->d_unpack, c->n_unpack,
@@ -2503,10 +2508,10 @@ int pt_dist_set_streams(pt_context* c, void* render0, void* render1, void* comm)
   if (!c || !c->dist) return fail(PT_ERR_INVALID, "pt_dist_set_streams: no communicator (pt_dist_init)");
   DistState* d = c->dist;
   PT_HIP(hipSetDevice(c->device));
-  for (hipStream_t s : {d->streams[0], d->streams[1], d->comm_stream}) PT_HIP(hipStreamSynchronize(s));
+  for (hipStream_t s : {d->streams[0], d->streams[1], d->streams[2], d->comm_stream}) PT_HIP(hipStreamSynchronize(s));
   d->streams[0] = render0 ? (hipStream_t)render0 : d->own[0];
   d->streams[1] = render1 ? (hipStream_t)render1 : d->own[1];
-  d->comm_stream = comm ? (hipStream_t)comm : d->own[2];
+  d->comm_stream = comm ? (hipStream_t)comm : d->own[kDistStreams];
   return PT_OK;
 }
 
@@ -2524,7 +2529,7 @@ int pt_dist_wait(pt_context* c, int timeout_ms) {
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     bool done = true;
-    for (hipStream_t s : {d->streams[0], d->streams[1], d->comm_stream}) {
+    for (hipStream_t s : {d->streams[0], d->streams[1], d->streams[2], d->comm_stream}) {
       const hipError_t q = hipStreamQuery(s);
       if (q == hipErrorNotReady) done = false;
       else if (q != hipSuccess) return fail(PT_ERR_HIP, std::string("pt_dist_wait: ") + hipGetErrorString(q));
@@ -2549,12 +2554,12 @@ int pt_dist_finalize(pt_context* c) {
   DistState* d = c->dist;
   if (!d) return PT_OK;
   (void)hipSetDevice(c->device);
-  for (hipStream_t s : {d->streams[0], d->streams[1], d->comm_stream})
+  for (hipStream_t s : {d->streams[0], d->streams[1], d->streams[2], d->comm_stream})
     if (s) (void)hipStreamSynchronize(s);
   const RcclApi* R = rccl_api();
   if (d->comm && R) (void)R->CommDestroy(d->comm);
   dev_free(d->ingest);
-  for (int b = 0; b < 2; ++b) dev_free(d->send[b]);
+  for (int b = 0; b < kDistStreams; ++b) dev_free(d->send[b]);
   for (hipStream_t s : d->own)
     if (s) (void)hipStreamDestroy(s);
   for (int b = 0; b < kDistSets; ++b) {

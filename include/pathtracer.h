@@ -238,8 +238,9 @@ int pt_partition_items(int width, int height, int sample_lanes, int nranks, int 
  * step on one GPU, nranks = 1 with an N-way partition on rank 0: the other
  * ranks' slots then arrive as a device copy of the same bytes -- an
  * emulation, not a gather); pt_dist_run: n_frames frames of n_batches
- * samples (batch 0..n-1, fresh) on 1 or 2 alternating streams (2: one
- * frame's tail overlaps the next one's head); the root writes frame j
+ * samples (batch 0..n-1, fresh) on 1 to 3 alternating streams (2 or 3: a
+ * frame's tail overlaps the next ones' heads; max(2, n_streams) frames are
+ * in flight before the root assembles one); the root writes frame j
  * to frames + (j % n_frame_bufs) * W*H*4 floats (device memory; ignored on
  * other ranks).  Every rank must have rendered the frame's configuration once
  * with pt_render (it fixes the item layout).  Work is enqueued; the frames
@@ -252,10 +253,12 @@ int pt_dist_init(pt_context* ctx, const void* id, int nranks, int rank);
 int pt_dist_run(pt_context* ctx, uint32_t n_batches, int n_frames, int n_streams, void* frames_device,
                 int n_frame_bufs);
 /* Run the loop on caller-owned streams (e.g. torch streams) instead of the
- * three it creates: two render streams and the gather stream (null keeps
- * the library's own).  With more streams than hardware queues
- * (GPU_MAX_HW_QUEUES) streams share queues, so the caller may know better
- * which ones overlap. */
+ * ones it creates: the first two render streams and the gather stream (null
+ * keeps the library's own; the third render stream is always the
+ * library's).  The library creates its render streams at the least priority
+ * and the gather stream at the greatest: the HIP runtime keeps a pool of
+ * GPU_MAX_HW_QUEUES hardware queues per priority, so each render stream gets
+ * a queue of its own. */
 int pt_dist_set_streams(pt_context* ctx, void* render_stream0, void* render_stream1, void* gather_stream);
 int pt_dist_slot_floats(pt_context* ctx, size_t* slot_floats);
 /* Wait (polling) up to timeout_ms for the loop's streams; PT_ERR_HIP on

@@ -57,15 +57,17 @@ def test_two_rank_bench_verifies_bitwise(collective, extra):
     assert out["config"]["rays_traced"] > 0
 
 
-def test_native_step_loop_single_rank_rccl():
+@pytest.mark.parametrize("streams", [2, 3])
+def test_native_step_loop_single_rank_rccl(streams):
     """pt_dist_run (RCCL driven from C++) at N = 1 on the box: a real RCCL
-    communicator of one rank, the grouped self send/recv, the two-stream
-    pipeline, the fused and the trailing assemblies -- checked bitwise by
-    bench.py's self-check and by --verify over every assembled frame."""
+    communicator of one rank, the grouped self send/recv, the two- or
+    three-stream pipeline (frames k-2 / k-3 assembled in frame k's launch),
+    the fused and the trailing assemblies -- checked bitwise by bench.py's
+    self-check and by --verify over every assembled frame."""
     env = dict(os.environ, PT_BENCH_FORCE_DIST="1", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "7", "--warmup", "3", "--verify",
-           "--no-scene-legs", "--no-cpu-baseline"]
+           "--no-scene-legs", "--no-cpu-baseline", "--streams", str(streams)]
     res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
     out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
@@ -76,14 +78,14 @@ def test_native_step_loop_single_rank_rccl():
 SHIM = os.path.join(ROOT, "tests", "_build", "libptdistshim.so")
 
 
-@pytest.mark.parametrize("streams", [1, 2])
+@pytest.mark.parametrize("streams", [1, 2, 3])
 def test_native_step_loop_two_ranks_grouped_send_recv(streams):
     """pt_dist_run's N > 1 schedule with two processes on the one GPU: the
     grouped ncclSend/ncclRecv of every frame go through the stand-in
     (tests/dist_shim.cpp via PT_RCCL_LIB: the same bytes moved between the
     processes over hipIpc handles), the root receives rank 1's live items
-    into its receive sets and assembles frames k-2 inside its render
-    launches.  bench.py's 4-frame self-check and --verify compare every
+    into its receive sets and assembles frames k-max(2, streams) inside its
+    render launches.  bench.py's 6-frame self-check and --verify compare every
     assembled frame bitwise with a single-GPU render.  (Throughput over xGMI
     is not measured by this: the stand-in is host-synchronous.)"""
     assert os.path.exists(SHIM), "build it first: make -C tests"
