@@ -159,15 +159,18 @@ def cpu_quota():
 def cpu_baseline(v, i, n, cam, light, W, H, spp, DEPTH, SSS):
     """The oracle (scalar C++ restatement of raytrace_comp.comp) on this host,
     on every CPU the process may use, on a bounded sample of the same
-    workload, plus the same traversal on one core."""
+    workload, plus the same traversal on one core.  Returns the baseline
+    block and the oracle's image when the sample is the whole frame (else
+    None): main() checks the timed GPU frame against it bit for bit."""
     import oracle_lib
     threads = cpu_threads()
     stride = 1 if W * H <= 1920 * 1080 else 4
     oracle_lib.render(v, i, n.reshape(-1), cam, light, 64, 64, n_batches=1, nthreads=threads)   # warm
     t0 = time.perf_counter()
-    _, st = oracle_lib.render(v, i, n.reshape(-1), cam, light, W, H, n_batches=spp, max_depth=DEPTH,
+    img, st = oracle_lib.render(v, i, n.reshape(-1), cam, light, W, H, n_batches=spp, max_depth=DEPTH,
                               sss_bounces=SSS, row_stride=stride, row_phase=0, nthreads=threads)
     dt = time.perf_counter() - t0
+    image = img if stride == 1 else None   # the whole frame: the timed frame is checked against it
     # the scalar traversal on one core (SURVEY §8d), on every 16th row of those
     s1 = stride * 16
     t1 = time.perf_counter()
@@ -179,10 +182,10 @@ def cpu_baseline(v, i, n, cam, light, W, H, spp, DEPTH, SSS):
                       f"{int(st[0])} rays, {dt:.2f} s, {threads} std::threads, oracle/pt_oracle.cpp)",
             "host_cpus_visible": os.cpu_count(), "cpus_allowed": threads, "cgroup_cpu_quota": cpu_quota(),
             "single_thread": {"value": round(float(st1[0]) / dt1 / 1e6, 3), "unit": "Mrays/s", "cores": 1,
-                              "sample": f"rows y%{s1}==0 ({int(st1[0])} rays, {dt1:.2f} s)"}}
+                              "sample": f"rows y%{s1}==0 ({int(st1[0])} rays, {dt1:.2f} s)"}}, image
 
 
-KERNEL_NAMES = {1: "render_kernel<false,*>", 2: "render_sm_kernel<false,*>",
+KERNEL_NAMES = {1: "render_kernel<false,*>",
                 3: "wavefront pipeline (wf_gen + wf_trace/wf_shade x rays + wf_fold), per frame"}
 
 TRACED_KEYS = ("closest_walks", "shadow_walks", "nodes", "tri_tests", "primaries")
@@ -284,6 +287,20 @@ def time_frames(r, spp, steps):
     return np.array(walls), r.launch_times_ms()
 
 
+def hip_runtime():
+    """The HIP runtime already mapped into this process (torch's, which
+    libptamd binds to by SONAME), opened with RTLD_NOLOAD: a stream made
+    through another copy of the runtime would not be valid in torch's or
+    libptamd's."""
+    import ctypes
+    with open("/proc/self/maps") as f:
+        for line in f:
+            parts = line.split()
+            if len(parts) >= 6 and os.path.basename(parts[-1]).startswith("libamdhip64.so"):
+                return ctypes.CDLL(parts[-1], mode=os.RTLD_NOLOAD | os.RTLD_GLOBAL)
+    raise RuntimeError("the HIP runtime is not loaded (import torch and initialise its device first)")
+
+
 class HipStream:
     """A HIP stream made for one context of a frames-in-flight run
     (non-blocking, the least priority), with a torch view of it
@@ -300,7 +317,7 @@ class HipStream:
     def __init__(self, device):
         import ctypes
         import torch
-        self._hip = ctypes.CDLL("libamdhip64.so")
+        self._hip = hip_runtime()
         self._hip.hipSetDevice(ctypes.c_int(device))
         least, greatest = ctypes.c_int(0), ctypes.c_int(0)
         self._hip.hipDeviceGetStreamPriorityRange(ctypes.byref(least), ctypes.byref(greatest))
@@ -1107,12 +1124,6 @@ def main():
             for _ in range(k):
                 step()
 
-    if native is not None and os.environ.get("PT_BENCH_NATIVE_TORCH_STREAMS", "0") == "1":
-        # the native loop on torch's streams (the Python step's, whose frames
-        # measured to overlap), the gather on a high-priority one
-        gs = torch.cuda.Stream(dev, priority=-1)
-        native["gather_stream"] = gs
-        r.dist_set_streams(streams[0].cuda_stream, streams[-1].cuda_stream, gs.cuda_stream)
     if native is not None:
         # an event pair around every 4th launch: the native loop's host cost is
         # a handful of HIP calls per frame, and each event record is one of them
@@ -1151,6 +1162,11 @@ def main():
         dt, kernel_ms, interval_ms = float(t[0]), float(t[1]), float(t[2])
     roof_ms = interval_ms if args.streams > 1 else kernel_ms
     pipelined = len(ctxs) > 1
+    # the last timed frame, checked bit for bit against the oracle's frame
+    # (cpu_baseline renders the whole frame) before the line is printed
+    timed_frame = None
+    if world == 1 and emu == 1 and not args.packed and args.collective == "gather":
+        timed_frame = ctxs[0].read_accum()
     if pipelined:
         # frames overlap across the contexts: the GPU time per frame is the
         # wall time per step (the launch events of one context span two frames)
@@ -1303,8 +1319,21 @@ def main():
             out_line["primary_cull_off"] = no_cull
         if verified is not None:
             out_line["verified_bitwise_vs_single_gpu"] = verified
+        oracle_mismatch = None
         if world == 1 and emu == 1 and not args.no_cpu_baseline and not args.profile_run:
-            out_line["cpu_baseline"] = cpu_baseline(v, i, n, cam, light, W, H, SPP, DEPTH, SSS)
+            out_line["cpu_baseline"], oracle_img = cpu_baseline(v, i, n, cam, light, W, H, SPP, DEPTH, SSS)
+            if oracle_img is not None and timed_frame is not None:
+                # raytrace_comp.comp:420-470 as restated by oracle/pt_oracle.cpp,
+                # on the same scene, camera, light and batches as the timed frames
+                bad = np.flatnonzero(timed_frame.view(np.uint32) != oracle_img.view(np.uint32))
+                out_line["verified_vs_oracle"] = bool(bad.size == 0)
+                out_line["verified_vs_oracle_basis"] = (
+                    f"last timed frame of context 0 ({W}x{H}x{SPP}spp, kernel options {list(args.opt)}) bitwise "
+                    "equal to the oracle's whole frame rendered by cpu_baseline")
+                if bad.size:
+                    oracle_mismatch = (f"bench: the timed frame differs from the oracle in {bad.size} floats; first at "
+                                       f"pixel {bad[0] // 4} ch {bad[0] % 4}: {timed_frame[bad[0]]} vs "
+                                       f"{oracle_img[bad[0]]}")
         if dist_legs is not None:
             out_line["configs"] = dist_legs
         if world == 1 and emu == 1 and default_cfg and not (args.no_scene_legs or args.profile_run or args.packed):
@@ -1322,6 +1351,9 @@ def main():
                                                      exhaustive_too=key == "config5", contexts=nctx)
         out_line["bench_wall_s"] = round(time.perf_counter() - T_START, 1)
         print(json.dumps(out_line), flush=True)
+        if oracle_mismatch is not None:
+            print(oracle_mismatch, file=sys.stderr, flush=True)
+            sys.exit(1)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -21,6 +21,7 @@
 
 #include "../../include/pathtracer.h"
 #include "pt_device.h"
+#include "pt_group.h"
 #include "pt_math.h"
 #include "scene/bvh.h"
 #include "scene/camera.h"
@@ -160,60 +161,6 @@ void collapse_implied(const std::vector<float4>& full, std::vector<float4>* out)
   }
 }
 
-// Child-pair records (pt_device.h): one 64-B record per internal node in DFS
-// order, right child first, plus record 0, a virtual parent of the root.
-// Links are validated by thread_bvh first.  *depth = the tree's depth.
-void build_pairs(const pt_bvh_node* nodes, size_t n, bool int_bits, std::vector<float4>* out, int* depth) {
-  auto link = [&](int32_t i, int which) {
-    const float f = which ? nodes[i].max_bounds[3] : nodes[i].min_bounds[3];
-    int32_t v;
-    if (int_bits) memcpy(&v, &f, 4);
-    else v = (int32_t)f;
-    return v;
-  };
-  auto is_leaf = [&](int32_t i) { return link(i, 0) == -1; };
-  std::vector<int32_t> rec(n, -1), order;
-  std::vector<std::pair<int32_t, int>> st{{0, 1}};
-  int maxd = 0;
-  int32_t next = 1;
-  while (!st.empty()) {
-    const auto [v, d] = st.back();
-    st.pop_back();
-    maxd = std::max(maxd, d);
-    if (is_leaf(v)) continue;
-    rec[v] = next++;
-    order.push_back(v);
-    st.push_back({link(v, 0), d + 1});   // left, walked second
-    st.push_back({link(v, 1), d + 1});   // right, walked first
-  }
-  auto child_link = [&](int32_t ch) { return is_leaf(ch) ? ~link(ch, 1) : rec[ch]; };
-  auto same = [&](int32_t a, int32_t b) {
-    return memcmp(nodes[a].min_bounds, nodes[b].min_bounds, 12) == 0 &&
-           memcmp(nodes[a].max_bounds, nodes[b].max_bounds, 12) == 0;
-  };
-  auto bits = [](int32_t v) { float f; memcpy(&f, &v, 4); return f; };
-  out->assign(4 * (size_t)next, make_float4(0, 0, 0, 0));
-  auto put = [&](size_t r, int32_t R, int32_t L, int32_t flags) {
-    const pt_bvh_node& a = nodes[R];
-    (*out)[4 * r + 0] = make_float4(a.min_bounds[0], a.min_bounds[1], a.min_bounds[2], bits(child_link(R)));
-    if (L >= 0) {
-      const pt_bvh_node& b = nodes[L];
-      (*out)[4 * r + 1] = make_float4(a.max_bounds[0], a.max_bounds[1], a.max_bounds[2], bits(child_link(L)));
-      (*out)[4 * r + 2] = make_float4(b.min_bounds[0], b.min_bounds[1], b.min_bounds[2], bits(flags));
-      (*out)[4 * r + 3] = make_float4(b.max_bounds[0], b.max_bounds[1], b.max_bounds[2], 0.0f);
-    } else {
-      (*out)[4 * r + 1] = make_float4(a.max_bounds[0], a.max_bounds[1], a.max_bounds[2], bits(-1));
-      (*out)[4 * r + 2] = make_float4(0.0f, 0.0f, 0.0f, bits(flags | 4));
-    }
-  };
-  put(0, 0, -1, 0);   // virtual parent: the root is tested like any node
-  for (int32_t v : order) {
-    const int32_t R = link(v, 1), L = link(v, 0);
-    put((size_t)rec[v], R, L, (same(R, v) ? 1 : 0) | (same(L, v) ? 2 : 0));
-  }
-  *depth = maxd;
-}
-
 // ---- primary-ray bundle culling -----------------------------
 // Camera model of raytrace_comp.comp:430-460 in the orthonormal camera frame
 // (right, up, ez = dir/|dir|) centred on the camera position, with the
@@ -349,12 +296,14 @@ struct DistState {
   hipStream_t own[kDistStreams + 1] = {};   // created here: render streams, then the gather stream
                                             // (pt_dist_set_streams may override)
   hipEvent_t render_done[kDistSets] = {}, gather_done[kDistSets] = {};
+  hipEvent_t entry[kDistStreams + 1] = {};  // pt_dist_run's entry barrier: each stream's last work
   float* send[kDistStreams] = {};        // non-root ranks: frame k's live items (k % D)
   float* recv[kDistSets] = {};           // root: one slot per rank of the partition; slot 0 its own
   float* ingest = nullptr;               // emulated root: stand-in for the other ranks' slots
   size_t slot_floats = 0, cap_floats = 0;
   std::vector<float> layout_key;         // frame_key of the layout the slots were sized for
   bool ready = false;
+  bool caller_streams = false;           // pt_dist_set_streams gave render streams (then at most 2)
 };
 
 struct pt_context {
@@ -364,8 +313,6 @@ struct pt_context {
   float4* d_nodes = nullptr;        // threaded, implied internal nodes collapsed (fast kernel)
   int n_nodes = 0;
   float4* d_nodes_full = nullptr;   // threaded, every reference node (stats mode)
-  float4* d_pairs = nullptr;        // child-pair records (wavefront walk of device-memory scenes)
-  int pair_depth = 0;               // tree depth (the pair walk's stack holds at most this)
   // culled wide walk (wide_walk.h): nodes, triangle records by rank, rank ->
   // slot, per-lane stack overflow areas (grown on demand)
   float4* d_wide = nullptr;
@@ -375,12 +322,6 @@ struct pt_context {
   int* d_wide_rank_of = nullptr;
   // the 8-wide layout (PT_OPT_WIDE_NODE 80): nodes, triangle records and
   // leaf boxes by leaf position, position -> rank, slot -> position
-  float4* d_w8 = nullptr;
-  float4* d_w8_tris = nullptr;
-  float4* d_w8_leafbox = nullptr;
-  int* d_w8_pos_rank = nullptr;
-  int* d_w8_pos_of = nullptr;
-  int n_w8 = 0, w8_stack = 0;
   int2* d_wide_ovf = nullptr;
   long long wide_ovf_lanes = 0;
   int wide_ovf_stack = 0;   // the stack bound d_wide_ovf was sized for
@@ -417,18 +358,16 @@ struct pt_context {
   int opt_sample_lanes = 0;   // PT_OPT_SAMPLE_LANES: 0 auto, else 1/2/4/8
   int opt_fresh = 0;          // PT_OPT_FRESH_BATCH0
   int opt_item_order = 1;     // PT_OPT_ITEM_ORDER
-  int opt_kernel = 0;         // PT_OPT_KERNEL: 0 auto, 1 path-recursive, 2 lane state machine, 3 wavefront
-  int opt_sm_batch = 1;       // PT_OPT_SM_BATCH
+  int opt_kernel = 0;         // PT_OPT_KERNEL: 0 auto, 1 path-recursive, 3 wavefront
   int opt_cull = 1;           // PT_OPT_PRIMARY_CULL
   int opt_wf_paths = 0;       // PT_OPT_WF_PATHS (0 = 2^27)
   long long wf_fail = 0;      // wavefront paths whose allocation failed (0: none)
   int opt_count = 0;          // PT_OPT_COUNT_TRACED
-  int opt_pairs = 0;          // PT_OPT_PAIRS
   int opt_wide_build = 1;     // PT_OPT_WIDE_BUILD (pt::WideBuild; read at upload)
   int opt_wf_streams = 1;     // PT_OPT_WF_STREAMS (2 measured slower: 10M cloud +9 %, sphere -0.8 %)
   hipStream_t wf_stream2 = nullptr;           // the wavefront pipeline's second half (created on first use)
   hipEvent_t wf_fork = nullptr, wf_join = nullptr;
-  int last_kernel = 0;        // kernel of the last render (1 recursive, 2 state machine, 3 wavefront)
+  int last_kernel = 0;        // kernel of the last render (1 recursive, 3 wavefront)
   // compact-launch item lists (live items, then culled ones), rebuilt when
   // the frame, partition, sample lanes or cull rectangles change
   int* d_items = nullptr;
@@ -495,6 +434,7 @@ struct pt_context {
   long long launch_n = 0;     // render launches since pt_reset_launch_times
   long long ring_launch[kRing] = {};   // launch number of each recorded pair
   DistState* dist = nullptr;           // pt_dist_init
+  pt_group* group = nullptr;           // pt_create_multi: every call goes to the group (pt_group.cpp)
   bool in_dist = false;                // inside pt_dist_run: it records the use events itself
 };
 
@@ -817,8 +757,6 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   if (!c->has_camera) return fail(PT_ERR_INVALID, "no camera set");
   if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
   ptd::RenderParams p;
-  p.pairs = nullptr;   // set below for the wavefront walk
-  p.pair_depth = 0;
   p.wide = nullptr;
   p.wide_tris = nullptr;
   p.wide_rank_of = nullptr;
@@ -830,7 +768,6 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.wf_tail = 0;
   p.wide_qn = 0;
   p.wide_leafbox = nullptr;
-  p.wide_pos_rank = nullptr;
   p.nodes = c->stats_mode ? c->d_nodes_full : c->d_nodes;
   p.tris = c->d_tris;
   p.hit_tris = c->d_tris;
@@ -878,7 +815,6 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.fresh = pack_out ? 1 : c->opt_fresh;
   p.item_order = c->opt_item_order;
   p.pack_out = nullptr;
-  p.sm_batch = c->opt_sm_batch;
   if (c->opt_sample_lanes) {
     p.spl = c->opt_sample_lanes;
   } else {
@@ -908,10 +844,6 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   const bool fits = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
   if (c->opt_scene_lds == 2 && !fits) return fail(PT_ERR_UNSUPPORTED, "scene too large for the LDS variant");
   const bool lds = c->opt_scene_lds == 2 || (c->opt_scene_lds == 1 && fits);
-  // auto: the path-recursive kernel.  The lane state machine is kept as an
-  // option; it was measured slower on every scene (1080p: displaced sphere
-  // 8 spp 1022 vs 596 ms, 1M-triangle cloud 1 spp 191 vs 127 ms).
-  const bool sm = c->opt_kernel == 2;
   // auto: the wavefront pipeline for scenes of at least kWfAutoTris triangles
   // (not LDS-resident) when the launch holds enough paths to keep its node
   // loads in flight, the path-recursive kernel otherwise.  Measured at 1080p
@@ -926,20 +858,18 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   // 20K sphere 2 spp 29.6 -> 23.3; 1M cloud 1 spp 108 -> 47.5; a sparse 100K
   // cloud at 1 spp (most rays miss) loses 14.3 -> 15.9.
   const long long paths = (long long)p.n_tiles * 256 * n_batches;
-  const bool wide_walk = c->opt_wide && c->n_wide > 0 && !c->opt_pairs;
+  const bool wide_walk = c->opt_wide && c->n_wide > 0;
   const bool wf_auto = wide_walk ? c->n_tris >= kWfWideAutoTris && paths >= (1ll << 20)
                                  : c->n_tris >= kWfAutoTris && paths >= (1ll << 20) &&
                                        (c->n_tris >= (1 << 20) || paths >= (1ll << 23));
   const bool wf = c->opt_kernel == 3 || (c->opt_kernel == 0 && !lds && !c->stats_mode && wf_auto);
   if (wf && c->stats_mode) return fail(PT_ERR_UNSUPPORTED, "stats mode runs the path-recursive kernel only");
-  if (sm) p.spl = 1;
   const bool cnt = c->opt_count != 0 && !c->stats_mode;
-  if (cnt && sm) return fail(PT_ERR_UNSUPPORTED, "PT_OPT_COUNT_TRACED: not with the state-machine kernel");
   p.n_cull = -1;
   p.items = nullptr;
   p.culled_items = nullptr;
   p.n_items = p.n_culled_items = 0;
-  if (c->opt_cull && !c->stats_mode && !sm)
+  if (c->opt_cull && !c->stats_mode)
     p.n_cull = cull_rects(c->cam, c->width, c->height, c->root_lo, c->root_hi, c->lights_host.data(),
                           c->n_lights, &p.cull[0][0], ptd::kMaxCullRects);
   if (p.n_cull >= 0) {
@@ -947,8 +877,8 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     if (rc) return rc;
   }
   c->last = p;   // the item exchange (pt_items_*) follows the last rendered frame
-  c->last_kernel = wf ? 3 : sm ? 2 : 1;
-  c->last_valid = !sm;
+  c->last_kernel = wf ? 3 : 1;
+  c->last_valid = true;
   p.unpack_src = nullptr;
   p.unpack_frame = nullptr;
   p.unpack_table = nullptr;
@@ -959,7 +889,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     const std::vector<float>& key = c->key_scratch;
     if (as.src && key != c->packed_key)
       return fail(PT_ERR_INVALID, "pt_render_packed: the frame to assemble has another item layout (size, partition, lanes, culling)");
-    if (wf || sm) {
+    if (wf) {
       // these kernels render into the accumulation buffer: render, pack,
       // then assemble the previous frame in a launch of its own (the calls
       // below rebuild c->key_scratch: keep this frame's key)
@@ -993,7 +923,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.pack_out = pack_out;
   // every launch but the path-recursive render_packed writes the context's
   // accumulation buffer or wavefront buffers
-  const bool shared = !pack_out || wf || sm || c->stats_mode;
+  const bool shared = !pack_out || wf || c->stats_mode;
   if (shared) {
     const int ro = order_shared(c);
     if (ro) return ro;
@@ -1006,14 +936,10 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     if (rc) return rc;
     ptd::WfBuffers b = c->wf;
     b.cap = chunk_paths;   // paths per chunk (the allocation may be larger)
-    if (c->opt_pairs && c->d_pairs && c->pair_depth <= 32) {
-      p.pairs = c->d_pairs;
-      p.pair_depth = std::max(1, c->pair_depth);
-    } else if (c->opt_wide && c->n_wide > 0 && !lds) {
+    if (c->opt_wide && c->n_wide > 0 && !lds) {
       const long long lanes = ptd::wide_trace_lanes();
       if (lanes <= 0) return fail(PT_ERR_HIP, "wide walk: occupancy query failed");
-      const bool w8 = c->opt_wide_node == 80 && c->n_w8 > 0;
-      const int stack = w8 ? c->w8_stack : c->wide_stack;
+      const int stack = c->wide_stack;
       if (lanes > c->wide_ovf_lanes || stack > c->wide_ovf_stack) {   // every lane of the grid gets its area
         { const int rc_ = quiesce(c); if (rc_) return rc_; }
         dev_free(c->d_wide_ovf);
@@ -1023,22 +949,13 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
         c->wide_ovf_lanes = lanes;
         c->wide_ovf_stack = stack;
       }
-      if (w8) {   // closest hits come back as leaf positions
-        p.wide_qn = 2;
-        p.wide = c->d_w8;
-        p.wide_leafbox = c->d_w8_leafbox;
-        p.wide_tris = c->d_w8_tris;
-        p.wide_rank_of = c->d_w8_pos_of;
-        p.wide_pos_rank = c->d_w8_pos_rank;
-        p.hit_tris = c->d_w8_tris;
-      } else {    // ... as ranks
-        p.wide_qn = c->opt_wide_node == 64 ? 1 : 0;
-        p.wide = p.wide_qn ? c->d_wide_q : c->d_wide;
-        p.wide_leafbox = c->d_wide_leafbox;
-        p.wide_tris = c->d_wide_tris;
-        p.wide_rank_of = c->d_wide_rank_of;
-        p.hit_tris = c->d_wide_tris;
-      }
+      // closest hits come back as leaf ranks
+      p.wide_qn = c->opt_wide_node == 64 ? 1 : 0;
+      p.wide = p.wide_qn ? c->d_wide_q : c->d_wide;
+      p.wide_leafbox = c->d_wide_leafbox;
+      p.wide_tris = c->d_wide_tris;
+      p.wide_rank_of = c->d_wide_rank_of;
+      p.hit_tris = c->d_wide_tris;
       p.wide_ovf = c->d_wide_ovf;
       p.wide_ovf_lanes = c->wide_ovf_lanes;
       p.wide_stack = stack;
@@ -1052,7 +969,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
       // 384.89, 117.72 -> 117.39 ms.  (2^20: 11.17 / 65.31 / 22.39; from the
       // first list: +28-57 % on whole frames.)
       const int tail_auto = 400000;
-      p.wf_tail = w8 ? 0 : c->opt_wf_tail >= 0 ? c->opt_wf_tail : tail_auto;
+      p.wf_tail = c->opt_wf_tail >= 0 ? c->opt_wf_tail : tail_auto;
     }
     if (c->opt_wf_streams == 2 && !c->wf_stream2) {
       PT_HIP(hipStreamCreateWithFlags(&c->wf_stream2, hipStreamNonBlocking));
@@ -1062,7 +979,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     const bool two = c->opt_wf_streams == 2;
     PT_HIP(ptd::launch_wavefront(p, b, lds, c->stream, cnt, two ? c->wf_stream2 : nullptr, c->wf_fork, c->wf_join));
   } else {
-    PT_HIP(ptd::launch_render(p, c->stats_mode, lds, sm, c->stream, cnt));
+    PT_HIP(ptd::launch_render(p, c->stats_mode, lds, c->stream, cnt));
   }
   if (shared) {
     const int rm = mark_shared(c);
@@ -1083,6 +1000,8 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
 }
 
 }  // namespace
+
+int pt_fail_internal(int code, const std::string& msg) { return fail(code, msg); }
 
 extern "C" {
 
@@ -1123,8 +1042,37 @@ int pt_create(int device_ordinal, pt_context** out) {
 
 int pt_dist_finalize(pt_context* c);
 
+int pt_create_multi(const int* device_ordinals, int n, pt_context** out) {
+  if (!out || !device_ordinals) return fail(PT_ERR_INVALID, "null argument");
+  *out = nullptr;
+  pt_group* g = nullptr;
+  const int rc = ptg::make(device_ordinals, n, &g);
+  if (rc) return rc;
+  pt_context* c = new pt_context();
+  c->device = device_ordinals[0];
+  c->group = g;
+  *out = c;
+  return PT_OK;
+}
+
+int pt_group_info(pt_context* c, int* n_devices, int* devices, int max_devices, int* peer_stores) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  if (!c->group) {
+    if (n_devices) *n_devices = 1;
+    if (devices && max_devices > 0) devices[0] = c->device;
+    if (peer_stores) *peer_stores = 0;
+    return PT_OK;
+  }
+  return ptg::members(c->group, n_devices, devices, max_devices, peer_stores);
+}
+
 int pt_destroy(pt_context* c) {
   if (!c) return PT_OK;
+  if (c->group) {   // a multi-device context: its members and buffers
+    (void)ptg::destroy(c->group);
+    delete c;
+    return PT_OK;
+  }
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->wf_stream2) (void)hipStreamSynchronize(c->wf_stream2);
@@ -1134,17 +1082,11 @@ int pt_destroy(pt_context* c) {
   c->uses.clear();
   dev_free(c->d_nodes);
   dev_free(c->d_nodes_full);
-  dev_free(c->d_pairs);
   dev_free(c->d_wide);
   dev_free(c->d_wide_q);
   dev_free(c->d_wide_leafbox);
   dev_free(c->d_wide_tris);
   dev_free(c->d_wide_rank_of);
-  dev_free(c->d_w8);
-  dev_free(c->d_w8_tris);
-  dev_free(c->d_w8_leafbox);
-  dev_free(c->d_w8_pos_rank);
-  dev_free(c->d_w8_pos_of);
   dev_free(c->d_wide_ovf);
   dev_free(c->d_tris);
   dev_free(c->d_lights);
@@ -1176,12 +1118,14 @@ int pt_destroy(pt_context* c) {
 }
 
 int pt_set_stream(pt_context* c, void* s) {
+  if (c && c->group) return ptg::set_stream(c->group, s);
   if (!c) return fail(PT_ERR_INVALID, "null context");
   c->stream = s ? (hipStream_t)s : c->own_stream;
   return PT_OK;
 }
 
 int pt_synchronize(pt_context* c) {
+  if (c && c->group) return ptg::synchronize(c->group);
   if (!c) return fail(PT_ERR_INVALID, "null context");
   PT_HIP(hipSetDevice(c->device));
   PT_HIP(hipStreamSynchronize(c->stream));
@@ -1195,6 +1139,7 @@ int pt_synchronize(pt_context* c) {
 int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats, const uint32_t* indices,
                     size_t n_indices, const pt_bvh_node* nodes, size_t n_nodes, const float* uvs,
                     size_t n_uv_floats, const uint32_t* mat_indices, size_t n_mat, uint32_t flags) {
+  if (c && c->group) return ptg::upload_scene(c->group, vertices, n_vertex_floats, indices, n_indices, nodes, n_nodes, uvs, n_uv_floats, mat_indices, n_mat, flags);
   if (!c) return fail(PT_ERR_INVALID, "null context");
   if (!vertices || !indices || !nodes) return fail(PT_ERR_INVALID, "null scene array");
   if (n_vertex_floats % 3 || n_indices % 3 || n_indices == 0)
@@ -1211,9 +1156,6 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   int rc = thread_bvh(nodes, n_nodes, (flags & PT_NODES_INT_BITS) != 0, n_indices / 3, &threaded);
   if (rc) return rc;
   collapse_implied(threaded, &collapsed);
-  std::vector<float4> pairs;
-  int pair_depth = 0;
-  build_pairs(nodes, n_nodes, (flags & PT_NODES_INT_BITS) != 0, &pairs, &pair_depth);
   pt::WideBVH wide;
   const std::string wide_reason =
       pt::build_wide_bvh((const float*)nodes, n_nodes, (flags & PT_NODES_INT_BITS) != 0, vertices, n_vertex_floats,
@@ -1224,17 +1166,11 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   { const int rc_ = quiesce(c); if (rc_) return rc_; }
   dev_free(c->d_nodes);
   dev_free(c->d_nodes_full);
-  dev_free(c->d_pairs);
   dev_free(c->d_wide);
   dev_free(c->d_wide_q);
   dev_free(c->d_wide_leafbox);
   dev_free(c->d_wide_tris);
   dev_free(c->d_wide_rank_of);
-  dev_free(c->d_w8);
-  dev_free(c->d_w8_tris);
-  dev_free(c->d_w8_leafbox);
-  dev_free(c->d_w8_pos_rank);
-  dev_free(c->d_w8_pos_of);
   dev_free(c->d_tris);
   // the wide walk's overflow area is sized by the scene's stack bound: a
   // deeper tree needs a new one (it is reallocated at the next wide launch)
@@ -1242,7 +1178,6 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   c->wide_ovf_lanes = 0;
   c->wide_ovf_stack = 0;
   c->n_wide = 0;
-  c->n_w8 = 0;
   c->has_scene = false;
   const int T = (int)(n_indices / 3);
   struct Staging {   // vertex/index copies live only until the triangle records are built
@@ -1259,8 +1194,6 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   PT_HIP(hipMalloc((void**)&c->d_nodes, collapsed.size() * sizeof(float4)));
   PT_HIP(hipMalloc((void**)&c->d_nodes_full, threaded.size() * sizeof(float4)));
   PT_HIP(hipMalloc((void**)&c->d_tris, (size_t)T * 3 * sizeof(float4)));
-  PT_HIP(hipMalloc((void**)&c->d_pairs, pairs.size() * sizeof(float4)));
-  PT_HIP(hipMemcpyAsync(c->d_pairs, pairs.data(), pairs.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
   PT_HIP(hipMalloc((void**)&st.v, n_vertex_floats * sizeof(float) + 16));
   PT_HIP(hipMalloc((void**)&st.i, n_indices * sizeof(uint32_t)));
   PT_HIP(hipMemcpyAsync(c->d_nodes, collapsed.data(), collapsed.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
@@ -1289,41 +1222,12 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
     PT_HIP(hipMemcpyAsync(c->d_wide_rank_of, rank_of_host.data(), (size_t)T * sizeof(int), hipMemcpyHostToDevice,
                           c->stream));
   }
-  std::vector<int> pos_slot, pos_of_host;
-  const bool w8 = wide_reason.empty() && wide.w8_reason.empty();
-  if (w8) {
-    pos_slot.resize((size_t)T);
-    pos_of_host.resize((size_t)T);
-    for (int q = 0; q < T; ++q) {
-      pos_slot[q] = wide.rank_tri[wide.w8_pos_rank[q]];
-      pos_of_host[pos_slot[q]] = q;
-    }
-    PT_HIP(hipMalloc((void**)&c->d_w8, wide.w8nodes.size() * sizeof(float)));
-    PT_HIP(hipMalloc((void**)&c->d_w8_leafbox, wide.w8_leaf_box.size() * sizeof(float)));
-    PT_HIP(hipMalloc((void**)&c->d_w8_pos_rank, (size_t)T * sizeof(int)));
-    PT_HIP(hipMalloc((void**)&c->d_w8_pos_of, (size_t)T * sizeof(int)));
-    PT_HIP(hipMalloc((void**)&c->d_w8_tris, (size_t)T * 3 * sizeof(float4)));
-    PT_HIP(hipMemcpyAsync(c->d_w8, wide.w8nodes.data(), wide.w8nodes.size() * sizeof(float), hipMemcpyHostToDevice,
-                          c->stream));
-    PT_HIP(hipMemcpyAsync(c->d_w8_leafbox, wide.w8_leaf_box.data(), wide.w8_leaf_box.size() * sizeof(float),
-                          hipMemcpyHostToDevice, c->stream));
-    PT_HIP(hipMemcpyAsync(c->d_w8_pos_rank, wide.w8_pos_rank.data(), (size_t)T * sizeof(int), hipMemcpyHostToDevice,
-                          c->stream));
-    // position -> slot first (the gather's map), then slot -> position
-    PT_HIP(hipMemcpyAsync(c->d_w8_pos_of, pos_slot.data(), (size_t)T * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    PT_HIP(ptd::launch_gather_tris(c->d_tris, c->d_w8_pos_of, T, c->d_w8_tris, c->stream));
-    PT_HIP(hipMemcpyAsync(c->d_w8_pos_of, pos_of_host.data(), (size_t)T * sizeof(int), hipMemcpyHostToDevice,
-                          c->stream));
-  }
   PT_HIP(hipStreamSynchronize(c->stream));
   c->n_wide = wide_reason.empty() ? wide.n_nodes : 0;
   c->wide_stack = wide.stack_cap;
-  c->n_w8 = w8 ? wide.w8_n_nodes : 0;
-  c->w8_stack = w8 ? wide.w8_stack_cap : 0;
   c->wide_reason = wide_reason;
   c->n_nodes = (int)(collapsed.size() / 2) - 1;
   c->n_nodes_full = (int)(threaded.size() / 2) - 1;
-  c->pair_depth = pair_depth;
   c->n_tris = T;
   memcpy(c->root_lo, lo, sizeof lo);
   memcpy(c->root_hi, hi, sizeof hi);
@@ -1332,6 +1236,7 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
 }
 
 int pt_upload_lights(pt_context* c, const pt_area_light* lights, size_t n) {
+  if (c && c->group) return ptg::upload_lights(c->group, lights, n);
   if (!c) return fail(PT_ERR_INVALID, "null context");
   if (n && !lights) return fail(PT_ERR_INVALID, "null lights");
   if (n > 1024) return fail(PT_ERR_UNSUPPORTED, "more than 1024 lights");
@@ -1354,6 +1259,7 @@ int pt_upload_lights(pt_context* c, const pt_area_light* lights, size_t n) {
 }
 
 int pt_set_camera(pt_context* c, const float ubo[16]) {
+  if (c && c->group) return ptg::set_camera(c->group, ubo);
   if (!c || !ubo) return fail(PT_ERR_INVALID, "null argument");
   memcpy(c->cam, ubo, sizeof c->cam);
   c->has_camera = true;
@@ -1361,6 +1267,7 @@ int pt_set_camera(pt_context* c, const float ubo[16]) {
 }
 
 int pt_set_params(pt_context* c, const pt_params* p) {
+  if (c && c->group) return ptg::set_params(c->group, p);
   if (!c || !p) return fail(PT_ERR_INVALID, "null argument");
   if (p->max_depth < 0 || p->max_depth > 64 || p->sss_bounces < 0 || p->sss_bounces > 64)
     return fail(PT_ERR_INVALID, "max_depth and sss_bounces must be in [0,64]");
@@ -1369,6 +1276,7 @@ int pt_set_params(pt_context* c, const pt_params* p) {
 }
 
 int pt_set_partition(pt_context* c, int nranks, int rank) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_set_partition: not on a multi-device context (pt_create_multi)");
   if (!c) return fail(PT_ERR_INVALID, "null context");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(PT_ERR_INVALID, "bad partition");
   c->nranks = nranks;
@@ -1380,6 +1288,7 @@ int pt_set_partition(pt_context* c, int nranks, int rank) {
 }
 
 int pt_set_partition_slots(pt_context* c, int nranks, int rank, const int* slots) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_set_partition_slots: not on a multi-device context (pt_create_multi)");
   if (!c || !slots) return fail(PT_ERR_INVALID, "null argument");
   if (nranks < 1 || rank < 0 || rank >= nranks) return fail(PT_ERR_INVALID, "bad partition");
   long long m = 0;
@@ -1397,6 +1306,7 @@ int pt_set_partition_slots(pt_context* c, int nranks, int rank, const int* slots
 }
 
 int pt_clear_accum(pt_context* c) {
+  if (c && c->group) return ptg::clear_accum(c->group);
   if (!c) return fail(PT_ERR_INVALID, "null context");
   if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
   PT_HIP(hipSetDevice(c->device));
@@ -1412,6 +1322,7 @@ int pt_clear_accum(pt_context* c) {
 }
 
 int pt_resize_and_clear(pt_context* c, int w, int h) {
+  if (c && c->group) return ptg::resize_and_clear(c->group, w, h);
   if (!c) return fail(PT_ERR_INVALID, "null context");
   if (w <= 0 || h <= 0 || (long long)w * h > (1ll << 31)) return fail(PT_ERR_INVALID, "bad resolution");
   PT_HIP(hipSetDevice(c->device));
@@ -1429,6 +1340,7 @@ int pt_resize_and_clear(pt_context* c, int w, int h) {
 }
 
 int pt_bind_accum(pt_context* c, void* ptr, int w, int h) {
+  if (c && c->group) return ptg::bind_accum(c->group, ptr, w, h);
   if (!c || !ptr) return fail(PT_ERR_INVALID, "null argument");
   if (w <= 0 || h <= 0) return fail(PT_ERR_INVALID, "bad resolution");
   if (((uintptr_t)ptr) & 15) return fail(PT_ERR_INVALID, "accumulation buffer must be 16-B aligned");
@@ -1442,9 +1354,13 @@ int pt_bind_accum(pt_context* c, void* ptr, int w, int h) {
   return PT_OK;
 }
 
-void* pt_accum_device_ptr(pt_context* c) { return c ? (void*)c->d_accum : nullptr; }
+void* pt_accum_device_ptr(pt_context* c) {
+  if (c && c->group) return ptg::accum_device_ptr(c->group);
+  return c ? (void*)c->d_accum : nullptr;
+}
 
 int pt_read_accum(pt_context* c, float* rgba, size_t n) {
+  if (c && c->group) return ptg::read_accum(c->group, rgba, n);
   if (!c || !rgba) return fail(PT_ERR_INVALID, "null argument");
   if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
   const size_t need = (size_t)c->width * c->height * 4;
@@ -1458,6 +1374,7 @@ int pt_read_accum(pt_context* c, float* rgba, size_t n) {
 }
 
 int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
+  if (c && c->group) return ptg::render(c->group, first_batch, n_batches);
   return render_impl(c, first_batch, n_batches, nullptr);
 }
 
@@ -1467,6 +1384,7 @@ int pt_render(pt_context* c, uint32_t first_batch, uint32_t n_batches) {
 // traffic.  The accumulation buffer is neither read nor written.
 int pt_render_packed(pt_context* c, uint32_t n_batches, void* packed, const void* gathered, size_t slot_floats,
                      void* frame) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_render_packed: not on a multi-device context (pt_create_multi)");
   if (!c || !packed) return fail(PT_ERR_INVALID, "null argument");
   if (((uintptr_t)packed) & 15) return fail(PT_ERR_INVALID, "packed buffer must be 16-B aligned");
   if (c->stats_mode) return fail(PT_ERR_UNSUPPORTED, "stats mode renders into the accumulation buffer");
@@ -1494,6 +1412,7 @@ int pt_dispatch(pt_context* c, uint32_t sample_batch) { return pt_render(c, samp
 // copies it to pinned host memory on a second stream, so rendering goes on
 // while the previous frame travels over PCIe.
 int pt_progressive_camera(pt_context* c, const float ubo[16], int* reset) {
+  if (c && c->group) return ptg::progressive_camera(c->group, ubo, reset);
   if (!c || !ubo) return fail(PT_ERR_INVALID, "null argument");
   const bool changed = !c->prog_has_cam || memcmp(ubo, c->prog_cam, sizeof c->prog_cam) != 0;
   if (changed) {
@@ -1508,6 +1427,7 @@ int pt_progressive_camera(pt_context* c, const float ubo[16], int* reset) {
 }
 
 int pt_progressive_advance(pt_context* c, uint32_t max_new, uint32_t limit, uint32_t* first, uint32_t* count) {
+  if (c && c->group) return ptg::progressive_advance(c->group, max_new, limit, first, count);
   if (!c) return fail(PT_ERR_INVALID, "null context");
   if (!c->prog_has_cam) return fail(PT_ERR_INVALID, "no camera (pt_progressive_camera)");
   const uint32_t room = limit > c->prog_batch ? limit - c->prog_batch : 0u;
@@ -1522,6 +1442,7 @@ int pt_progressive_advance(pt_context* c, uint32_t max_new, uint32_t limit, uint
 }
 
 int pt_readback_begin(pt_context* c, int* ticket) {
+  if (c && c->group) return ptg::readback_begin(c->group, ticket);
   if (!c || !ticket) return fail(PT_ERR_INVALID, "null argument");
   if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
   PT_HIP(hipSetDevice(c->device));
@@ -1563,6 +1484,7 @@ int pt_readback_begin(pt_context* c, int* ticket) {
 }
 
 int pt_readback_end(pt_context* c, int ticket, float* rgba, size_t n) {
+  if (c && c->group) return ptg::readback_end(c->group, ticket, rgba, n);
   if (!c || !rgba) return fail(PT_ERR_INVALID, "null argument");
   for (auto& r : c->rb) {
     if (r.ticket != ticket || ticket == 0) continue;
@@ -1578,16 +1500,19 @@ int pt_readback_end(pt_context* c, int ticket, float* rgba, size_t n) {
 }
 
 int pt_last_kernel(pt_context* c, int* kernel) {
+  if (c && c->group) return ptg::last_kernel(c->group, kernel);
   if (!c || !kernel) return fail(PT_ERR_INVALID, "null argument");
   *kernel = c->last_kernel;
   return PT_OK;
 }
 
 int pt_set_option(pt_context* c, int key, int value) {
+  if (c && c->group) return ptg::set_option(c->group, key, value);
   if (!c) return fail(PT_ERR_INVALID, "null context");
   switch (key) {
     case PT_OPT_KERNEL:
-      if (value < 0 || value > 3) return fail(PT_ERR_INVALID, "PT_OPT_KERNEL takes 0, 1, 2 or 3");
+      if (value == 2) return fail(PT_ERR_UNSUPPORTED, "PT_OPT_KERNEL 2 (lane state machine) was removed: slower on every scene");
+      if (value < 0 || value > 3) return fail(PT_ERR_INVALID, "PT_OPT_KERNEL takes 0, 1 or 3");
       c->opt_kernel = value;
       return PT_OK;
     case PT_OPT_WIDE:
@@ -1595,8 +1520,8 @@ int pt_set_option(pt_context* c, int key, int value) {
       c->opt_wide = value;
       return PT_OK;
     case PT_OPT_WIDE_NODE:
-      if (value != 64 && value != 80 && value != 128)
-        return fail(PT_ERR_INVALID, "PT_OPT_WIDE_NODE takes 64, 80 or 128");
+      if (value == 80) return fail(PT_ERR_UNSUPPORTED, "PT_OPT_WIDE_NODE 80 (8-wide nodes) was removed: slower on every scene");
+      if (value != 64 && value != 128) return fail(PT_ERR_INVALID, "PT_OPT_WIDE_NODE takes 64 or 128");
       c->opt_wide_node = value;
       return PT_OK;
     case PT_OPT_WF_FUSE:
@@ -1616,8 +1541,8 @@ int pt_set_option(pt_context* c, int key, int value) {
       c->opt_wide_build = value;
       return PT_OK;
     case PT_OPT_PAIRS:
-      if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_PAIRS takes 0 or 1");
-      c->opt_pairs = value;
+      if (value == 1) return fail(PT_ERR_UNSUPPORTED, "PT_OPT_PAIRS 1 (child-pair records) was removed: slower on every scene");
+      if (value != 0) return fail(PT_ERR_INVALID, "PT_OPT_PAIRS takes 0");
       return PT_OK;
     case PT_OPT_COUNT_TRACED:
       if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_COUNT_TRACED takes 0 or 1");
@@ -1632,9 +1557,7 @@ int pt_set_option(pt_context* c, int key, int value) {
       c->opt_wf_paths = value;
       return PT_OK;
     case PT_OPT_SM_BATCH:
-      if (value < 1 || value > 64) return fail(PT_ERR_INVALID, "PT_OPT_SM_BATCH takes 1..64");
-      c->opt_sm_batch = value;
-      return PT_OK;
+      return fail(PT_ERR_UNSUPPORTED, "PT_OPT_SM_BATCH: the lane state-machine kernel was removed");
     case PT_OPT_LAUNCH_TIMING:
       if (value < 0) return fail(PT_ERR_INVALID, "PT_OPT_LAUNCH_TIMING takes 0 (off) or k >= 1 (every k-th launch)");
       c->opt_timing = value;
@@ -1662,6 +1585,7 @@ int pt_set_option(pt_context* c, int key, int value) {
 }
 
 int pt_tiles_owned(pt_context* c, int* n_tiles) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_tiles_owned: not on a multi-device context (pt_create_multi)");
   if (!c || !n_tiles) return fail(PT_ERR_INVALID, "null argument");
   if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
   *n_tiles = ptd::owned_tiles(c->width, c->height, part_of(c, c->rank));
@@ -1669,6 +1593,7 @@ int pt_tiles_owned(pt_context* c, int* n_tiles) {
 }
 
 int pt_tiles_pack(pt_context* c, void* dst) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_tiles_pack: not on a multi-device context (pt_create_multi)");
   if (!c || !dst) return fail(PT_ERR_INVALID, "null argument");
   if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer");
   PT_HIP(hipSetDevice(c->device));
@@ -1684,6 +1609,7 @@ int pt_tiles_pack(pt_context* c, void* dst) {
 }
 
 int pt_tiles_unpack(pt_context* c, const void* src, int src_rank, void* frame) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_tiles_unpack: not on a multi-device context (pt_create_multi)");
   if (!c || !src || !frame) return fail(PT_ERR_INVALID, "null argument");
   if (!c->d_accum) return fail(PT_ERR_INVALID, "no accumulation buffer (it sets the frame size)");
   if (src_rank < 0 || src_rank >= c->nranks) return fail(PT_ERR_INVALID, "src_rank out of range");
@@ -1701,6 +1627,7 @@ int pt_tiles_unpack(pt_context* c, const void* src, int src_rank, void* frame) {
 // ---- sparse tile exchange (live items only) --------------------------------
 
 int pt_items_live(pt_context* c, int rank, int* n_items, int* item_pixels) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_items_live: not on a multi-device context (pt_create_multi)");
   if (!c || !n_items || !item_pixels) return fail(PT_ERR_INVALID, "null argument");
   if (!c->last_valid) return fail(PT_ERR_INVALID, "no path-recursive pt_render yet");
   if (rank < 0 || rank >= c->last.nranks || rank >= (int)c->slots.size()) return fail(PT_ERR_INVALID, "rank out of range");
@@ -1712,6 +1639,7 @@ int pt_items_live(pt_context* c, int rank, int* n_items, int* item_pixels) {
 }
 
 int pt_items_pack(pt_context* c, void* dst) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_items_pack: not on a multi-device context (pt_create_multi)");
   if (!c || !dst) return fail(PT_ERR_INVALID, "null argument");
   if (!c->last_valid || !c->d_accum) return fail(PT_ERR_INVALID, "no path-recursive pt_render yet");
   PT_HIP(hipSetDevice(c->device));
@@ -1733,6 +1661,7 @@ int pt_items_pack(pt_context* c, void* dst) {
 }
 
 int pt_items_unpack_all(pt_context* c, const void* src, size_t slot_floats, void* frame) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_items_unpack_all: not on a multi-device context (pt_create_multi)");
   if (!c || !src || !frame) return fail(PT_ERR_INVALID, "null argument");
   if (!c->last_valid) return fail(PT_ERR_INVALID, "no path-recursive pt_render yet");
   if (c->last.first_batch != 0)
@@ -1749,12 +1678,14 @@ int pt_items_unpack_all(pt_context* c, const void* src, size_t slot_floats, void
 }
 
 int pt_set_stats_mode(pt_context* c, int enabled) {
+  if (c && c->group) return ptg::set_stats_mode(c->group, enabled);
   if (!c) return fail(PT_ERR_INVALID, "null context");
   c->stats_mode = enabled != 0;
   return PT_OK;
 }
 
 int pt_get_stats(pt_context* c, pt_stats* out) {
+  if (c && c->group) return ptg::get_stats(c->group, out);
   if (!c || !out) return fail(PT_ERR_INVALID, "null argument");
   unsigned long long h[4];
   PT_HIP(hipSetDevice(c->device));
@@ -1768,6 +1699,7 @@ int pt_get_stats(pt_context* c, pt_stats* out) {
 }
 
 int pt_wide_info(pt_context* c, int info[2]) {
+  if (c && c->group) return ptg::wide_info(c->group, info);
   if (!c || !info) return fail(PT_ERR_INVALID, "null argument");
   info[0] = c->n_wide;
   info[1] = c->n_wide ? c->wide_stack : 0;
@@ -1776,6 +1708,7 @@ int pt_wide_info(pt_context* c, int info[2]) {
 }
 
 int pt_get_traced(pt_context* c, pt_traced* out) {
+  if (c && c->group) return ptg::get_traced(c->group, out);
   if (!c || !out) return fail(PT_ERR_INVALID, "null argument");
   unsigned long long h[ptd::kStatsWords];
   PT_HIP(hipSetDevice(c->device));
@@ -1790,6 +1723,7 @@ int pt_get_traced(pt_context* c, pt_traced* out) {
 }
 
 int pt_reset_stats(pt_context* c) {
+  if (c && c->group) return ptg::reset_stats(c->group);
   if (!c) return fail(PT_ERR_INVALID, "null context");
   PT_HIP(hipSetDevice(c->device));
   PT_HIP(hipMemsetAsync(c->d_stats, 0, ptd::kStatsWords * sizeof(unsigned long long), c->stream));
@@ -1797,6 +1731,7 @@ int pt_reset_stats(pt_context* c) {
 }
 
 int pt_last_launch_ms(pt_context* c, float* ms) {
+  if (c && c->group) return ptg::last_launch_ms(c->group, ms);
   if (!c || !ms) return fail(PT_ERR_INVALID, "null argument");
   if (!c->timed) return fail(PT_ERR_INVALID, "no launch recorded");
   PT_HIP(hipSetDevice(c->device));
@@ -1806,6 +1741,7 @@ int pt_last_launch_ms(pt_context* c, float* ms) {
 }
 
 int pt_launch_times_ms(pt_context* c, float* out, size_t max_n, size_t* n_out) {
+  if (c && c->group) return ptg::launch_times_ms(c->group, out, max_n, n_out);
   if (!c || !n_out) return fail(PT_ERR_INVALID, "null argument");
   const int have = c->ring_n < pt_context::kRing ? c->ring_n : pt_context::kRing;
   const int first = c->ring_n - have;
@@ -1825,6 +1761,7 @@ int pt_launch_times_ms(pt_context* c, float* out, size_t max_n, size_t* n_out) {
 // from the first launch's start to the last end, i.e. the busy span a
 // throughput figure divides by.
 int pt_launch_span_ms(pt_context* c, float* ms, size_t* n_out) {
+  if (c && c->group) return ptg::launch_span_ms(c->group, ms, n_out);
   if (!c || !ms || !n_out) return fail(PT_ERR_INVALID, "null argument");
   if (c->ring_n == 0) return fail(PT_ERR_INVALID, "no launch recorded since pt_reset_launch_times");
   if (c->ring_n > pt_context::kRing) return fail(PT_ERR_UNSUPPORTED, "more launches than the event ring holds");
@@ -1842,6 +1779,7 @@ int pt_launch_span_ms(pt_context* c, float* ms, size_t* n_out) {
 }
 
 int pt_reset_launch_times(pt_context* c) {
+  if (c && c->group) return ptg::reset_launch_times(c->group);
   if (!c) return fail(PT_ERR_INVALID, "null context");
   c->ring_n = 0;
   c->launch_n = 0;
@@ -2382,6 +2320,7 @@ int pt_dist_unique_id(void* id, size_t id_bytes) {
 }
 
 int pt_dist_init(pt_context* c, const void* id, int nranks, int rank) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_dist_init: not on a multi-device context (pt_create_multi)");
   if (!c || !id) return fail(PT_ERR_INVALID, "null argument");
   const bool emulated = nranks == 1 && rank == 0 && c->rank == 0 && c->nranks > 1;
   if (!emulated && (nranks != c->nranks || rank != c->rank))
@@ -2410,6 +2349,7 @@ int pt_dist_init(pt_context* c, const void* id, int nranks, int rank) {
     PT_HIP(hipEventCreateWithFlags(&d->render_done[b], hipEventDisableTiming));
     PT_HIP(hipEventCreateWithFlags(&d->gather_done[b], hipEventDisableTiming));
   }
+  for (hipEvent_t& e : d->entry) PT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
   PT_NCCL(R->CommInitRank(&d->comm, nranks, u, rank));
@@ -2418,6 +2358,7 @@ int pt_dist_init(pt_context* c, const void* id, int nranks, int rank) {
 }
 
 int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, void* frames, int n_frame_bufs) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_dist_run: not on a multi-device context (pt_create_multi)");
   if (!c) return fail(PT_ERR_INVALID, "null context");
   DistState* d = c->dist;
   if (!d || !d->ready) return fail(PT_ERR_INVALID, "pt_dist_run: no communicator (pt_dist_init)");
@@ -2425,6 +2366,8 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, 
   if (d->rank == 0 && (!frames || n_frame_bufs < 1 || (((uintptr_t)frames) & 15)))
     return fail(PT_ERR_INVALID, "pt_dist_run: the root needs 16-B aligned frame buffers");
   if (n_streams < 1 || n_streams > kDistStreams) return fail(PT_ERR_INVALID, "pt_dist_run: 1 to 3 streams");
+  if (d->caller_streams && n_streams > 2)
+    return fail(PT_ERR_INVALID, "pt_dist_run: 3 streams with caller render streams (pt_dist_set_streams sets two)");
   const bool emulated = d->nranks == 1 && c->nranks > 1;
   if ((d->nranks != c->nranks && !emulated) || d->rank != c->rank)
     return fail(PT_ERR_INVALID, "partition changed since pt_dist_init");
@@ -2449,6 +2392,20 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, 
   // on frame k's own stream (S divides D: S = 1 or D); a send slot is read by
   // the gather of frame k-D, which frame k's launch waits for.
   const int D = std::max(2, n_streams), nsets = 2 * D;
+  // Those hazards hold within a call.  Across calls, frame k < D of this call
+  // has no gather_done to wait for: a previous call's last sends (comm stream)
+  // may still read send slot k % D, and its trailing assemblies (other render
+  // streams) may still write the frame buffers.  So every render stream
+  // starts behind every stream's last work of the previous call.
+  {
+    hipStream_t all[kDistStreams + 1];
+    for (int s = 0; s < kDistStreams; ++s) all[s] = d->streams[s];
+    all[kDistStreams] = d->comm_stream;
+    for (int s = 0; s <= kDistStreams; ++s) PT_HIP(hipEventRecord(d->entry[s], all[s]));
+    for (int s = 0; s < n_streams; ++s)
+      for (int e = 0; e <= kDistStreams; ++e)
+        if (all[e] != d->streams[s]) PT_HIP(hipStreamWaitEvent(d->streams[s], d->entry[e], 0));
+  }
   c->in_dist = true;
   for (int k = 0; k < n_frames && rc == PT_OK; ++k) {
     const int b = k % nsets;
@@ -2505,17 +2462,20 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, 
 }
 
 int pt_dist_set_streams(pt_context* c, void* render0, void* render1, void* comm) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_dist_set_streams: not on a multi-device context (pt_create_multi)");
   if (!c || !c->dist) return fail(PT_ERR_INVALID, "pt_dist_set_streams: no communicator (pt_dist_init)");
   DistState* d = c->dist;
   PT_HIP(hipSetDevice(c->device));
   for (hipStream_t s : {d->streams[0], d->streams[1], d->streams[2], d->comm_stream}) PT_HIP(hipStreamSynchronize(s));
   d->streams[0] = render0 ? (hipStream_t)render0 : d->own[0];
   d->streams[1] = render1 ? (hipStream_t)render1 : d->own[1];
+  d->caller_streams = render0 || render1;
   d->comm_stream = comm ? (hipStream_t)comm : d->own[kDistStreams];
   return PT_OK;
 }
 
 int pt_dist_slot_floats(pt_context* c, size_t* slot_floats) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_dist_slot_floats: not on a multi-device context (pt_create_multi)");
   if (!c || !slot_floats) return fail(PT_ERR_INVALID, "null argument");
   if (!c->dist || !c->dist->slot_floats) return fail(PT_ERR_INVALID, "no pt_dist_run yet");
   *slot_floats = c->dist->slot_floats;
@@ -2523,6 +2483,7 @@ int pt_dist_slot_floats(pt_context* c, size_t* slot_floats) {
 }
 
 int pt_dist_wait(pt_context* c, int timeout_ms) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_dist_wait: not on a multi-device context (pt_create_multi)");
   if (!c || !c->dist) return fail(PT_ERR_INVALID, "pt_dist_wait: no communicator");
   DistState* d = c->dist;
   PT_HIP(hipSetDevice(c->device));
@@ -2542,6 +2503,7 @@ int pt_dist_wait(pt_context* c, int timeout_ms) {
 }
 
 int pt_dist_abort(pt_context* c) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_dist_abort: not on a multi-device context (pt_create_multi)");
   if (!c || !c->dist) return PT_OK;
   const RcclApi* R = rccl_api();
   if (c->dist->comm && R) (void)R->CommAbort(c->dist->comm);   // ends outstanding transfers
@@ -2567,6 +2529,8 @@ int pt_dist_finalize(pt_context* c) {
     if (d->render_done[b]) (void)hipEventDestroy(d->render_done[b]);
     if (d->gather_done[b]) (void)hipEventDestroy(d->gather_done[b]);
   }
+  for (hipEvent_t e : d->entry)
+    if (e) (void)hipEventDestroy(e);
   delete d;
   c->dist = nullptr;
   return PT_OK;

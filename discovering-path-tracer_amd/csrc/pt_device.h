@@ -74,24 +74,14 @@ __host__ __device__ inline bool part_owns(const Part& p, int b) {
   return own;
 }
 
-// Child-pair record (wavefront traversal of device-memory scenes): one per
-// internal node, in DFS order (right child first), 64 B:
-//   [0] = {R.min.xyz, R link}   [1] = {R.max.xyz, L link}
-//   [2] = {L.min.xyz, flags}    [3] = {L.max.xyz, 0}
-// link: the child's record index if internal, ~triangle slot if a leaf;
-// flags: 1 R implied hit, 2 L implied hit (bounds bitwise the parent's),
-// 4 L absent.  Record 0 is a virtual parent: R = the root, L absent.
 struct RenderParams {
-  const float4* pairs;      // child-pair records, or null (threaded walk)
-  int pair_depth;           // tree depth: entries of the pair walk's stack
   // culled wide walk (wide_walk.h), or null: 4-wide nodes, triangle records
   // by leaf rank, triangle slot -> rank, per-lane stack overflow areas
   // (wide_ovf_lanes lanes of wide_stack entries, lane-strided)
   const float4* hit_tris;   // the records a closest hit's index refers to: wide_tris (by rank) with the wide walk, else tris
-  const float4* wide;        // 64-B nodes when wide_qn 1, 80-B 8-wide nodes when 2, else 128-B (wide_walk.h)
+  const float4* wide;        // 64-B nodes when wide_qn 1, else 128-B (wide_walk.h)
   int wide_qn;
-  const float4* wide_leafbox;   // wide_qn: the reference's leaf box per rank (8-wide: per position), 2 float4
-  const int* wide_pos_rank;     // wide_qn 2: leaf position -> rank (exact ties); the indices below are positions
+  const float4* wide_leafbox;   // wide_qn: the reference's leaf box per rank, 2 float4
   const float4* wide_tris;
   const int* wide_rank_of;
   int2* wide_ovf;
@@ -126,7 +116,6 @@ struct RenderParams {
   const int* part_pos;
   int spl;                      // sample lanes per pixel: 1, 2, 4 or 8
   int fresh;                    // first_batch == 0 starts from +0 without reading accum
-  int sm_batch;                 // state-machine kernel: lanes that must be waiting before shading runs
   // primary-ray culling (pt_primary_cull_rects): -1 = trace every pixel; else
   // a pixel traces only if its NDC origin lies in one of cull[0..n_cull)
   // compact launch (host-built when culling applies): items (owned tile *
@@ -175,8 +164,7 @@ inline size_t scene_lds_bytes(const RenderParams& p) {
   return ((size_t)2 * p.n_nodes + (size_t)3 * p.n_tris) * 16;
 }
 // cnt: the fast kernel with traced-work counters (PT_OPT_COUNT_TRACED)
-hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool state_machine, hipStream_t stream,
-                         bool cnt = false);
+hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, hipStream_t stream, bool cnt = false);
 // Wavefront pipeline (PT_OPT_KERNEL 3): one path per (pixel, sample) held in
 // HBM; generate, then alternate a persistent traversal kernel over the list of
 // paths waiting for a ray and a shading kernel that consumes the hits and

@@ -1471,110 +1471,6 @@ __device__ bool path_step(const RenderParams& P, const CamFrame& F, PathSt& S, T
   }
 }
 
-// Runs a lane's samples in order: path_step until a ray is needed (true) or
-// the lane's last sample is folded into acc (false).
-template <bool STATS>
-__device__ bool sm_run(const RenderParams& P, const CamFrame& F, PathSt& S, Trav& T, Ctr& c, float* acc) {
-  for (;;) {
-    v3 color;
-    if (path_step<STATS>(P, F, S, T, c, &color)) return true;
-    const uint32_t batch = P.first_batch + S.s;
-    const float fb = (float)batch, fb1 = (float)(batch + 1u);          // :468
-    acc[0] = (acc[0] * fb + color.x) / fb1;
-    acc[1] = (acc[1] * fb + color.y) / fb1;
-    acc[2] = (acc[2] * fb + color.z) / fb1;
-    acc[3] = (acc[3] * fb + 1.0f) / fb1;
-    S.s++;
-    if (S.s >= P.n_batches) return false;
-    S.phase = PH_BEGIN;
-  }
-}
-
-template <bool STATS, bool LDS>
-#ifndef PT_SM_MIN_BLOCKS
-#define PT_SM_MIN_BLOCKS 1
-#endif
-__global__ __launch_bounds__(256, PT_SM_MIN_BLOCKS) void render_sm_kernel(RenderParams P) {
-  const int tid = (int)threadIdx.x;
-  if (LDS) {
-    extern __shared__ float4 lds_scene[];
-    const int nn = 2 * P.n_nodes, nt = 3 * P.n_tris;
-    for (int i = tid; i < nn; i += 256) lds_scene[i] = P.nodes[i];
-    for (int i = tid; i < nt; i += 256) lds_scene[nn + i] = P.tris[i];
-    __syncthreads();
-    P.nodes = lds_scene;
-    P.tris = lds_scene + nn;
-    P.hit_tris = P.tris;   // no wide walk here: hits are slots
-  }
-  // one pixel per lane, all its samples in order: 16x16 tile per workgroup,
-  // 8x8 per wave
-  const int tile = rank_tile(P, (int)blockIdx.x);
-  const int wave = tid >> 6, lane = tid & 63;
-  __shared__ int cand_buf[4][kCand][64];
-  int* cand = &cand_buf[wave][0][lane];
-  CamFrame F;
-  F.W = P.width;
-  F.H = P.height;
-  int bx, by;
-  tile_block(tile, P.blocks_x, &bx, &by);
-  F.px = bx * 16 + (wave & 1) * 8 + (lane & 7);
-  F.py = by * 16 + (wave >> 1) * 8 + (lane >> 3);
-  const bool active = tile < P.blocks_total && F.px < F.W && F.py < F.H;
-  F.cpos = mk(P.cam_pos[0], P.cam_pos[1], P.cam_pos[2]);
-  F.cdir = mk(P.cam_dir[0], P.cam_dir[1], P.cam_dir[2]);
-  F.ndcX0 = (2.0f * (float)F.px / (float)F.W) - 1.0f;
-  F.ndcY0 = (2.0f * (float)F.py / (float)F.H) - 1.0f;
-  F.aspect = (float)F.W / (float)F.H;
-  F.right = mk(P.cam_right[0], P.cam_right[1], P.cam_right[2]);   // host-computed frame (:430-432)
-  F.up = mk(P.cam_upv[0], P.cam_upv[1], P.cam_upv[2]);
-  F.tanFov = P.tan_fov;
-  const size_t pix = (size_t)F.py * (size_t)F.W + (size_t)F.px;
-  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  if (active && !(P.fresh && P.first_batch == 0)) {
-    const float4 a = P.accum[pix];
-    acc[0] = a.x; acc[1] = a.y; acc[2] = a.z; acc[3] = a.w;
-  }
-  Ctr c = {0u, 0u, 0u, 0u, 0u};
-  PathSt S;
-  S.s = 0;
-  S.phase = PH_BEGIN;
-  Trav T;
-  bool tracing = active && P.n_batches > 0 && sm_run<STATS>(P, F, S, T, c, acc);
-  bool waiting = false;
-  const int batch_min = P.sm_batch;
-  for (;;) {
-    if (tracing && !waiting) {
-      for (int it = 0; it < 4; ++it) {
-        if (trav_step<STATS>(P, T, cand)) {
-          waiting = true;
-          break;
-        }
-      }
-    }
-    const unsigned long long wmask = __ballot(waiting);
-    const unsigned long long tmask = __ballot(tracing && !waiting);
-    if (wmask == 0ull && tmask == 0ull) break;
-    if (tmask == 0ull || (int)__popcll(wmask) >= batch_min) {
-      if (waiting) {
-        waiting = false;
-        tracing = sm_run<STATS>(P, F, S, T, c, acc);
-      }
-    }
-  }
-  if (active && P.n_batches > 0) P.accum[pix] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-  if (STATS) {
-    const unsigned long long rays = wave_sum(c.rays), nodes = wave_sum(c.nodes), leaves = wave_sum(c.leaves);
-    const unsigned long long smp = wave_sum(active ? (unsigned long long)P.n_batches : 0ull);
-    if (lane == 0) {
-      atomicAdd(&P.stats[0], rays);
-      atomicAdd(&P.stats[1], nodes);
-      atomicAdd(&P.stats[2], leaves);
-      atomicAdd(&P.stats[3], smp);
-    }
-  }
-}
-
-
 // ===========================================================================
 // Wavefront pipeline, for scenes too large for LDS.
 //
@@ -1929,9 +1825,6 @@ constexpr unsigned long long group_lead() {
   return G == 1 ? ~0ull : G == 2 ? 0x5555555555555555ull : G == 4 ? 0x1111111111111111ull
                                     : G == 8 ? 0x0101010101010101ull : 0x0001000100010001ull;
 }
-#ifndef PT_WF_PAIR_MIN_BLOCKS
-#define PT_WF_PAIR_MIN_BLOCKS 7
-#endif
 #ifndef PT_WF_MIN_BLOCKS
 #define PT_WF_MIN_BLOCKS 7   // 72 VGPRs (11 spilled): sphere -7 %, 1M cloud -0.6 % vs 6; 8 spills 30 (+50 %)
 #endif
@@ -2009,169 +1902,6 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
           } else if (test_shadow_candidates(P, L.o, L.d, L.lim, cand, L.nc)) {
             L.res = 1;
             L.k = P.n_nodes;   // occluded: the walk ends (its next step reports it)
-          }
-          L.nc = 0;
-        }
-      }
-    }
-  }
-  if (CNT) flush_traced(P, c, lane);
-}
-
-// ---------------------------------------------------------------------------
-// Child-pair traversal for scenes in device memory (PT_OPT_PAIRS, off by
-// default: measured at 1080p 8 spp, sphere 234 -> 249 ms, 1M cloud 590 -> 574,
-// 10M cloud 2827 -> 3526; the stack's LDS cuts occupancy to 4-6 waves/SIMD
-// and L2 requests fell only 21 %, not the simulated half).
-//
-// The reference's exhaustive DFS tests both children of every internal node
-// whose box is hit (raytrace_comp.comp:196-200), so both child boxes are
-// stored together in one 64-B record per internal node (pt_device.h
-// PairRec): one fetch serves two box tests, where the threaded layout
-// fetched each child's 32-B node separately.  The right child is walked
-// first; a hit left child waits on a per-lane stack of pending subtrees and
-// hit leaves in that order, so the candidate sequence -- every hit leaf in
-// the reference's visit order -- and hence every result is the reference's.
-// Implied-hit children (bounds bitwise the parent's) skip their slab test.
-// Record 0 is a virtual parent whose right child is the root.
-// ---------------------------------------------------------------------------
-
-struct PairLane {
-  v3 o, d, inv;
-  int rec;     // record to fetch next, or -1: take the next pending entry
-  int sp;      // pending entries on the stack
-  int nc, res, shadow;
-  float lim;
-};
-
-__device__ __forceinline__ void pair_lane_start(float4 r0, float4 r1, PairLane& L) {
-  L.o = mk(r0.x, r0.y, r0.z);
-  L.d = mk(r1.x, r1.y, r1.z);
-  L.inv = mk(rcp_(L.d.x), rcp_(L.d.y), rcp_(L.d.z));
-  const int kind = __float_as_int(r1.w);   // 0 closest, 1 shadow, 2 null shadow (trav_null)
-  L.shadow = kind ? 1 : 0;
-  L.lim = L.shadow ? r0.w : 1e30f;
-  L.res = L.shadow ? 0 : -1;
-  L.rec = kind == 2 ? -1 : 0;
-  L.sp = 0;
-  L.nc = 0;
-}
-
-// One record (two box tests) and the pending entries it frees; true when the
-// walk is finished, with its remaining candidates tested.  Enqueues at most
-// two candidates before the pops, which stop when the queue is full: the
-// caller flushes wave-wide once a lane holds more than kCand - 2.
-template <bool CNT, int SS>
-__device__ __forceinline__ bool pair_step(const RenderParams& P, PairLane& L, int* stk, int* cand, Ctr& c) {
-  if (L.rec >= 0) {
-    const float4* rp = P.pairs + 4 * (size_t)L.rec;
-    const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2], r3 = rp[3];
-    const int flags = __float_as_int(r2.w);
-    const bool hR = slab(L.o, L.inv, r0, r1) || (flags & 1);
-    const bool hL = (slab(L.o, L.inv, r2, r3) || (flags & 2)) && !(flags & 4);
-    if (CNT) c.nodes += (flags & 4) ? 1u : 2u;
-    const int lr = __float_as_int(r0.w), ll = __float_as_int(r1.w);
-    int next = -1;
-    if (hR) {
-      if (lr < 0) {
-        cand[L.nc * 64] = ~lr;
-        ++L.nc;
-      } else {
-        next = lr;
-      }
-    }
-    if (hL) {
-      if (next >= 0) {
-        stk[SS * L.sp++] = ll;   // after the right subtree (a leaf stays a leaf marker)
-      } else if (ll < 0) {
-        cand[L.nc * 64] = ~ll;
-        ++L.nc;
-      } else {
-        next = ll;
-      }
-    }
-    if (CNT) c.leaves += (hR && lr < 0 ? 1u : 0u) + (hL && ll < 0 ? 1u : 0u);
-    L.rec = next;
-  }
-  while (L.rec < 0 && L.sp > 0 && L.nc < kCand) {
-    const int e = stk[SS * --L.sp];
-    if (e < 0) {
-      cand[L.nc * 64] = ~e;
-      ++L.nc;
-    } else {
-      L.rec = e;
-    }
-  }
-  if (L.rec >= 0 || L.sp > 0) return false;
-  if (!L.shadow)
-    test_candidates(P, L.o, L.d, cand, L.nc, &L.lim, &L.res);
-  else if (L.nc > 0 && test_shadow_candidates(P, L.o, L.d, L.lim, cand, L.nc))
-    L.res = 1;
-  L.nc = 0;
-  return true;
-}
-
-template <int G, bool CNT = false>
-__global__ __launch_bounds__(256, PT_WF_PAIR_MIN_BLOCKS) void wf_trace_pairs_kernel(RenderParams P, WfBuffers B,
-                                                                                   int cur) {
-  const int tid = (int)threadIdx.x;
-  if (blockIdx.x == 0 && tid == 0) B.counters[cur ^ 1] = 0;   // filled by the shading that follows
-  const int count = B.counters[cur];
-  if (count == 0) return;
-  const int wave = tid >> 6, lane = tid & 63;
-  __shared__ int cand_buf[4][kCand][64];
-  int* cand = &cand_buf[wave][0][lane];
-  // per-lane pending entries: in LDS, [depth][lane] per wave (P.pair_depth
-  // entries, sized by the host); private memory is written through to L2 on
-  // CDNA, and a stack there made every pop an L2 round trip
-  extern __shared__ int stk_lds[];
-  int* stk = stk_lds + wave * 64 * P.pair_depth + lane;
-  const float4* __restrict__ rays = B.rays[cur];
-  int p = -1;   // list slot this lane traces
-  bool more = true;
-  PairLane L;
-  L.rec = -1;
-  L.sp = 0;
-  L.nc = 0;
-  Ctr c = {0u, 0u, 0u, 0u, 0u};
-  for (;;) {
-    const unsigned long long idle = __ballot(p < 0);
-    unsigned long long gm = idle;
-#pragma unroll
-    for (int sh = 1; sh < G; sh <<= 1) gm &= gm >> sh;
-    gm &= group_lead<G>();
-    const int ng = (int)__popcll(gm);
-    if (more && ng * G >= PT_WF_REFILL) {
-      int base = 0;
-      if (lane == 0) base = atomicAdd(&B.counters[2], ng * G);
-      base = __shfl(base, 0);
-      if (base + ng * G >= count) more = false;
-      const int lead = lane & ~(G - 1);
-      if ((gm >> lead) & 1ull) {
-        const int slot = base + (int)__popcll(gm & ((1ull << lead) - 1ull)) * G + (lane - lead);
-        if (slot < count) {
-          p = slot;
-          float4 r0, r1;
-          wf_load_ray(rays, B.cap, slot, &r0, &r1);
-          pair_lane_start(r0, r1, L);
-          if (CNT) count_start(r1, c);
-        }
-      }
-    }
-    if (!more && __ballot(p >= 0) == 0ull) break;
-    for (int it = 0; it < PT_WF_STEPS; ++it) {
-      if (p >= 0 && pair_step<CNT, 64>(P, L, stk, cand, c)) {
-        B.hits[p] = make_float2(L.lim, __int_as_float(L.res));
-        p = -1;
-      }
-      if (__ballot(p >= 0 && L.nc > kCand - 2)) {   // wave-uniform flush
-        if (p >= 0 && L.nc > 0) {
-          if (!L.shadow) {
-            test_candidates(P, L.o, L.d, cand, L.nc, &L.lim, &L.res);
-          } else if (test_shadow_candidates(P, L.o, L.d, L.lim, cand, L.nc)) {
-            L.res = 1;
-            L.rec = -1;   // occluded: the walk ends (its next step reports it)
-            L.sp = 0;
           }
           L.nc = 0;
         }
@@ -2348,8 +2078,7 @@ __device__ __forceinline__ bool wide_flush_wave(WideRay& R, bool mine, const flo
   return false;
 }
 
-// LAYOUT: 0 128-B 4-wide nodes, 1 64-B 4-wide nodes (QN), 2 80-B 8-wide
-// nodes (w8_step; leaf indices are positions, ties go by pos_rank)
+// LAYOUT: 0 128-B 4-wide nodes, 1 64-B 4-wide nodes (QN)
 template <int G, bool CNT = false, int LAYOUT = 1>
 __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(RenderParams P, WfBuffers B,
                                                                                 int cur) {
@@ -2363,7 +2092,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
   int2* lds = &stk[wave][0][lane];
   __shared__ int cq[PT_WIDE_QUEUE ? 4 : 1][PT_WIDE_QUEUE ? kWideQ : 1][64];
   int* cand = PT_WIDE_QUEUE ? &cq[wave][0][lane] : nullptr;
-  constexpr bool FW = PT_WIDE_FLUSH_WAVE && PT_WIDE_QUEUE && LAYOUT != 2;
+  constexpr bool FW = PT_WIDE_FLUSH_WAVE && PT_WIDE_QUEUE;
   __shared__ unsigned long long fkeys[FW ? 4 : 1][64];
   bool fin = false;
   const long long os = (long long)gridDim.x * 256;
@@ -2463,7 +2192,6 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
     for (int it = 0; it < PT_WIDE_STEPS; ++it) {
       bool exact = false;
       if (!PT_WIDE_QUEUE) {
-        static_assert(!PT_WIDE_QUEUE ? LAYOUT != 2 : true, "the 8-wide walk runs with PT_WIDE_QUEUE");
         if (p >= 0 && wide_step<CNT, false, QN>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact,
                                                 &c.nodes, &c.leaves, nullptr, P.wide_leafbox)) {
           int res;
@@ -2475,14 +2203,9 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
         }
       } else {
         // fin: the walk has no node left (its queue may still hold candidates)
-        if (p >= 0 && !fin) {
-          if (LAYOUT == 2)
-            fin = w8_step<CNT, true>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
-                                     &c.leaves, cand, P.wide_leafbox, P.wide_pos_rank);
-          else
-            fin = wide_step<CNT, true, QN>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
-                                           &c.leaves, cand, P.wide_leafbox);
-        }
+        if (p >= 0 && !fin)
+          fin = wide_step<CNT, true, QN>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
+                                         &c.leaves, cand, P.wide_leafbox);
         if (exact) {
           R.nc = 0;
           // a fused shadow ray the walk cannot take goes to the shading's next round
@@ -2533,8 +2256,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
           if (FW ? wide_flush_wave<CNT, QN>(R, p >= 0, P.wide_tris, cand, fkeys[FW ? wave : 0], lane, &c.leaves,
                                             P.wide_leafbox)
                  : (p >= 0 && R.nc > 0 &&
-                    wide_flush<CNT, QN>(R, P.wide_tris, cand, &c.leaves, P.wide_leafbox,
-                                        LAYOUT == 2 ? P.wide_pos_rank : nullptr))) {
+                    wide_flush<CNT, QN>(R, P.wide_tris, cand, &c.leaves, P.wide_leafbox))) {
             fin = true;   // occluded
             R.sp = 0;
             R.cur = -1;
@@ -2938,19 +2660,18 @@ hipError_t launch_clear(float4* accum, int width, int height, const Part& part, 
   return hipGetLastError();
 }
 
-hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool state_machine, hipStream_t stream,
-                         bool cnt) {
-  if (cnt && (stats || state_machine)) return hipErrorInvalidValue;
+hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, hipStream_t stream, bool cnt) {
+  if (cnt && stats) return hipErrorInvalidValue;
   if (p.spl != 1 && p.spl != 2 && p.spl != 4 && p.spl != 8) return hipErrorInvalidValue;
   // owned tiles (part_tile); the recursive kernel splits each into spl workgroups
   const long long tiles = p.n_tiles;
-  long long grid = state_machine ? tiles : tiles * p.spl;
+  long long grid = tiles * p.spl;
   if (grid <= 0 || p.n_batches == 0) return hipSuccess;
-  if (p.pack_out && (state_machine || stats)) return hipErrorInvalidValue;
+  if (p.pack_out && stats) return hipErrorInvalidValue;
   if (p.pack_out) {   // live items (p.n_items), then the assembly workgroups
     const long long px = (long long)p.n_unpack * (256 / p.spl);
     grid = p.n_items + (px + 256 * kPixPerFill - 1) / (256 * kPixPerFill);
-  } else if (p.items && !state_machine) {   // compact list of live items, then the fill workgroups
+  } else if (p.items) {   // compact list of live items, then the fill workgroups
     const long long px = (long long)p.n_culled_items * (256 / p.spl);
     grid = p.n_items + (px + 256 * kPixPerFill - 1) / (256 * kPixPerFill);
   }
@@ -2958,10 +2679,7 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, bool
   const size_t lds = lds_scene ? scene_lds_bytes(p) : 0;
   if (lds > kMaxSceneLds) return hipErrorInvalidValue;
   void (*kern)(RenderParams);
-  if (state_machine)
-    kern = lds_scene ? (stats ? render_sm_kernel<true, true> : render_sm_kernel<false, true>)
-                     : (stats ? render_sm_kernel<true, false> : render_sm_kernel<false, false>);
-  else if (cnt)
+  if (cnt)
     kern = lds_scene ? render_kernel<false, true, true> : render_kernel<false, false, true>;
   else
     kern = lds_scene ? (stats ? render_kernel<true, true> : render_kernel<false, true>)
@@ -2975,8 +2693,7 @@ long long wide_trace_lanes() {
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
   int most = 0;
-  for (auto k : {wf_trace_wide_kernel<kWideG, false, 2>, wf_trace_wide_kernel<kWideG, true, 2>,
-                 wf_trace_wide_kernel<kWideG, false, 1>, wf_trace_wide_kernel<kWideG, true, 1>,
+  for (auto k : {wf_trace_wide_kernel<kWideG, false, 1>, wf_trace_wide_kernel<kWideG, true, 1>,
                  wf_trace_wide_kernel<kWideG, false, 0>, wf_trace_wide_kernel<kWideG, true, 0>}) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0) != hipSuccess) return 0;
     most = std::max(most, per_cu);
@@ -3013,21 +2730,15 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
                        : (g2 ? wf_trace_kernel<false, 2, true> : wf_trace_kernel<false, 4, true>))
           : (lds_scene ? (g2 ? wf_trace_kernel<true, 2> : wf_trace_kernel<true, 4>)
                        : (g2 ? wf_trace_kernel<false, 2> : wf_trace_kernel<false, 4>));
-  if (p0.pairs && !lds_scene)   // child-pair records (PT_OPT_PAIRS)
-    trace = cnt ? (g2 ? wf_trace_pairs_kernel<2, true> : wf_trace_pairs_kernel<4, true>)
-                : (g2 ? wf_trace_pairs_kernel<2> : wf_trace_pairs_kernel<4>);
-  const bool wide = p0.wide && !lds_scene && !p0.pairs;
+  const bool wide = p0.wide && !lds_scene;
   if (wide)   // culled wide walk (PT_OPT_WIDE, default)
-    trace = p0.wide_qn == 2 ? (cnt ? wf_trace_wide_kernel<kWideG, true, 2> : wf_trace_wide_kernel<kWideG, false, 2>)
-            : p0.wide_qn ? (cnt ? wf_trace_wide_kernel<kWideG, true, 1> : wf_trace_wide_kernel<kWideG, false, 1>)
-                         : (cnt ? wf_trace_wide_kernel<kWideG, true, 0> : wf_trace_wide_kernel<kWideG, false, 0>);
-  size_t lds_t = lds;
-  if (p0.pairs && !lds_scene) lds_t = (size_t)4 * 64 * p0.pair_depth * sizeof(int);   // the walk stacks
-  if (wide) lds_t = 0;
+    trace = p0.wide_qn ? (cnt ? wf_trace_wide_kernel<kWideG, true, 1> : wf_trace_wide_kernel<kWideG, false, 1>)
+                       : (cnt ? wf_trace_wide_kernel<kWideG, true, 0> : wf_trace_wide_kernel<kWideG, false, 0>);
+  const size_t lds_t = wide ? 0 : lds;
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_t, trace, 256, lds_t);
   if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_s, wf_shade_kernel, 256, 0);
   // PT_OPT_WF_TAIL (the 4-wide layouts of the wide walk): wf_tail_kernel after each round's trace
-  const bool tail = wide && p0.wf_tail > 0 && p0.wide_qn != 2;
+  const bool tail = wide && p0.wf_tail > 0;
   void (*tailk)(RenderParams, WfBuffers, int) =
       p0.wide_qn ? (cnt ? wf_tail_kernel<true, true> : wf_tail_kernel<false, true>)
                  : (cnt ? wf_tail_kernel<true, false> : wf_tail_kernel<false, false>);

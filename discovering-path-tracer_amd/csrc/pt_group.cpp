@@ -1,0 +1,443 @@
+// pt_group.cpp — one context driving several GPUs from one process
+// (pt_create_multi, include/pathtracer.h).
+//
+// The reference drives its GPU from one detached thread of one process
+// (VulkanRenderer.cpp:643-647; the loop is VulkanRayTracer::mainLoop,
+// VulkanRayTracer.cpp:717-865).  A group gives that caller the tile split of
+// SURVEY §8e without a launcher: member r is an ordinary context on device
+// ordinals[r] owning the screen tiles b with b % n == r (pt_set_partition,
+// rows rotated), and every call on the group behaves as on one device, with
+// the frame in device memory of ordinals[0].
+//
+// Exchange.  In one process the devices of an MI355X node reach each
+// other's HBM over xGMI with ordinary loads and stores once peer access is
+// enabled, so no collective is needed: every member binds the frame on
+// ordinals[0] as its accumulation buffer (pt_bind_accum) and its render
+// kernel reads and writes its own tiles there.  The only traffic is the
+// accumulator's own 16 B per owned pixel per launch (read only when the
+// first batch is not 0), spread over the kernel; the tiles are disjoint, so
+// no two members touch a pixel.  Where a member cannot map the first device
+// (or with PT_OPT_GROUP_EXCHANGE 1) it renders into an accumulation buffer of
+// its own (+0 on its tiles, -0 elsewhere) and after each launch packs its
+// tiles (pt_tiles_pack), copies them to a receive buffer on the first device
+// (hipMemcpyPeerAsync) and the first device scatters them into the frame
+// (pt_tiles_unpack).  Either way the frame is bit-identical to a single-GPU
+// render: each pixel is computed by exactly one member, by the same kernels.
+//
+// Ordering.  The first member's stream is the group's stream.  A render
+// records an event on it that every other member's stream waits for (so the
+// clear or readback before it is done), and the group's stream then waits
+// for every member's completion event (so a read, clear or readback after it
+// sees every tile).  Members on other devices are waited for with
+// cross-device events, never with a host synchronisation.
+#include "pt_group.h"
+
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+namespace {
+
+#define G_HIP(call)                                                                             \
+  do {                                                                                          \
+    hipError_t e_ = (call);                                                                     \
+    if (e_ != hipSuccess) return pt_fail_internal(PT_ERR_HIP, std::string(#call ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+#define G_RC(call)            \
+  do {                        \
+    const int rc_ = (call);   \
+    if (rc_) return rc_;      \
+  } while (0)
+
+constexpr int kOptGroupExchange = 18;   // PT_OPT_GROUP_EXCHANGE (pathtracer.h)
+
+}  // namespace
+
+struct pt_group {
+  int n = 0;
+  std::vector<int> dev;              // member r's device
+  std::vector<pt_context*> m;        // member contexts
+  std::vector<hipStream_t> own;      // streams created here, one per member
+  std::vector<hipStream_t> s;        // the streams the members run on (s[0] may be the caller's)
+  std::vector<hipEvent_t> done;      // member r's last launch (r > 0)
+  hipEvent_t start = nullptr;        // the group stream's work before a render
+  bool peer_ok = true;               // every member can map the first device's memory
+  int exchange = 0;                  // PT_OPT_GROUP_EXCHANGE: 0 auto, 1 staged copies
+  bool staged = false;               // the exchange the current frame buffer was set up for
+  float* frame = nullptr;            // W x H float4 on dev[0]
+  bool own_frame = false;
+  int W = 0, H = 0;
+  // staged exchange: member r's tiles, packed on its device and received on dev[0]
+  std::vector<float*> pack_local, pack_root;
+  std::vector<size_t> pack_bytes;
+  // progressive loop (the group's own counter; VulkanRayTracer.cpp:739-754)
+  float prog_cam[16] = {0};
+  bool prog_has_cam = false;
+  uint32_t prog_batch = 0;
+};
+
+namespace {
+
+template <class T>
+void gfree(int device, T*& p) {
+  if (p) {
+    (void)hipSetDevice(device);
+    (void)hipFree(p);
+  }
+  p = nullptr;
+}
+
+// Runs f(r) for every member, concurrently when there is more than one
+// device (host-side scene preparation and uploads), and returns the first
+// failure with its message.
+template <class F>
+int each_parallel(pt_group* g, F f) {
+  if (g->n == 1) return f(0);
+  std::vector<int> rc((size_t)g->n, PT_OK);
+  std::vector<std::string> msg((size_t)g->n);
+  std::vector<std::thread> t;
+  for (int r = 0; r < g->n; ++r)
+    t.emplace_back([&, r] {
+      rc[(size_t)r] = f(r);
+      if (rc[(size_t)r]) msg[(size_t)r] = pt_last_error();
+    });
+  for (auto& x : t) x.join();
+  for (int r = 0; r < g->n; ++r)
+    if (rc[(size_t)r]) return pt_fail_internal(rc[(size_t)r], "member " + std::to_string(r) + ": " + msg[(size_t)r]);
+  return PT_OK;
+}
+
+template <class F>
+int each(pt_group* g, F f) {
+  for (int r = 0; r < g->n; ++r) G_RC(f(r));
+  return PT_OK;
+}
+
+void free_exchange(pt_group* g) {
+  for (int r = 0; r < g->n; ++r) {
+    if (r < (int)g->pack_local.size()) gfree(g->dev[(size_t)r], g->pack_local[(size_t)r]);
+    if (r < (int)g->pack_root.size()) gfree(g->dev[0], g->pack_root[(size_t)r]);
+  }
+  g->pack_local.assign((size_t)g->n, nullptr);
+  g->pack_root.assign((size_t)g->n, nullptr);
+  g->pack_bytes.assign((size_t)g->n, 0);
+}
+
+int quiesce_all(pt_group* g) {
+  for (int r = 0; r < g->n; ++r) {
+    G_HIP(hipSetDevice(g->dev[(size_t)r]));
+    G_HIP(hipStreamSynchronize(g->s[(size_t)r]));
+  }
+  return PT_OK;
+}
+
+// (Re)binds the frame of W x H on dev[0] to the members for the exchange in
+// force: peer stores (every member renders into the frame) or staged copies
+// (members r > 0 render into their own buffers and ship packed tiles).
+int setup_frame(pt_group* g) {
+  G_RC(quiesce_all(g));
+  free_exchange(g);
+  g->staged = g->n > 1 && (g->exchange == 1 || !g->peer_ok);
+  for (int r = 0; r < g->n; ++r) {
+    pt_context* c = g->m[(size_t)r];
+    if (r == 0 || !g->staged) {
+      G_RC(pt_bind_accum(c, g->frame, g->W, g->H));
+      continue;
+    }
+    G_RC(pt_resize_and_clear(c, g->W, g->H));   // +0 on its tiles, -0 elsewhere
+    int tiles = 0;
+    G_RC(pt_tiles_owned(c, &tiles));
+    const size_t bytes = (size_t)std::max(tiles, 1) * 256 * 16;
+    G_HIP(hipSetDevice(g->dev[(size_t)r]));
+    G_HIP(hipMalloc((void**)&g->pack_local[(size_t)r], bytes));
+    G_HIP(hipSetDevice(g->dev[0]));
+    G_HIP(hipMalloc((void**)&g->pack_root[(size_t)r], bytes));
+    g->pack_bytes[(size_t)r] = bytes;
+  }
+  return PT_OK;
+}
+
+}  // namespace
+
+namespace ptg {
+
+int make(const int* ordinals, int n, pt_group** out) {
+  if (!ordinals || !out) return pt_fail_internal(PT_ERR_INVALID, "null argument");
+  if (n < 1 || n > 64) return pt_fail_internal(PT_ERR_INVALID, "pt_create_multi: 1 to 64 devices");
+  *out = nullptr;
+  int ndev = 0;
+  G_HIP(hipGetDeviceCount(&ndev));
+  for (int r = 0; r < n; ++r)
+    if (ordinals[r] < 0 || ordinals[r] >= ndev)
+      return pt_fail_internal(PT_ERR_INVALID, "device ordinal " + std::to_string(ordinals[r]) + " out of range (" +
+                                                  std::to_string(ndev) + " devices)");
+  pt_group* g = new pt_group();
+  g->n = n;
+  g->dev.assign(ordinals, ordinals + n);
+  g->m.assign((size_t)n, nullptr);
+  g->own.assign((size_t)n, nullptr);
+  g->s.assign((size_t)n, nullptr);
+  g->done.assign((size_t)n, nullptr);
+  free_exchange(g);
+  auto bail = [&](int rc) {
+    const std::string msg = pt_last_error();
+    destroy(g);
+    return pt_fail_internal(rc, msg);
+  };
+  for (int r = 0; r < n; ++r) {
+    int rc = pt_create(g->dev[(size_t)r], &g->m[(size_t)r]);
+    if (!rc) rc = pt_set_partition(g->m[(size_t)r], n, r);
+    if (rc) return bail(rc);
+    if (hipSetDevice(g->dev[(size_t)r]) != hipSuccess ||
+        hipStreamCreateWithFlags(&g->own[(size_t)r], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&g->done[(size_t)r], hipEventDisableTiming) != hipSuccess)
+      return bail(pt_fail_internal(PT_ERR_HIP, "pt_create_multi: stream/event setup failed"));
+    g->s[(size_t)r] = g->own[(size_t)r];
+    rc = pt_set_stream(g->m[(size_t)r], g->s[(size_t)r]);
+    if (rc) return bail(rc);
+    // the members' kernels store into the first device's frame over xGMI
+    if (g->dev[(size_t)r] != g->dev[0]) {
+      int ok = 0;
+      if (hipDeviceCanAccessPeer(&ok, g->dev[(size_t)r], g->dev[0]) != hipSuccess) ok = 0;
+      if (ok) {
+        const hipError_t e = hipDeviceEnablePeerAccess(g->dev[0], 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) ok = 0;
+        (void)hipGetLastError();
+      }
+      if (!ok) g->peer_ok = false;
+    }
+  }
+  if (hipSetDevice(g->dev[0]) != hipSuccess ||
+      hipEventCreateWithFlags(&g->start, hipEventDisableTiming) != hipSuccess)
+    return bail(pt_fail_internal(PT_ERR_HIP, "pt_create_multi: event setup failed"));
+  *out = g;
+  return PT_OK;
+}
+
+int destroy(pt_group* g) {
+  if (!g) return PT_OK;
+  for (int r = 0; r < g->n; ++r)
+    if (g->s[(size_t)r]) {
+      (void)hipSetDevice(g->dev[(size_t)r]);
+      (void)hipStreamSynchronize(g->s[(size_t)r]);
+    }
+  for (int r = 0; r < g->n; ++r)
+    if (g->m[(size_t)r]) (void)pt_destroy(g->m[(size_t)r]);
+  free_exchange(g);
+  if (g->own_frame) gfree(g->dev[0], g->frame);
+  for (int r = 0; r < g->n; ++r) {
+    (void)hipSetDevice(g->dev[(size_t)r]);
+    if (g->own[(size_t)r]) (void)hipStreamDestroy(g->own[(size_t)r]);
+    if (g->done[(size_t)r]) (void)hipEventDestroy(g->done[(size_t)r]);
+  }
+  if (g->start) {
+    (void)hipSetDevice(g->dev[0]);
+    (void)hipEventDestroy(g->start);
+  }
+  delete g;
+  return PT_OK;
+}
+
+int set_stream(pt_group* g, void* s) {
+  G_RC(quiesce_all(g));
+  g->s[0] = s ? (hipStream_t)s : g->own[0];
+  return pt_set_stream(g->m[0], g->s[0]);
+}
+
+int synchronize(pt_group* g) { return quiesce_all(g); }
+
+int upload_scene(pt_group* g, const float* vertices, size_t n_vertex_floats, const uint32_t* indices,
+                 size_t n_indices, const pt_bvh_node* nodes, size_t n_nodes, const float* uvs, size_t n_uv_floats,
+                 const uint32_t* mat_indices, size_t n_mat, uint32_t flags) {
+  return each_parallel(g, [&](int r) {
+    return pt_upload_scene(g->m[(size_t)r], vertices, n_vertex_floats, indices, n_indices, nodes, n_nodes, uvs,
+                           n_uv_floats, mat_indices, n_mat, flags);
+  });
+}
+
+int upload_lights(pt_group* g, const pt_area_light* lights, size_t n) {
+  return each(g, [&](int r) { return pt_upload_lights(g->m[(size_t)r], lights, n); });
+}
+
+int set_camera(pt_group* g, const float ubo[16]) {
+  return each(g, [&](int r) { return pt_set_camera(g->m[(size_t)r], ubo); });
+}
+
+int set_params(pt_group* g, const pt_params* p) {
+  return each(g, [&](int r) { return pt_set_params(g->m[(size_t)r], p); });
+}
+
+int clear_accum(pt_group* g) {
+  if (!g->frame) return pt_fail_internal(PT_ERR_INVALID, "no accumulation buffer");
+  // every pixel +0 on the group's stream, after its members' last launches
+  G_HIP(hipSetDevice(g->dev[0]));
+  for (int r = 1; r < g->n; ++r) G_HIP(hipStreamWaitEvent(g->s[0], g->done[(size_t)r], 0));
+  G_HIP(hipMemsetAsync(g->frame, 0, (size_t)g->W * g->H * 16, g->s[0]));
+  if (g->staged)
+    for (int r = 1; r < g->n; ++r) G_RC(pt_clear_accum(g->m[(size_t)r]));
+  return PT_OK;
+}
+
+int resize_and_clear(pt_group* g, int w, int h) {
+  if (w <= 0 || h <= 0 || (long long)w * h > (1ll << 31)) return pt_fail_internal(PT_ERR_INVALID, "bad resolution");
+  if (!(g->own_frame && g->W == w && g->H == h)) {
+    G_RC(quiesce_all(g));
+    if (g->own_frame) gfree(g->dev[0], g->frame);
+    g->frame = nullptr;
+    g->own_frame = false;
+    G_HIP(hipSetDevice(g->dev[0]));
+    G_HIP(hipMalloc((void**)&g->frame, (size_t)w * h * 16));
+    g->own_frame = true;
+    g->W = w;
+    g->H = h;
+    G_RC(setup_frame(g));
+  }
+  return clear_accum(g);
+}
+
+int bind_accum(pt_group* g, void* ptr, int w, int h) {
+  if (!ptr) return pt_fail_internal(PT_ERR_INVALID, "null argument");
+  if (w <= 0 || h <= 0) return pt_fail_internal(PT_ERR_INVALID, "bad resolution");
+  if (((uintptr_t)ptr) & 15) return pt_fail_internal(PT_ERR_INVALID, "accumulation buffer must be 16-B aligned");
+  G_RC(quiesce_all(g));
+  if (g->own_frame) gfree(g->dev[0], g->frame);
+  g->frame = (float*)ptr;
+  g->own_frame = false;
+  g->W = w;
+  g->H = h;
+  return setup_frame(g);
+}
+
+void* accum_device_ptr(pt_group* g) { return g->frame; }
+
+int read_accum(pt_group* g, float* rgba, size_t n) { return pt_read_accum(g->m[0], rgba, n); }
+
+int render(pt_group* g, uint32_t first_batch, uint32_t n_batches) {
+  if (!g->frame) return pt_fail_internal(PT_ERR_INVALID, "no accumulation buffer");
+  // the members start after the group stream's earlier work (clear, readback)
+  G_HIP(hipSetDevice(g->dev[0]));
+  G_HIP(hipEventRecord(g->start, g->s[0]));
+  for (int r = 1; r < g->n; ++r) {
+    G_HIP(hipSetDevice(g->dev[(size_t)r]));
+    G_HIP(hipStreamWaitEvent(g->s[(size_t)r], g->start, 0));
+    G_RC(pt_render(g->m[(size_t)r], first_batch, n_batches));
+    if (g->staged) {
+      G_RC(pt_tiles_pack(g->m[(size_t)r], g->pack_local[(size_t)r]));
+      G_HIP(hipSetDevice(g->dev[(size_t)r]));
+      G_HIP(hipMemcpyPeerAsync(g->pack_root[(size_t)r], g->dev[0], g->pack_local[(size_t)r], g->dev[(size_t)r],
+                               g->pack_bytes[(size_t)r], g->s[(size_t)r]));
+    }
+    G_HIP(hipSetDevice(g->dev[(size_t)r]));
+    G_HIP(hipEventRecord(g->done[(size_t)r], g->s[(size_t)r]));
+  }
+  G_RC(pt_render(g->m[0], first_batch, n_batches));
+  G_HIP(hipSetDevice(g->dev[0]));
+  for (int r = 1; r < g->n; ++r) {
+    G_HIP(hipStreamWaitEvent(g->s[0], g->done[(size_t)r], 0));
+    if (g->staged) G_RC(pt_tiles_unpack(g->m[0], g->pack_root[(size_t)r], r, g->frame));
+  }
+  return PT_OK;
+}
+
+int progressive_camera(pt_group* g, const float ubo[16], int* reset) {
+  if (!ubo) return pt_fail_internal(PT_ERR_INVALID, "null argument");
+  const bool changed = !g->prog_has_cam || memcmp(ubo, g->prog_cam, sizeof g->prog_cam) != 0;
+  if (changed) {
+    memcpy(g->prog_cam, ubo, sizeof g->prog_cam);
+    g->prog_has_cam = true;
+    g->prog_batch = 0;
+    G_RC(set_camera(g, ubo));
+  }
+  if (reset) *reset = changed ? 1 : 0;
+  return PT_OK;
+}
+
+int progressive_advance(pt_group* g, uint32_t max_new, uint32_t limit, uint32_t* first, uint32_t* count) {
+  if (!g->prog_has_cam) return pt_fail_internal(PT_ERR_INVALID, "no camera (pt_progressive_camera)");
+  const uint32_t room = limit > g->prog_batch ? limit - g->prog_batch : 0u;
+  const uint32_t k = max_new < room ? max_new : room;
+  if (first) *first = g->prog_batch;
+  if (count) *count = k;
+  if (k == 0) return PT_OK;
+  G_RC(render(g, g->prog_batch, k));
+  g->prog_batch += k;
+  return PT_OK;
+}
+
+// the first member's readback runs on the group's stream, which has waited
+// for every member's tiles
+int readback_begin(pt_group* g, int* ticket) { return pt_readback_begin(g->m[0], ticket); }
+int readback_end(pt_group* g, int ticket, float* rgba, size_t n) { return pt_readback_end(g->m[0], ticket, rgba, n); }
+
+int set_option(pt_group* g, int key, int value) {
+  if (key == kOptGroupExchange) {
+    if (value < 0 || value > 1) return pt_fail_internal(PT_ERR_INVALID, "PT_OPT_GROUP_EXCHANGE takes 0 or 1");
+    if (value == g->exchange) return PT_OK;
+    g->exchange = value;
+    return g->frame ? setup_frame(g) : PT_OK;
+  }
+  return each(g, [&](int r) { return pt_set_option(g->m[(size_t)r], key, value); });
+}
+
+int last_kernel(pt_group* g, int* kernel) { return pt_last_kernel(g->m[0], kernel); }
+
+int set_stats_mode(pt_group* g, int enabled) {
+  return each(g, [&](int r) { return pt_set_stats_mode(g->m[(size_t)r], enabled); });
+}
+
+int get_stats(pt_group* g, pt_stats* out) {
+  if (!out) return pt_fail_internal(PT_ERR_INVALID, "null argument");
+  pt_stats sum{};
+  for (int r = 0; r < g->n; ++r) {
+    pt_stats s{};
+    G_RC(pt_get_stats(g->m[(size_t)r], &s));
+    sum.rays += s.rays;
+    sum.nodes += s.nodes;
+    sum.leaf_tests += s.leaf_tests;
+    sum.samples += s.samples;
+  }
+  *out = sum;
+  return PT_OK;
+}
+
+int reset_stats(pt_group* g) { return each(g, [&](int r) { return pt_reset_stats(g->m[(size_t)r]); }); }
+
+int get_traced(pt_group* g, pt_traced* out) {
+  if (!out) return pt_fail_internal(PT_ERR_INVALID, "null argument");
+  pt_traced sum{};
+  for (int r = 0; r < g->n; ++r) {
+    pt_traced t{};
+    G_RC(pt_get_traced(g->m[(size_t)r], &t));
+    sum.closest_walks += t.closest_walks;
+    sum.shadow_walks += t.shadow_walks;
+    sum.nodes += t.nodes;
+    sum.tri_tests += t.tri_tests;
+    sum.primaries += t.primaries;
+  }
+  *out = sum;
+  return PT_OK;
+}
+
+int wide_info(pt_group* g, int info[2]) { return pt_wide_info(g->m[0], info); }
+int last_launch_ms(pt_group* g, float* ms) { return pt_last_launch_ms(g->m[0], ms); }
+int launch_times_ms(pt_group* g, float* out, size_t max_n, size_t* n_out) {
+  return pt_launch_times_ms(g->m[0], out, max_n, n_out);
+}
+int launch_span_ms(pt_group* g, float* ms, size_t* n_out) { return pt_launch_span_ms(g->m[0], ms, n_out); }
+int reset_launch_times(pt_group* g) {
+  return each(g, [&](int r) { return pt_reset_launch_times(g->m[(size_t)r]); });
+}
+
+int members(pt_group* g, int* n, int* devices, int max_devices, int* peer) {
+  if (n) *n = g->n;
+  if (devices)
+    for (int r = 0; r < g->n && r < max_devices; ++r) devices[r] = g->dev[(size_t)r];
+  if (peer) *peer = g->n > 1 && !(g->exchange == 1 || !g->peer_ok) ? 1 : 0;
+  return PT_OK;
+}
+
+}  // namespace ptg

@@ -93,45 +93,6 @@ bool quantize_node(const float* rec, float* q) {
   return true;
 }
 
-// The grid of one axis of a node (quantize_node's rule, any child count):
-// origin p (the least lo), step 2^e, and each valid child's lo rounded down
-// and hi rounded up onto it, checked with the device's decode fmaf(q, s, p).
-bool quantize_axis(const float* lo, const float* hi, const bool* valid, int n, float* p_out, uint32_t* e_biased,
-                   uint8_t* ql, uint8_t* qh) {
-  float pmin = INFINITY, hmax = -INFINITY;
-  for (int j = 0; j < n; ++j)
-    if (valid[j]) {
-      pmin = std::min(pmin, lo[j]);
-      hmax = std::max(hmax, hi[j]);
-    }
-  if (!(pmin <= hmax)) return false;
-  const float p = pmin;
-  const double d = (double)hmax - (double)p;
-  int e = d > 0.0 ? (int)ceil(log2(d / 255.0)) : -126;
-  e = std::max(-126, std::min(127, e));
-  while (e < 127 && fmaf(255.0f, ldexpf(1.0f, e), p) < hmax) ++e;
-  while (e > -126 && fmaf(255.0f, ldexpf(1.0f, e - 1), p) >= hmax) --e;
-  const float s = ldexpf(1.0f, e);
-  if (!(fmaf(255.0f, s, p) >= hmax)) return false;
-  *p_out = p;
-  *e_biased = (uint32_t)(e + 127);
-  for (int j = 0; j < n; ++j) {
-    ql[j] = 255;
-    qh[j] = 0;
-    if (!valid[j]) continue;
-    int l = (int)std::max(0.0, std::min(255.0, floor(((double)lo[j] - (double)p) / (double)s)));
-    while (l > 0 && fmaf((float)l, s, p) > lo[j]) --l;
-    while (l < 255 && fmaf((float)(l + 1), s, p) <= lo[j]) ++l;
-    int h = (int)std::max(0.0, std::min(255.0, ceil(((double)hi[j] - (double)p) / (double)s)));
-    while (h < 255 && fmaf((float)h, s, p) < hi[j]) ++h;
-    while (h > 0 && fmaf((float)(h - 1), s, p) >= hi[j]) --h;
-    if (!(fmaf((float)l, s, p) <= lo[j] && fmaf((float)h, s, p) >= hi[j])) return false;
-    ql[j] = (uint8_t)l;
-    qh[j] = (uint8_t)h;
-  }
-  return true;
-}
-
 }  // namespace
 
 WideCoeffs coeff_max(const WideCoeffs& a, const WideCoeffs& b) {
@@ -352,180 +313,6 @@ void sah_build(BinTree& T, std::vector<int32_t>& ids, std::vector<float>& lbox, 
   }
 }
 
-// The 8-wide layout (wide_walk.h kW8NodeF4) of binary tree T: a node's
-// children are found as for the 4-wide nodes (expand the largest box) up to
-// eight, then placed in octant slots: slot s (bit a: the high side of axis a)
-// goes to the child whose centroid lies furthest toward that octant of the
-// node's centre (greedy, cheapest pair first).  A ray walks the slots in the
-// order i ^ (its direction's sign bits), which puts near children before far
-// ones without sorting (the walk still expands the nearest live child
-// first).  Inner children are allocated consecutively from child_base, leaf
-// children take consecutive positions from leaf_base, both in slot order;
-// the slot map holds each slot's 4-bit code (15 empty, 8 | k the k-th leaf,
-// k the k-th inner child; a node with eight children sets bit 15 of its
-// E0|E1 word, and code 15 is then its eighth leaf).  rank: the leaf rank of
-// every reference node.
-std::string build_w8(const BinTree& T, const std::vector<int32_t>& rank, size_t n_tris, const std::vector<float>& leaf_box,
-                     WideBVH* out) {
-  if (n_tris >= (size_t)1 << 29) return "too many triangles for the 8-wide layout";
-  auto area = [&](int32_t v) { return half_area(&T.box[6 * (size_t)v]); };
-  std::vector<float>& W = out->w8nodes;
-  W.clear();
-  std::vector<int32_t> n_inner, first_kid;   // per node: inner children, the first one's index
-  std::vector<std::pair<int32_t, int32_t>> st;   // (binary node, 8-wide node)
-  W.resize(20, 0.0f);
-  n_inner.push_back(0);
-  first_kid.push_back(0);
-  st.push_back({0, 0});
-  int32_t next_pos = 0;
-  out->w8_pos_rank.assign(n_tris, -1);
-  out->w8_leaf_box.assign(8 * n_tris, 0.0f);
-  while (!st.empty()) {
-    const auto [v, w] = st.back();
-    st.pop_back();
-    std::vector<int32_t> list;
-    if (T.leaf(v)) {
-      list.push_back(v);
-    } else {
-      list = {T.kid[2 * v], T.kid[2 * v + 1]};
-      while (list.size() < 8) {
-        int best = -1;
-        double ba = -1.0;
-        for (size_t j = 0; j < list.size(); ++j)
-          if (!T.leaf(list[j]) && area(list[j]) > ba) {
-            ba = area(list[j]);
-            best = (int)j;
-          }
-        if (best < 0) break;
-        const int32_t x = list[best];
-        list[best] = T.kid[2 * x];
-        list.insert(list.begin() + best + 1, T.kid[2 * x + 1]);
-      }
-    }
-    // octant slots
-    const float* nb = &T.box[6 * (size_t)v];
-    double pc[3];
-    for (int a = 0; a < 3; ++a) pc[a] = 0.5 * ((double)nb[a] + (double)nb[3 + a]);
-    int32_t slot[8];
-    for (int k = 0; k < 8; ++k) slot[k] = -1;
-    std::vector<char> used(list.size(), 0);
-    for (size_t k = 0; k < list.size(); ++k) {
-      double bc = INFINITY;
-      int bj = -1, bs = -1;
-      for (size_t j = 0; j < list.size(); ++j) {
-        if (used[j]) continue;
-        const float* cb = &T.box[6 * (size_t)list[j]];
-        for (int sl = 0; sl < 8; ++sl) {
-          if (slot[sl] >= 0) continue;
-          double c = 0.0;
-          for (int a = 0; a < 3; ++a) {
-            const double off = 0.5 * ((double)cb[a] + (double)cb[3 + a]) - pc[a];
-            c -= ((sl >> a) & 1) ? off : -off;
-          }
-          if (c < bc) {
-            bc = c;
-            bj = (int)j;
-            bs = sl;
-          }
-        }
-      }
-      used[bj] = 1;
-      slot[bs] = list[bj];
-    }
-    // children: inner nodes consecutive, leaves at consecutive positions
-    int ni = 0, nl = 0;
-    for (int sl = 0; sl < 8; ++sl)
-      if (slot[sl] >= 0) (T.leaf(slot[sl]) ? nl : ni)++;
-    const int32_t child_base = (int32_t)n_inner.size();
-    const int32_t leaf_base = next_pos;
-    n_inner[w] = ni;
-    first_kid[w] = child_base;
-    for (int k = 0; k < ni; ++k) {
-      n_inner.push_back(0);
-      first_kid.push_back(0);
-    }
-    W.resize(20 * n_inner.size(), 0.0f);
-    uint32_t smap = 0;
-    float lo[3][8], hi[3][8];
-    bool valid[8];
-    WideCoeffs co{0.0, 0.0, 0.0, 0.0};
-    int ki = 0, kl = 0;
-    for (int sl = 0; sl < 8; ++sl) {
-      const int32_t c = slot[sl];
-      valid[sl] = c >= 0;
-      uint32_t code = 15;
-      for (int a = 0; a < 3; ++a) lo[a][sl] = hi[a][sl] = 0.0f;
-      if (c >= 0) {
-        const float* cb = &T.box[6 * (size_t)c];
-        for (int a = 0; a < 3; ++a) {
-          lo[a][sl] = cb[a];
-          hi[a][sl] = cb[3 + a];
-        }
-        co = coeff_max(co, T.co[c]);
-        if (T.leaf(c)) {
-          const int32_t r = rank[T.kid[2 * (size_t)c + 1]];
-          const int32_t pos = leaf_base + kl;
-          out->w8_pos_rank[(size_t)pos] = r;
-          memcpy(&out->w8_leaf_box[8 * (size_t)pos], &leaf_box[8 * (size_t)r], 8 * sizeof(float));
-          code = 8u | (uint32_t)kl++;
-        } else {
-          st.push_back({c, child_base + ki});
-          code = (uint32_t)ki++;
-        }
-      }
-      smap |= code << (4 * sl);
-    }
-    next_pos += nl;
-    float* rec = &W[20 * (size_t)w];
-    uint32_t meta = 0;
-    for (int a = 0; a < 3; ++a) {
-      uint32_t eb = 0;
-      uint8_t ql[8], qh[8];
-      if (!quantize_axis(lo[a], hi[a], valid, 8, &rec[a], &eb, ql, qh)) return "an 8-wide node's boxes cannot be quantized";
-      meta |= eb << (8 * a);
-      uint32_t words[4] = {0, 0, 0, 0};   // qlo slots 0-3, 4-7, qhi slots 0-3, 4-7
-      for (int sl = 0; sl < 8; ++sl) {
-        words[sl >> 2] |= (uint32_t)ql[sl] << (8 * (sl & 3));
-        words[2 + (sl >> 2)] |= (uint32_t)qh[sl] << (8 * (sl & 3));
-      }
-      memcpy(&rec[4 + 4 * a], words, sizeof words);
-    }
-    // cull constants: c1 as the 8-bit code q (c1' = 1 - q / 512 <= c1; 255 =
-    // no bound, c1' = 0), E0 and E1 as bf16 rounded up
-    float cc[4];
-    node_cull_consts(co, cc);
-    uint32_t q = 255;
-    if (cc[0] > 0.0f) {
-      const double qd = ceil((1.0 - (double)cc[0]) * 512.0);
-      if (qd >= 0.0 && qd <= 254.0) q = (uint32_t)qd;
-    }
-    meta |= q << 24;
-    memcpy(&rec[3], &meta, 4);
-    memcpy(&rec[16], &child_base, 4);
-    memcpy(&rec[17], &leaf_base, 4);
-    memcpy(&rec[18], &smap, 4);
-    // bit 15 (E0's sign, E0 >= 0): all eight slots hold children -- code 15
-    // is then the eighth leaf, not an empty slot
-    const uint32_t e01 = bf16_up(cc[1]) | (bf16_up(cc[2]) << 16) | (ni + nl == 8 ? 0x8000u : 0u);
-    memcpy(&rec[19], &e01, 4);
-  }
-  if ((size_t)next_pos != n_tris) return "8-wide leaves do not cover the triangles once";
-  for (size_t i = 0; i < n_tris; ++i)
-    if (out->w8_pos_rank[i] < 0) return "8-wide leaves do not cover the triangles once";
-  // stack bound, as for the 4-wide nodes: a node pushes at most (inner children - 1)
-  const size_t nw = n_inner.size();
-  std::vector<int32_t> bound(nw, 0);
-  for (size_t w = nw; w-- > 0;) {   // children are allocated after their parent
-    int32_t m = 0;
-    for (int k = 0; k < n_inner[w]; ++k) m = std::max(m, bound[(size_t)first_kid[w] + k]);
-    bound[w] = std::max(0, n_inner[w] - 1) + m;
-  }
-  if (bound[0] > 4096) return "tree too deep for the wide walk's stack";
-  out->w8_n_nodes = (int)nw;
-  out->w8_stack_cap = bound[0] + 8;   // w8_step checks room for a whole node's pushes before it starts
-  return "";
-}
-
 }  // namespace
 
 std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float* V, size_t n_vf,
@@ -730,13 +517,6 @@ std::string build_wide_bvh(const float* N, size_t n, bool int_bits, const float*
       }
   out->n_nodes = (int)nw;
   out->stack_cap = bound[0] + 1;
-  out->w8_reason = build_w8(T, rank, n_tris, out->leaf_box, out);
-  if (!out->w8_reason.empty()) {
-    out->w8nodes.clear();
-    out->w8_pos_rank.clear();
-    out->w8_leaf_box.clear();
-    out->w8_n_nodes = 0;
-  }
   return "";
 }
 

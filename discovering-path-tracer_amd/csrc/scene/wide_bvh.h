@@ -24,15 +24,6 @@ struct WideBVH {
   std::vector<int32_t> rank_tri;   // leaf rank -> triangle slot (the reference's triIdx)
   int n_nodes = 0;
   int stack_cap = 0;               // most stack entries a walk can hold
-  // The 8-wide layout (wide_walk.h kW8NodeF4; PT_OPT_WIDE_NODE 80), collapsed
-  // from the same binary tree: 20 floats per node, children in octant slots,
-  // each node's leaves at consecutive *positions* (the walk's leaf index).
-  std::vector<float> w8nodes;
-  std::vector<int32_t> w8_pos_rank;   // leaf position -> rank (ties go to the lower rank)
-  std::vector<float> w8_leaf_box;     // 8 floats per position: the reference's leaf box {lo.xyz, 0, hi.xyz, 0}
-  int w8_n_nodes = 0;
-  int w8_stack_cap = 0;
-  std::string w8_reason = "not built";   // "" when the 8-wide layout was built
 };
 
 // How the 4-wide nodes group the reference's leaves.  Either way every child

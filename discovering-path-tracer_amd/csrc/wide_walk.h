@@ -221,11 +221,9 @@ template <bool QN = false>
 PT_FN bool wide_leaf_ok(const WideRay& R, const float4* __restrict__ leaf_box, int r) {
   return !QN || slab(R.o, R.inv, leaf_box[2 * (size_t)r], leaf_box[2 * (size_t)r + 1]);
 }
-// pos_rank (the 8-wide layout): r is a leaf position, and a tie in t goes to
-// the lower rank (the reference's visit order), read only for exact ties.
+// A tie in t goes to the lower rank (the reference's visit order).
 template <bool QN = false>
-PT_FN bool wide_cand(WideRay& R, int r, float4 A, float4 B, float4 C, const float4* __restrict__ leaf_box = nullptr,
-                     const int* __restrict__ pos_rank = nullptr) {
+PT_FN bool wide_cand(WideRay& R, int r, float4 A, float4 B, float4 C, const float4* __restrict__ leaf_box = nullptr) {
   float t;
   if (tri_test(R.o, R.d, A, B, C, &t)) {
     if (R.shadow) {
@@ -233,8 +231,7 @@ PT_FN bool wide_cand(WideRay& R, int r, float4 A, float4 B, float4 C, const floa
         R.best = 1;
         return true;
       }
-    } else if ((t < R.lim || (t == R.lim && R.best >= 0 &&
-                              (pos_rank ? pos_rank[r] < pos_rank[R.best] : r < R.best))) &&
+    } else if ((t < R.lim || (t == R.lim && R.best >= 0 && r < R.best)) &&
                wide_leaf_ok<QN>(R, leaf_box, r)) {   // :185
       R.lim = t;   // strict '<' in visit order
       R.best = r;
@@ -254,7 +251,7 @@ PT_FN bool wide_cand(WideRay& R, int r, float4 A, float4 B, float4 C, const floa
 #endif
 template <bool CNT, bool QN = false>
 PT_FN bool wide_flush(WideRay& R, const float4* __restrict__ tris, const int* cand, uint32_t* cl,
-                      const float4* __restrict__ leaf_box = nullptr, const int* __restrict__ pos_rank = nullptr) {
+                      const float4* __restrict__ leaf_box = nullptr) {
   const int n = R.nc;
   R.nc = 0;
   constexpr int KB = PT_WIDE_FLUSH_BATCH;
@@ -273,7 +270,7 @@ PT_FN bool wide_flush(WideRay& R, const float4* __restrict__ tris, const int* ca
     for (int k = 0; k < KB; ++k) {
       if (i + k < n) {
         if (CNT) ++*cl;
-        if (wide_cand<QN>(R, r[k], A[k], B[k], C[k], leaf_box, pos_rank)) return true;
+        if (wide_cand<QN>(R, r[k], A[k], B[k], C[k], leaf_box)) return true;
       }
     }
   }
@@ -397,140 +394,6 @@ PT_FN bool wide_step(WideRay& R, const float4* __restrict__ nodes, const float4*
     first = s;
   }
   R.cur = first == 0 ? c0 : first == 1 ? c1 : first == 2 ? c2 : c3;
-  return false;
-}
-
-// ---------------------------------------------------------------------------
-// 8-wide nodes (PT_OPT_WIDE_NODE 80, wide_bvh.cpp build_w8): 80 B = 5 float4
-//   [0] {p.xyz, meta}  meta bytes 0-2: biased exponent of the axis grid step,
-//       byte 3: c1 code q (c1 = 1 - q / 512, rounded down; 255: c1 = 0)
-//   [1] x: {qlo slots 0-3, qlo slots 4-7, qhi slots 0-3, qhi slots 4-7} (a byte each)
-//   [2] y, [3] z: the same
-//   [4] {child_base, leaf_base, slot map, E0 | E1 << 16 (bf16, rounded up)}
-// Slot map nibble s: 15 empty; 8 | k: the leaf at position leaf_base + k;
-// k: the inner node child_base + k.  Bit 15 of the E0|E1 word (E0's sign):
-// all eight slots are children, code 15 then being the eighth leaf.  Leaf positions index the triangle
-// records and exact leaf boxes (both by position) and pos_rank.
-// Children sit in octant slots (bit a: the high side of axis a); a ray with
-// direction sign bits oc takes slot i ^ oc as its i-th child, so its walk
-// order is near to far without a sort: the child bytes are permuted once per
-// node with v_perm, the slot map's nibbles with a rotate, a byte swap and a
-// nibble swap.  The nearest live inner child (least t_near) is expanded next,
-// the others pushed in that order, farthest first.  Every child box encloses
-// the boxes below it (rounded outward on the node's grid), so the cull and
-// the exactness argument are those above; a leaf's exact box is tested
-// before its hit counts (wide_cand<QN>).  The walk queues a node's leaf hits
-// while its queue has room (kWideQ) and tests the rest at once.
-constexpr int kW8NodeF4 = 5;
-PT_FN uint32_t w8_perm(uint32_t hi_word, uint32_t lo_word, uint32_t sel) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_perm(hi_word, lo_word, sel);
-#else   // host harness: byte k of the result = byte sel_k of {lo_word (0-3), hi_word (4-7)}
-  const uint64_t b = ((uint64_t)hi_word << 32) | lo_word;
-  uint32_t r = 0;
-  for (int k = 0; k < 4; ++k) r |= (uint32_t)((b >> (8 * ((sel >> (8 * k)) & 7u))) & 0xffu) << (8 * k);
-  return r;
-#endif
-}
-// the slot map with nibble i holding slot i ^ oc's code
-PT_FN uint32_t w8_slot_order(uint32_t m, uint32_t oc) {
-  if (oc & 4u) m = (m >> 16) | (m << 16);
-  if (oc & 2u) m = ((m & 0x00ff00ffu) << 8) | ((m >> 8) & 0x00ff00ffu);
-  if (oc & 1u) m = ((m & 0x0f0f0f0fu) << 4) | ((m >> 4) & 0x0f0f0f0fu);
-  return m;
-}
-PT_FN float w8_byte(uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xffu); }
-
-template <bool CNT, bool QUEUE>
-PT_FN bool w8_step(WideRay& R, const float4* __restrict__ nodes, const float4* __restrict__ tris, int2* lds, int ls,
-                   int2* ovf, long long os, int stack_cap, bool* exact, uint32_t* cn, uint32_t* cl, int* cand,
-                   const float4* __restrict__ leaf_box, const int* __restrict__ pos_rank) {
-  while (R.cur < 0) {
-    if (R.sp == 0) return true;
-    const int2 e = wide_pop(R, lds, ls, ovf, os);
-    if (!(R.lim < u2f((uint32_t)e.y))) R.cur = e.x;   // still able to hold a winner
-  }
-  const float4* nd = nodes + (size_t)R.cur * kW8NodeF4;
-  const float4 h = nd[0], qx = nd[1], qy = nd[2], qz = nd[3], m = nd[4];
-  if (CNT) ++*cn;
-  const uint32_t oc = (f2u(R.d.x) >> 31) | ((f2u(R.d.y) >> 31) << 1) | ((f2u(R.d.z) >> 31) << 2);
-  const uint32_t ocb = oc * 0x01010101u;
-  const uint32_t meta = f2u(h.w);
-  const float sx = wq_scale(meta, 0), sy = wq_scale(meta, 1), sz = wq_scale(meta, 2);
-  const uint32_t q = meta >> 24;
-  const uint32_t e01 = f2u(m.w);
-  const float4 kf = make_float4(q == 255u ? 0.0f : fma_((float)q, -0x1p-9f, 1.0f), u2f((e01 & 0x7fffu) << 16),
-                                u2f(e01 & 0xffff0000u), 0.0f);
-  const uint32_t empty = (e01 & 0x8000u) ? 16u : 15u;   // the code of an empty slot (none when full)
-  const int child_base = (int)f2u(m.x), leaf_base = (int)f2u(m.y);
-  const uint32_t pm = w8_slot_order(f2u(m.z), oc);
-  const v3 ainv = wide_ainv(R);
-  if (R.sp + 7 > stack_cap) {   // cannot happen with the builder's bound; stay memory-safe
-    *exact = true;
-    return true;
-  }
-  // Children in walk order i (slot i ^ oc), streamed from the last to the
-  // first: a live inner child is pushed at once unless it is the nearest so
-  // far (least t_near), which is kept (the one it displaces is pushed then)
-  // and expanded next; the stack so pops the others near to far in walk order.
-  int keep = -1;        // node index of the nearest live inner child so far
-  uint32_t keep_th = 0u;
-  float keep_tn = __builtin_inff();
-  uint32_t now = 0u;    // leaf hits the queue had no room for
-#pragma unroll
-  for (int half = 1; half >= 0; --half) {
-    // child i's bytes (slot i ^ oc) at byte i & 3 of the permuted words
-    const uint32_t sel = (half ? 0x07060504u : 0x03020100u) ^ ocb;
-    const uint32_t wlx = w8_perm(f2u(qx.y), f2u(qx.x), sel), whx = w8_perm(f2u(qx.w), f2u(qx.z), sel);
-    const uint32_t wly = w8_perm(f2u(qy.y), f2u(qy.x), sel), why = w8_perm(f2u(qy.w), f2u(qy.z), sel);
-    const uint32_t wlz = w8_perm(f2u(qz.y), f2u(qz.x), sel), whz = w8_perm(f2u(qz.w), f2u(qz.z), sel);
-#pragma unroll
-    for (int k = 3; k >= 0; --k) {
-      const int i = 4 * half + k;
-      bool hit;
-      float tn, th;
-      wide_child(R, ainv, fma_(w8_byte(wlx, k), sx, h.x), fma_(w8_byte(whx, k), sx, h.x),
-                 fma_(w8_byte(wly, k), sy, h.y), fma_(w8_byte(why, k), sy, h.y), fma_(w8_byte(wlz, k), sz, h.z),
-                 fma_(w8_byte(whz, k), sz, h.z), kf, &hit, &tn, &th);
-      const uint32_t code = (pm >> (4 * i)) & 15u;
-      hit = hit && code != empty && !(R.lim < th);
-      if (hit && (code & 8u)) {   // a leaf: queued for the wave-wide flush, or tested below
-        if (QUEUE && R.nc < kWideQ) {
-          cand[R.nc * 64] = leaf_base + (int)(code & 7u);
-          ++R.nc;
-        } else {
-          now |= 1u << i;
-        }
-      } else if (hit) {
-        const int ref = child_base + (int)code;
-        const bool nearer = tn < keep_tn;
-        if (keep >= 0 || !nearer) {   // push the farther of (kept, this)
-          const int pr = nearer ? keep : ref;
-          const uint32_t pt = nearer ? keep_th : f2u(th);
-          wide_push(R, make_int2(pr, (int)pt), lds, ls, ovf, os);
-        }
-        if (nearer) {
-          keep = ref;
-          keep_th = f2u(th);
-          keep_tn = tn;
-        }
-      }
-    }
-  }
-  R.cur = keep;
-  while (now) {   // (tested even if a hit found meanwhile culls it: an extra test cannot change the answer)
-    const int i = __builtin_ctz(now);
-    now &= now - 1u;
-    const int r = leaf_base + (int)((pm >> (4 * i)) & 7u);
-    if (CNT) ++*cl;
-    const float4* T = tris + 3 * (size_t)r;
-    if (wide_cand<true>(R, r, T[0], T[1], T[2], leaf_box, pos_rank)) {   // an occluded shadow ray
-      R.cur = -1;
-      R.sp = 0;
-      return true;
-    }
-  }
-  if (R.cur >= 0 && R.lim < u2f(keep_th)) R.cur = -1;   // culled by a hit found just now
   return false;
 }
 

@@ -34,7 +34,8 @@ PT_OPT_WIDE_BUILD = 14
 PT_OPT_WF_FUSE = 15
 PT_OPT_WIDE_NODE = 16
 PT_OPT_WF_TAIL = 17
-KERNEL_AUTO, KERNEL_RECURSIVE, KERNEL_STATE_MACHINE, KERNEL_WAVEFRONT = 0, 1, 2, 3
+PT_OPT_GROUP_EXCHANGE = 18
+KERNEL_AUTO, KERNEL_RECURSIVE, KERNEL_WAVEFRONT = 0, 1, 3   # 2 (lane state machine) was removed
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).
 EXPORTS = [
@@ -50,7 +51,7 @@ EXPORTS = [
     "pt_items_live", "pt_items_pack", "pt_items_unpack_all", "pt_render_packed", "pt_launch_span_ms",
     "pt_set_partition_slots", "pt_get_traced", "pt_wide_info", "pt_partition_items",
     "pt_dist_unique_id", "pt_dist_init", "pt_dist_run", "pt_dist_slot_floats", "pt_dist_finalize",
-    "pt_dist_set_streams", "pt_dist_wait", "pt_dist_abort",
+    "pt_dist_set_streams", "pt_dist_wait", "pt_dist_abort", "pt_create_multi", "pt_group_info",
 ]
 
 
@@ -87,6 +88,8 @@ def lib():
         sig = {
             "pt_abi_version": ([], i32), "pt_last_error": ([], ctypes.c_char_p),
             "pt_create": ([i32, ctypes.POINTER(vp)], i32), "pt_destroy": ([vp], i32),
+            "pt_create_multi": ([vp, i32, ctypes.POINTER(vp)], i32),
+            "pt_group_info": ([vp, ctypes.POINTER(i32), vp, i32, ctypes.POINTER(i32)], i32),
             "pt_set_stream": ([vp, vp], i32), "pt_synchronize": ([vp], i32),
             "pt_upload_scene": ([vp, vp, sz, vp, sz, vp, sz, vp, sz, vp, sz, u32], i32),
             "pt_upload_lights": ([vp, vp, sz], i32), "pt_set_camera": ([vp, vp], i32),
@@ -331,10 +334,25 @@ def default_camera():
 class Renderer:
     """One GPU's path tracer: upload, dispatch/render, read back."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, devices=None):
+        """One GPU (pt_create), or with `devices` (a list of ordinals) one
+        context over all of them (pt_create_multi: tile split, the frame on
+        devices[0])."""
         self._c = ctypes.c_void_p()
-        _check(lib().pt_create(device, ctypes.byref(self._c)), "pt_create")
+        if devices is None:
+            _check(lib().pt_create(device, ctypes.byref(self._c)), "pt_create")
+        else:
+            d = np.ascontiguousarray(devices, np.int32)
+            _check(lib().pt_create_multi(d.ctypes.data, d.size, ctypes.byref(self._c)), "pt_create_multi")
         self.width = self.height = 0
+
+    def group_info(self):
+        """(device ordinals, members store straight into the frame)."""
+        n, peer = ctypes.c_int(0), ctypes.c_int(0)
+        devs = np.zeros(64, np.int32)
+        _check(lib().pt_group_info(self._c, ctypes.byref(n), devs.ctypes.data, devs.size, ctypes.byref(peer)),
+               "pt_group_info")
+        return [int(x) for x in devs[:n.value]], bool(peer.value)
 
     def upload_scene(self, vertices, indices, nodes, uvs=None, mat=None, int_bits=False):
         v = np.ascontiguousarray(vertices, np.float32).reshape(-1)
@@ -428,7 +446,7 @@ class Renderer:
         _check(lib().pt_set_option(self._c, key, value), "pt_set_option")
 
     def last_kernel(self):
-        """Kernel of the last render: KERNEL_RECURSIVE, KERNEL_STATE_MACHINE or KERNEL_WAVEFRONT."""
+        """Kernel of the last render: KERNEL_RECURSIVE or KERNEL_WAVEFRONT."""
         k = ctypes.c_int(0)
         _check(lib().pt_last_kernel(self._c, ctypes.byref(k)), "pt_last_kernel")
         return k.value

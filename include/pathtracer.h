@@ -99,6 +99,26 @@ const char* pt_last_error(void);
 /* Replaces VulkanWindow's device/queue selection (VulkanWindow.cpp:106-174)
  * and VulkanRayTracer::initComputePipeline's pipeline creation (:624-672). */
 int pt_create(int device_ordinal, pt_context** out);
+/* One context over n devices of this process (SURVEY.md §8b create(device
+ * ordinals[], n)): the reference's single host thread (VulkanRenderer.cpp:
+ * 643-647, mainLoop VulkanRayTracer.cpp:717-865) drives all of them through
+ * the calls below exactly as it drives one.  Member r renders the 16x16
+ * screen tiles of rank r of an n-way pt_set_partition; the frame lives in
+ * device memory of device_ordinals[0] (pt_accum_device_ptr), where pt_read_accum,
+ * pt_readback_* and pt_synchronize see every member's tiles, bit-identical to
+ * a single-GPU render.  Members store their tiles into that frame directly
+ * over xGMI (peer access), or -- when a member cannot map it, or with
+ * PT_OPT_GROUP_EXCHANGE 1 -- ship them as packed tiles copied to the first
+ * device.  An ordinal may repeat (several members on one device: tests).
+ * Calls on a member's share (pt_set_partition*, pt_tiles_*, pt_items_*,
+ * pt_render_packed, pt_dist_*) return PT_ERR_UNSUPPORTED on such a context;
+ * the launch-timing calls report the first device's launches.  pt_destroy
+ * frees it. */
+int pt_create_multi(const int* device_ordinals, int n, pt_context** out);
+/* Devices of a context (1 and its ordinal for a pt_create context) and
+ * whether its members store their tiles straight into the frame (1) or ship
+ * packed tiles (0). */
+int pt_group_info(pt_context* ctx, int* n_devices, int* devices, int max_devices, int* peer_stores);
 int pt_destroy(pt_context* ctx);
 /* Launch on a caller-owned hipStream_t (e.g. a torch.cuda.Stream's handle);
  * NULL returns to the context's own stream — so the legacy default stream
@@ -254,8 +274,9 @@ int pt_dist_run(pt_context* ctx, uint32_t n_batches, int n_frames, int n_streams
                 int n_frame_bufs);
 /* Run the loop on caller-owned streams (e.g. torch streams) instead of the
  * ones it creates: the first two render streams and the gather stream (null
- * keeps the library's own; the third render stream is always the
- * library's).  The library creates its render streams at the least priority
+ * keeps the library's own).  With caller render streams pt_dist_run takes at
+ * most 2 streams (PT_ERR_INVALID for 3, which would mix in a library stream
+ * outside the caller's ordering).  The library creates its render streams at the least priority
  * and the gather stream at the greatest: the HIP runtime keeps a pool of
  * GPU_MAX_HW_QUEUES hardware queues per priority, so each render stream gets
  * a queue of its own. */
@@ -282,14 +303,13 @@ int pt_dist_finalize(pt_context* ctx);
  * 0 (default) = read the accumulator, as the reference does (prev * 0). */
 #define PT_OPT_FRESH_BATCH0 3
 /* PT_OPT_KERNEL: 0 auto (wavefront for scenes of >= 32768 triangles that
- * are not LDS-resident, else path-recursive), 1 path-recursive, 2 lane state
- * machine (slower on every scene measured; kept for comparison), 3 wavefront
+ * are not LDS-resident, else path-recursive), 1 path-recursive, 3 wavefront
  * pipeline (paths held in device memory, traversal and shading in separate
  * kernels; 416 bytes of device memory per pixel x sample, at most 2^27 paths
  * per chunk; not with stats mode; auto picks it from 16384 triangles with the
- * culled wide walk).  Output is identical for every value.
- * PT_OPT_SM_BATCH: state machine only — finished rays wait until this many
- * lanes of the wave need shading (1..64, default 1).  Output is identical. */
+ * culled wide walk).  Output is identical for every value.  2 (a lane state
+ * machine, measured slower on every scene) was removed: PT_ERR_UNSUPPORTED,
+ * as is PT_OPT_SM_BATCH, its only knob. */
 #define PT_OPT_KERNEL 4
 #define PT_OPT_SM_BATCH 5
 /* PT_OPT_PRIMARY_CULL: 1 (default) = a pixel whose every possible primary
@@ -317,11 +337,8 @@ int pt_dist_finalize(pt_context* ctx);
 /* PT_OPT_COUNT_TRACED: 1 = run the fast kernels with counters of the work
  * they actually do (pt_get_traced); slower, output identical.  Default 0. */
 #define PT_OPT_COUNT_TRACED 10
-/* PT_OPT_PAIRS: 1 = the wavefront pipeline walks device-memory scenes over
- * child-pair records (both child boxes of an internal node in one 64-B
- * record, the right subtree first, pending siblings on a per-lane LDS
- * stack); 0 (default) = the threaded node walk, faster on the BASELINE
- * scenes.  Output is identical. */
+/* PT_OPT_PAIRS: 0 only.  1 (child-pair records, measured slower on every
+ * scene) was removed: PT_ERR_UNSUPPORTED. */
 #define PT_OPT_PAIRS 11
 /* PT_OPT_WIDE: 1 (default) = the wavefront pipeline walks device-memory
  * scenes over a 4-wide BVH of the reference's own boxes, nearest child first,
@@ -357,10 +374,9 @@ int pt_dist_finalize(pt_context* ctx);
 /* PT_OPT_WIDE_NODE: byte size of the culled wide walk's nodes.  64 (default)
  * = child boxes rounded outward onto an 8-bit grid per node (half the bytes
  * and load instructions per node visit; a leaf's exact box is tested before
- * its hit counts); 128 = the boxes as floats; 80 = 8-wide nodes on the same
- * grid, children in direction-octant slots (a third fewer node visits, but
- * twice the box tests per visit: measured slower, an option).  All are built
- * at upload.  Output is identical. */
+ * its hit counts); 128 = the boxes as floats.  Both are built at upload.
+ * Output is identical.  80 (8-wide nodes, measured slower) was removed:
+ * PT_ERR_UNSUPPORTED. */
 #define PT_OPT_WIDE_NODE 16
 /* PT_OPT_WF_TAIL: with the culled wide walk (4-wide nodes), once a ray
  * round's list holds fewer than this many rays, one persistent launch runs
@@ -369,6 +385,12 @@ int pt_dist_finalize(pt_context* ctx);
  * round; 0 = never; -1 (default) = auto (400000 rays).  Output is
  * identical. */
 #define PT_OPT_WF_TAIL 17
+/* PT_OPT_GROUP_EXCHANGE (pt_create_multi contexts only): 0 (default) = each
+ * member stores its tiles straight into the frame on the first device (peer
+ * access over xGMI) when every member can map it, else packed copies; 1 =
+ * always packed copies (pt_tiles_pack, hipMemcpyPeerAsync, pt_tiles_unpack).
+ * Output is identical. */
+#define PT_OPT_GROUP_EXCHANGE 18
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */

@@ -53,9 +53,6 @@ def lib():
         L.wide_set_variant.argtypes = [ctypes.c_int, ctypes.c_int]
         L.wide_dump.argtypes = [F32P, sz, U32P, sz, F32P, sz, ctypes.c_int, F32P, sz, I32P, ctypes.c_char_p, sz]
         L.wide_dump.restype = ctypes.c_longlong
-        L.wide_dump8.argtypes = [F32P, sz, U32P, sz, F32P, sz, ctypes.c_int, F32P, sz, I32P, F32P, ctypes.c_char_p,
-                                 sz]
-        L.wide_dump8.restype = ctypes.c_longlong
         L.wide_counts.argtypes = [F32P, sz, U32P, sz, F32P, sz, ctypes.c_int, F32P, sz, I32P, I32P, ctypes.c_char_p,
                                   sz]
         _LIB = L
@@ -74,12 +71,11 @@ WIDE_FROM_REFERENCE, WIDE_SAH = 0, 1
 # leaf's exact box before its hit counts (wide_walk.h); queued: leaf hits are
 # tested in flushes, as one lane of the trace kernel does (PT_WIDE_QUEUE)
 BUILDS = pytest.mark.parametrize(
-    "build", [(WIDE_SAH, 80, 1), (WIDE_SAH, 80, 0), (WIDE_SAH, 64, 1), (WIDE_SAH, 64, 0), (WIDE_SAH, 128, 1),
-              (WIDE_SAH, 128, 0), (WIDE_FROM_REFERENCE, 80, 1), (WIDE_FROM_REFERENCE, 64, 1),
-              (WIDE_FROM_REFERENCE, 128, 0), (WIDE_SAH, 64, 2), (WIDE_SAH, 128, 2), (WIDE_FROM_REFERENCE, 64, 2)],
-    ids=["sah-w8-queue", "sah-w8", "sah-64-queue", "sah-64", "sah-128-queue", "sah-128", "reference_tree-w8-queue",
-         "reference_tree-64-queue", "reference_tree-128", "sah-64-waveflush", "sah-128-waveflush",
-         "reference_tree-64-waveflush"])
+    "build", [(WIDE_SAH, 64, 1), (WIDE_SAH, 64, 0), (WIDE_SAH, 128, 1), (WIDE_SAH, 128, 0),
+              (WIDE_FROM_REFERENCE, 64, 1), (WIDE_FROM_REFERENCE, 128, 0), (WIDE_SAH, 64, 2), (WIDE_SAH, 128, 2),
+              (WIDE_FROM_REFERENCE, 64, 2)],
+    ids=["sah-64-queue", "sah-64", "sah-128-queue", "sah-128", "reference_tree-64-queue", "reference_tree-128",
+         "sah-64-waveflush", "sah-128-waveflush", "reference_tree-64-waveflush"])
 
 
 def check(v, idx, nodes, rays, build=(WIDE_SAH, 64, 1)):
@@ -309,84 +305,3 @@ def test_wide_tree_invariants(build):
                 below = leaves_below(r)
                 assert (leaf_lo[below] >= lo[w, j]).all() and (leaf_hi[below] <= hi[w, j]).all()
     assert (seen == 1).all()
-
-
-def _dump8(v, idx, nodes, build):
-    L = lib()
-    L.wide_set_mode(build)
-    nt = idx.size // 3
-    cap = 20 * (nt + 8)
-    out = np.zeros(cap, np.float32)
-    pr = np.zeros(nt, np.int32)
-    lb = np.zeros(8 * nt, np.float32)
-    err = ctypes.create_string_buffer(256)
-    n = L.wide_dump8(v, v.size, idx, nt, nodes, nodes.size // 8, 0, out, cap, pr, lb, err, 256)
-    assert n > 0, err.value.decode()
-    return out[:n].reshape(-1, 20).copy(), pr, lb.reshape(-1, 8)
-
-
-def w8_decode(W):
-    """Child boxes (node, slot, axis) as the kernel decodes them
-    (fma(q, 2^e, p)), slot codes, child and leaf bases."""
-    u = W.view(np.uint32)
-    meta = u[:, 3]
-    lo = np.zeros((len(W), 8, 3), np.float32)
-    hi = np.zeros((len(W), 8, 3), np.float32)
-    for a in range(3):
-        e = ((meta >> np.uint32(8 * a)) & np.uint32(0xff)).astype(np.int64) - 127
-        s = np.ldexp(np.float64(1.0), e)
-        p = W[:, a].astype(np.float64)
-        for sl in range(8):
-            wl = u[:, 4 + 4 * a + (sl >> 2)]
-            wh = u[:, 4 + 4 * a + 2 + (sl >> 2)]
-            ql = ((wl >> np.uint32(8 * (sl & 3))) & np.uint32(0xff)).astype(np.float64)
-            qh = ((wh >> np.uint32(8 * (sl & 3))) & np.uint32(0xff)).astype(np.float64)
-            lo[:, sl, a] = (ql * s + p).astype(np.float32)   # q*s exact: one rounding, as fmaf
-            hi[:, sl, a] = (qh * s + p).astype(np.float32)
-    codes = np.stack([(u[:, 18] >> np.uint32(4 * sl)) & np.uint32(15) for sl in range(8)], 1).astype(np.int64)
-    full = (u[:, 19] & np.uint32(0x8000)) != 0
-    codes[~full] = np.where(codes[~full] == 15, -1, codes[~full])   # -1: empty slot
-    return lo, hi, codes, u[:, 16].astype(np.int64), u[:, 17].astype(np.int64)
-
-
-@pytest.mark.parametrize("build", [WIDE_SAH, WIDE_FROM_REFERENCE], ids=["sah", "reference_tree"])
-def test_w8_tree_invariants(build):
-    """The 8-wide layout's premises: every leaf position once and its rank
-    once; each decoded child box encloses every reference leaf box below it
-    (so the slab test passes wherever the reference's does); the leaf box
-    stored by position is the reference's, bitwise."""
-    sv, si = scenes.displaced_sphere(subdiv=3)
-    v, idx, nodes = _scene(sv, si)
-    W, pos_rank, lbox = _dump8(v, idx, nodes, build)
-    nt = idx.size // 3
-    assert np.array_equal(np.sort(pos_rank), np.arange(nt))
-    N = nodes.reshape(-1, 8)
-    order, st = [], [0]
-    while st:
-        k = st.pop()
-        if N[k, 3] == -1:
-            order.append(k)
-        else:
-            st += [int(N[k, 3]), int(N[k, 7])]
-    leaf_lo, leaf_hi = N[order, 0:3], N[order, 4:7]
-    assert np.array_equal(lbox[:, 0:3].view(np.uint32), leaf_lo[pos_rank].view(np.uint32))
-    assert np.array_equal(lbox[:, 4:7].view(np.uint32), leaf_hi[pos_rank].view(np.uint32))
-    lo, hi, codes, cb, lb = w8_decode(W)
-    seen = np.zeros(nt, np.int32)
-    below = [None] * len(W)
-    for w in range(len(W) - 1, -1, -1):   # children come after their parent
-        allp = []
-        for sl in range(8):
-            c = int(codes[w, sl])
-            if c < 0:
-                continue
-            if c & 8:
-                pos = [int(lb[w]) + (c & 7)]
-                seen[pos[0]] += 1
-            else:
-                pos = below[int(cb[w]) + c]
-            pl, ph = leaf_lo[pos_rank[pos]], leaf_hi[pos_rank[pos]]
-            assert np.all(lo[w, sl] <= pl) and np.all(hi[w, sl] >= ph), (w, sl)
-            allp += pos
-        below[w] = allp
-    assert np.all(seen == 1)

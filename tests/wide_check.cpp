@@ -26,7 +26,6 @@ int g_queue = 0;             // ... and 1: the queued leaf tests with per-lane f
 struct Built {
   pt::WideBVH w;
   std::vector<float4> tris;    // by rank: {v0, e1.x} {e1.yz, e2.xy} {e2.z, n}
-  std::vector<float4> tris8;   // the same records by 8-wide leaf position
 };
 
 std::string build(const float* V, size_t nvf, const uint32_t* I, size_t nt, const float* N, size_t nn, int int_bits,
@@ -47,37 +46,7 @@ std::string build(const float* V, size_t nvf, const uint32_t* I, size_t nt, cons
     b->tris[3 * r + 1] = make_float4(e1.y, e1.z, e2.x, e2.y);
     b->tris[3 * r + 2] = make_float4(e2.z, n.x, n.y, n.z);
   }
-  if (g_node == 80) {
-    if (!b->w.w8_reason.empty()) return "8-wide: " + b->w.w8_reason;
-    b->tris8.resize(3 * nt);
-    for (size_t p = 0; p < nt; ++p)
-      for (int k = 0; k < 3; ++k) b->tris8[3 * p + k] = b->tris[3 * (size_t)b->w.w8_pos_rank[p] + k];
-  }
   return "";
-}
-
-// The 8-wide walk (w8_step), queued or not, flushed as walk() does.
-template <bool QUEUE>
-void walk8(WideRay& R, const Built& b, int2* lds, int2* ovf, bool* exact, uint32_t* cn, uint32_t* cl) {
-  const float4* nodes = (const float4*)b.w.w8nodes.data();
-  const float4* leafbox = (const float4*)b.w.w8_leaf_box.data();
-  const int* pr = b.w.w8_pos_rank.data();
-  std::vector<int> cand(kWideQ * 64, -1);
-  bool fin = false;
-  for (;;) {
-    if (!fin)
-      fin = w8_step<true, QUEUE>(R, nodes, b.tris8.data(), lds, 1, ovf, 1, b.w.w8_stack_cap, exact, cn, cl,
-                                 cand.data(), leafbox, pr);
-    if (*exact) return;
-    if (QUEUE && (R.nc > kWideQ - 4 || (fin && R.nc > 0))) {
-      if (wide_flush<true, true>(R, b.tris8.data(), cand.data(), cl, leafbox, pr)) {   // occluded
-        fin = true;
-        R.sp = 0;
-        R.cur = -1;
-      }
-    }
-    if (fin && R.nc == 0) return;
-  }
 }
 
 // One ray's walk in the configured variant, as the trace kernel runs it:
@@ -158,7 +127,7 @@ extern "C" {
 
 // The wide builder the next calls use (pt::WideBuild).
 void wide_set_mode(int mode) { g_mode = mode; }
-// The walk variant the next wide_check calls run: node bytes 64 or 128 (4-wide) or 80 (8-wide),
+// The walk variant the next wide_check calls run: node bytes 64 or 128,
 // queued leaf tests or not.
 void wide_set_variant(int node_bytes, int queue) {
   g_node = node_bytes;
@@ -174,8 +143,8 @@ int wide_info(const float* V, size_t nvf, const uint32_t* I, size_t nt, const fl
     snprintf(err, errlen, "%s", why.c_str());
     return 1;
   }
-  info[0] = g_node == 80 ? b.w.w8_n_nodes : b.w.n_nodes;
-  info[1] = g_node == 80 ? b.w.w8_stack_cap : b.w.stack_cap;
+  info[0] = b.w.n_nodes;
+  info[1] = b.w.stack_cap;
   return 0;
 }
 
@@ -199,28 +168,6 @@ long long wide_dump(const float* V, size_t nvf, const uint32_t* I, size_t nt, co
   return (long long)w.nodes.size();
 }
 
-// The 8-wide layout of the built tree: node floats (20 per node) into nodes
-// (room for cap floats), position -> rank into pos_rank, the leaf boxes by
-// position into leaf_box (8 floats each).  Returns the float count, or -1.
-long long wide_dump8(const float* V, size_t nvf, const uint32_t* I, size_t nt, const float* N, size_t nn, int int_bits,
-                     float* nodes, size_t cap, int32_t* pos_rank, float* leaf_box, char* err, size_t errlen) {
-  pt::WideBVH w;
-  std::string why = pt::build_wide_bvh(N, nn, int_bits != 0, V, nvf, I, nt, &w, g_mode);
-  if (why.empty()) why = w.w8_reason;
-  if (!why.empty()) {
-    snprintf(err, errlen, "%s", why.c_str());
-    return -1;
-  }
-  if (w.w8nodes.size() > cap || w.w8_pos_rank.size() != nt) {
-    snprintf(err, errlen, "buffer too small");
-    return -1;
-  }
-  memcpy(nodes, w.w8nodes.data(), w.w8nodes.size() * sizeof(float));
-  memcpy(pos_rank, w.w8_pos_rank.data(), nt * sizeof(int32_t));
-  memcpy(leaf_box, w.w8_leaf_box.data(), 8 * nt * sizeof(float));
-  return (long long)w.w8nodes.size();
-}
-
 // rays: n x 8 floats {o.xyz, d.xyz, kind (0 closest, 1 shadow), limit}.
 // out: n x 4 {wide t|lim, wide hit/occluded (-1 exact walk needed), oracle t, oracle hit/occluded}.
 // stats: [0] closest mismatches [1] shadow mismatches [2] exact hand-backs
@@ -234,7 +181,7 @@ int wide_check(const float* V, size_t nvf, const uint32_t* I, size_t nt, const f
     snprintf(err, errlen, "%s", why.c_str());
     return 1;
   }
-  std::vector<int2> lds(kWideLds), ovf((size_t)std::max(b.w.stack_cap, b.w.w8_stack_cap) + 1);
+  std::vector<int2> lds(kWideLds), ovf((size_t)(size_t)b.w.stack_cap + 1);
   memset(stats, 0, 8 * sizeof(uint64_t));
   stats[7] = ~0ull;
   for (size_t i = 0; i < n; ++i) {
@@ -254,10 +201,7 @@ int wide_check(const float* V, size_t nvf, const uint32_t* I, size_t nt, const f
     bool exact = !wide_ray_ok(R.o, R.d, R.inv);
     uint32_t cn = 0, cl = 0;
     if (!exact) {
-      if (g_node == 80)
-        g_queue ? walk8<true>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl)
-                : walk8<false>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl);
-      else if (g_node == 64)
+      if (g_node == 64)
         g_queue ? walk<true, true>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl)
                 : walk<true, false>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl);
       else
@@ -289,7 +233,7 @@ int wide_check(const float* V, size_t nvf, const uint32_t* I, size_t nt, const f
       bad = (R.best >= 0) != ohit;
       if (!bad && ohit) {
         // same t bits and the same triangle (its geometric normal, :189)
-        const float4* T = g_node == 80 ? &b.tris8[3 * (size_t)R.best] : &b.tris[3 * (size_t)R.best];
+        const float4* T = &b.tris[3 * (size_t)R.best];
         const v3 e1 = mk(T[0].w, T[1].x, T[1].y), e2 = mk(T[1].z, T[1].w, T[2].x);
         const v3 nn3 = normalize(cross(e1, e2));
         bad = memcmp(&R.lim, &ref[1], 4) != 0 || memcmp(&nn3.x, &ref[5], 4) != 0 ||
@@ -314,7 +258,7 @@ int wide_counts(const float* V, size_t nvf, const uint32_t* I, size_t nt, const 
     snprintf(err, errlen, "%s", why.c_str());
     return 1;
   }
-  std::vector<int2> lds(kWideLds), ovf((size_t)std::max(b.w.stack_cap, b.w.w8_stack_cap) + 1);
+  std::vector<int2> lds(kWideLds), ovf((size_t)(size_t)b.w.stack_cap + 1);
   for (size_t i = 0; i < n; ++i) {
     const float* r = rays + 8 * i;
     WideRay R;
@@ -322,10 +266,7 @@ int wide_counts(const float* V, size_t nvf, const uint32_t* I, size_t nt, const 
     bool exact = !wide_ray_ok(R.o, R.d, R.inv);
     uint32_t cn = 0, cl = 0;
     if (!exact) {
-      if (g_node == 80)
-        g_queue ? walk8<true>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl)
-                : walk8<false>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl);
-      else if (g_node == 64)
+      if (g_node == 64)
         g_queue ? walk<true, true>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl)
                 : walk<true, false>(R, b, lds.data(), ovf.data(), &exact, &cn, &cl);
       else
