@@ -274,6 +274,44 @@ SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 12, "sphere_1080p8", 3),
               ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5, "synthetic10M_1080p8", 1))
 
 
+# Which measured gather ceiling bounds each leg's trace kernel
+# (tools/gather_roof.hip, dependent 64-B chains at 6 workgroups per CU,
+# profiles/r04/gather_roof.jsonl): the 2.6-MB wide tree of the displaced
+# sphere (configs 3, 4) is L2-resident; the 10M cloud's 313-MB 64-B tree is
+# not (its leg keeps the HBM roofline primary; the chase ceiling is beside
+# it).
+GATHER_CASES = {"sphere_1080p8": ("l2_gather", "l2_4MB"), "sphere_4k16_d8": ("l2_gather", "l2_4MB")}
+
+
+def gather_roofline(workload):
+    if workload not in GATHER_CASES:
+        return None
+    bound, case = GATHER_CASES[workload]
+    path = os.path.join(ROOT, "profiles", "r04", "gather_roof.jsonl")
+    try:
+        rows = [json.loads(x) for x in open(path) if x.strip()]
+    except (OSError, ValueError):
+        return None
+    for d in rows:
+        if d.get("pattern") == "dependent_chain" and d.get("case") == case and d.get("record_B") == 64:
+            return {"bound": bound, "Grec_per_s": d["Grec_per_s"],
+                    "basis": f"tools/gather_roof.hip: dependent chains of 64-B records over a {d['table_MB']}-MB "
+                             f"table, {d['blocks']} workgroups of 256 (6 per CU, the trace kernel's occupancy), one "
+                             f"load in flight per lane ({os.path.relpath(path, ROOT)})"}
+    return None
+
+
+def trace_share(prof):
+    """wf_trace_wide_kernel's share of the frame's kernel time in a committed
+    rocprofv3 summary (None without one)."""
+    if prof is None:
+        return None
+    ks = prof[1].get("kernels", {})
+    tot = sum(v.get("total_ns", 0.0) for k, v in ks.items() if "ptd::" in k)
+    tr = sum(v.get("total_ns", 0.0) for k, v in ks.items() if "wf_trace_wide_kernel" in k)
+    return tr / tot if tot > 0 and tr > 0 else None
+
+
 def time_frames(r, spp, steps):
     """`steps` timed frames, one at a time (each synchronized): wall ms per
     frame and the kernel ms of each frame's launches (HIP events)."""
@@ -437,6 +475,29 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
                                       "stream)"),
            "contexts": contexts,
            "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
+    gather = gather_roofline(workload)
+    if gather is not None:
+        # the wide walk's node fetches against the measured ceiling of
+        # dependent 64-B gathers from a table of the tree's size (one fetch
+        # in flight per lane, the trace kernel's occupancy): the tree of
+        # configs 3/4 (2.6 MB) lives in L2, so HBM is not its bound
+        visits = float(traced["nodes"])
+        ach = visits / (kernel_ms * 1e-3) / 1e9
+        roof = {"bound": gather["bound"], "achieved": round(ach, 3), "peak": gather["Grec_per_s"],
+                "unit": "G wide-node fetches/s", "frac": round(ach / gather["Grec_per_s"], 4),
+                "traffic": out["roofline"]["traffic"], "node_visits_per_frame": int(visits),
+                "time_basis": out["roofline"]["time_basis"] + "; every kernel of the frame",
+                "peak_basis": gather["basis"], "hbm": {k: out["roofline"][k] for k in
+                                                       ("achieved", "peak", "unit", "frac", "traffic",
+                                                        "traffic_source")}}
+        share = trace_share(prof)
+        if share is not None:
+            # the trace kernel's own time: its share of the frame's kernel
+            # time in the committed profile of this source and workload
+            roof["trace_kernel_share"] = round(share, 4)
+            roof["achieved_trace_kernel"] = round(ach / share, 3)
+            roof["frac_trace_kernel"] = round(ach / share / gather["Grec_per_s"], 4)
+        out["roofline"] = roof
     if prof is not None and prof[1].get("sq_per_launch", {}).get("SQ_INSTS_VALU"):
         # the same frame against the VALU issue peak (committed PMC profile):
         # the traversal of an L2/MALL-resident tree is bound by issue and
@@ -753,8 +814,10 @@ def main():
                          "(-1 auto: the root gives up the share its frame assembly costs; 0: equal shares)")
     ap.add_argument("--packed", action="store_true", help="N=1: run the gather path (render_packed + assembly)")
     ap.add_argument("--compare-no-cull", type=int, choices=[0, 1], default=None,
-                    help="N=1: also time the same steps with primary-ray culling off (reported as "
-                         "primary_cull_off); default on for the box headline at N=1")
+                    help="also time the same frames with primary-ray culling off, before the warmup (reported "
+                         "as primary_cull_off); default on for the box headline")
+    ap.add_argument("--no-cull-min-ms", type=float, default=40.0,
+                    help="the culling-off frames run for at least this long (and at least --steps frames)")
     ap.add_argument("--no-scene-legs", action="store_true",
                     help="skip the scene legs (`configs` in the JSON line): configs 3, 4 and 5 on one GPU at "
                          "N=1, configs 4 and 5 across the N GPUs at N>1")
@@ -1129,6 +1192,43 @@ def main():
         # a handful of HIP calls per frame, and each event record is one of them
         args.timing_every = max(args.timing_every, 4)
         r.set_option(ptamd.PT_OPT_LAUNCH_TIMING, args.timing_every)
+    # Primary-ray culling off, for reference beside the default: the same
+    # frames (each rank's tile share at N > 1, rendered alone, no exchange)
+    # with every pixel generated and traced, in runs of 16 frames until at
+    # least --no-cull-min-ms have passed.  They run here, right before the
+    # warmup, so the timed region starts on a GPU that has been busy: from
+    # idle the GPU's clocks take ~15 ms of load to ramp up (tools/r04_step_probe.py,
+    # profiles/r04a/probe.log: 20-frame runs 0.2512 ms per frame after 300 ms
+    # idle, 0.2374 -> 0.2302 -> 0.2216 in back-to-back runs, 0.2198 over 200).
+    no_cull = None
+    default_cfg = args.scene == "box" and (W, H, SPP, DEPTH, SSS) == (1920, 1080, 8, 4, 3)
+    if args.compare_no_cull is None:
+        args.compare_no_cull = int(default_cfg and emu == 1 and not args.packed and not args.profile_run)
+    if args.compare_no_cull:
+        nc = ctxs if (dist is None and emu == 1 and not args.packed) else [r]
+        for c in nc:
+            c.set_option(ptamd.PT_OPT_PRIMARY_CULL, 0)
+        for c in nc:
+            c.render(0, SPP)
+        torch.cuda.synchronize(dev)
+        nc_frames = 0
+        t1 = time.perf_counter()
+        while True:
+            for _ in range(16):
+                nc[nc_frames % len(nc)].render(0, SPP)
+                nc_frames += 1
+            torch.cuda.synchronize(dev)
+            dt_nc = time.perf_counter() - t1
+            if nc_frames >= args.steps and dt_nc * 1e3 >= args.no_cull_min_ms:
+                break
+        for c in nc:
+            c.set_option(ptamd.PT_OPT_PRIMARY_CULL, 1)
+            c.render(0, SPP)   # the item layout the exchange follows is the last render's (culled)
+        no_cull = {"ms_per_step": round(dt_nc / nc_frames * 1e3, 4), "frames": nc_frames,
+                   "basis": "runs of 16 frames, synchronized after each run" +
+                            (f"; rank {rank}'s tile share alone, no exchange" if world > 1 else "")}
+        if world == 1:
+            no_cull["value"] = round(rays_per_frame * nc_frames / dt_nc / 1e6, 3)
     run_steps(args.warmup)
     drain()
     if native is not None and native.get("emulated"):
@@ -1177,29 +1277,6 @@ def main():
         for c in ctxs[1:]:
             if not np.array_equal(c.read_accum().view(np.uint32), want):
                 raise SystemExit("bench: the pipelined contexts' frames differ")
-
-    no_cull = None
-    default_cfg = args.scene == "box" and (W, H, SPP, DEPTH, SSS) == (1920, 1080, 8, 4, 3)
-    if args.compare_no_cull is None:
-        args.compare_no_cull = int(world == 1 and emu == 1 and default_cfg and not args.packed and not args.profile_run
-                                   and dist is None)
-    if world == 1 and args.compare_no_cull:
-        # the same frames with primary-ray culling off (every pixel generated
-        # and traced), for reference next to the default
-        for c in ctxs:
-            c.set_option(ptamd.PT_OPT_PRIMARY_CULL, 0)
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize(dev)
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize(dev)
-        dt_nc = time.perf_counter() - t1
-        for c in ctxs:
-            c.set_option(ptamd.PT_OPT_PRIMARY_CULL, 1)
-        no_cull = {"ms_per_step": round(dt_nc / args.steps * 1e3, 4),
-                   "value": round(rays_per_frame * args.steps / dt_nc / 1e6, 3)}
 
     verified = None
     if args.verify and dist is not None and rank == 0:

@@ -1151,19 +1151,14 @@ __global__ __launch_bounds__(256) void exhaustive_kernel(int fn, unsigned long l
 }
 
 // ===========================================================================
-// Lane state-machine kernel, for scenes where traversal dominates.
-//
-// In the path-recursive kernel above every lane of a wave walks its own ray
-// and the wave runs until its longest walk ends: with thousands of node
-// visits per ray and a wide spread between rays (measured lane utilisation
-// 14 % on a 1M-triangle cloud) most lanes idle.  Here each lane is a small
-// state machine over pathTrace (:300-418) — phases PRIMARY, DIRECT, SSS,
-// SSS_SHADOW, BOUNCE — holding at most one ray in flight.  The wave steps
-// every in-flight ray a few nodes at a time; a lane whose ray has finished
-// runs the shading that consumes the result and emits its next ray (or starts
-// its pixel's next sample) so lanes stay busy until the pixel's last sample.
-// The arithmetic, RNG draws and traversal order per ray are exactly those of
-// path_trace(); only the interleaving across lanes differs.
+// pathTrace (:300-418) as a state machine over one sample -- phases PRIMARY,
+// DIRECT, SSS, SSS_SHADOW, BOUNCE -- holding at most one ray in flight: the
+// shading half of the wavefront pipeline and of the tail kernel below.  The
+// arithmetic, RNG draws and traversal order per ray are exactly those of
+// path_trace(); only the interleaving across paths differs.  (A lane
+// state-machine kernel built on it, each lane running its own pixel's
+// samples, measured slower than the path-recursive kernel on every scene and
+// was removed in round 4.)
 // ===========================================================================
 enum : int { PH_BEGIN = 0, PH_PRIMARY, PH_DIRECT, PH_SSS, PH_SSS_SHADOW, PH_BOUNCE };
 
@@ -1290,7 +1285,7 @@ __device__ __forceinline__ void camera_ray(const CamFrame& F, uint32_t seed, v3*
 // the current phase until a ray must be traced (returns true, T set up; the
 // caller traces it and calls again with T.lim/T.res holding the result) or
 // the sample is complete (returns false, *out = its radiance).  Shared by the
-// lane state-machine kernel and the wavefront pipeline.
+// wavefront pipeline's generation, shading and tail kernels.
 template <bool STATS>
 __device__ bool path_step(const RenderParams& P, const CamFrame& F, PathSt& S, Trav& T, Ctr& c, v3* out) {
   const float OFFSET = 0.001f;
@@ -1930,13 +1925,15 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
 // list still held rays -- a lane could refill only once its whole aligned
 // group of four was idle.  G = 1 vs the earlier choice (2 below 500K
 // triangles, 4 above): sphere 78.0 -> 75.1 ms, 10M cloud 237 -> 206 ms;
-// a refill threshold of 16 or 8 lanes instead of 32: +3-15 % (each refill is
-// an atomic and a dependent ray load the whole wave waits for); 24: PT_WIDE_REFILL.
+// the refill threshold is PT_WIDE_REFILL.
 #ifndef PT_WIDE_G
 #define PT_WIDE_G 1
 #endif
-// refill threshold of the wide walk: 24 idle lanes (sphere -0.9 %, 10M cloud
-// -0.35 % against 32, repeated; 16: +3 %)
+// refill threshold of the wide walk: 16 idle lanes.  Before the finished
+// walks were batched at the refill check (PT_WIDE_DEFER_DONE), 24 measured
+// best (sphere -0.9 %, 10M cloud -0.35 % against 32; 16 then +3 %); with
+// them batched, 16 against 24: sphere -2 %, 10M cloud -1.5 % (DESIGN item
+// 36); 12: +0.2 % / +4 %, 8: +7 % / +31 %.
 #ifndef PT_WIDE_REFILL
 #define PT_WIDE_REFILL 16
 #endif

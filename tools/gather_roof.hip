@@ -1,9 +1,16 @@
-// tools/gather_roof.hip — ceiling of random small-record gathers on MI355X
-// (the access pattern of BVH traversal over a scene far larger than the
-// caches).  Every lane issues U independent random loads of a 32-B record
-// (2 x float4, the node layout) per iteration from a table of T bytes, for
-// ITER iterations; reports useful GB/s (32 B per record) and the 64-B
-// granule rate.  Not part of the product.
+// tools/gather_roof.hip — ceilings of random small-record gathers on MI355X
+// (the access pattern of BVH traversal).  Not part of the product.
+//
+// gather: every lane issues U independent random loads of an F4 x 16-B
+// record per iteration from a table of T bytes (throughput ceiling: many
+// loads in flight per lane).
+// chase: every lane follows a chain of dependent loads -- the next record's
+// index is read from the record just loaded -- one load in flight per lane,
+// as the wide walk's node fetches are (a node's children are known only
+// once it has arrived).  Run at the trace kernel's occupancy (6 workgroups
+// of 256 per CU) this is the ceiling for one node fetch per lane per step:
+// the "l2_gather" roofline of cache-resident trees.
+// Reports records/s and useful GB/s (record bytes).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -38,6 +45,34 @@ __global__ __launch_bounds__(256) void gather(const float4* __restrict__ t, uint
   if (s == 1234.5f) out[0] = s;
 }
 
+// record r's first word: a random record index (the chain's next link)
+template <int F4>
+__global__ void init_links(float4* t, uint64_t nrec) {
+  const uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (r >= nrec) return;
+  const uint32_t nxt = (uint32_t)(mix(r * 0x9e3779b97f4a7c15ull + 7) & (nrec - 1));
+  for (int k = 0; k < F4; ++k) t[r * F4 + k] = make_float4(k == 0 ? __uint_as_float(nxt) : 0.0f, 0.0f, 0.0f, 1.0f);
+}
+
+template <int F4>
+__global__ __launch_bounds__(256) void chase(const float4* __restrict__ t, uint64_t nrec, int iters, float* out) {
+  const uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint32_t mask = (uint32_t)(nrec - 1), seed = (uint32_t)mix(g + 1);
+  uint32_t r = seed & mask;
+  float s = 0.0f;
+  for (int it = 0; it < iters; ++it) {
+    float4 v[F4];
+#pragma unroll
+    for (int k = 0; k < F4; ++k) v[k] = t[(uint64_t)r * F4 + k];
+#pragma unroll
+    for (int k = 1; k < F4; ++k) s += v[k].w;
+    // the loaded link, re-scrambled per step so no chain settles into a
+    // short cycle (a random mapping's cycles would end up in L1)
+    r = (__float_as_uint(v[0].x) ^ (seed + (uint32_t)it * 0x9e3779b9u)) & mask;
+  }
+  if (s == 1234.5f || r == 0xffffffffu) out[0] = s;
+}
+
 template <int U, int F4>
 void run(const float4* t, uint64_t table_bytes, int blocks, int iters, float* out, const char* tag) {
   const uint64_t nrec = table_bytes / (16 * F4);
@@ -52,13 +87,37 @@ void run(const float4* t, uint64_t table_bytes, int blocks, int iters, float* ou
   float ms = 0;
   CK(hipEventElapsedTime(&ms, e0, e1));
   const double recs = (double)blocks * 256 * iters * U;
-  printf("{\"case\": \"%s\", \"table_MB\": %.0f, \"record_B\": %d, \"unroll\": %d, \"blocks\": %d, \"ms\": %.3f, "
-         "\"Grec_per_s\": %.2f, \"useful_GBps\": %.1f}\n",
+  printf("{\"case\": \"%s\", \"pattern\": \"independent\", \"table_MB\": %.1f, \"record_B\": %d, \"unroll\": %d, "
+         "\"blocks\": %d, \"ms\": %.3f, \"Grec_per_s\": %.2f, \"useful_GBps\": %.1f}\n",
          tag, table_bytes / 1e6, 16 * F4, U, blocks, ms, recs / ms / 1e6, recs * 16 * F4 / ms / 1e6);
   fflush(stdout);
 }
 
-int main() {
+template <int F4>
+void run_chase(float4* t, uint64_t table_bytes, int blocks, int iters, float* out, const char* tag) {
+  const uint64_t nrec = table_bytes / (16 * F4);
+  init_links<F4><<<(unsigned)((nrec + 255) / 256), 256>>>(t, nrec);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  chase<F4><<<blocks, 256>>>(t, nrec, 8, out);   // warm
+  CK(hipEventRecord(e0));
+  chase<F4><<<blocks, 256>>>(t, nrec, iters, out);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double recs = (double)blocks * 256 * iters;
+  printf("{\"case\": \"%s\", \"pattern\": \"dependent_chain\", \"table_MB\": %.1f, \"record_B\": %d, \"blocks\": %d, "
+         "\"iters\": %d, \"ms\": %.3f, \"Grec_per_s\": %.2f, \"useful_GBps\": %.1f, "
+         "\"latency_ns_per_load\": %.1f}\n",
+         tag, table_bytes / 1e6, 16 * F4, blocks, iters, ms, recs / ms / 1e6, recs * 16 * F4 / ms / 1e6,
+         ms * 1e6 / iters);
+  fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+  const bool quick = argc > 1;   // only the chase cases (the l2_gather roofline)
   const uint64_t big = 4ull << 30;
   float4* t = nullptr;
   float* out = nullptr;
@@ -67,14 +126,25 @@ int main() {
   CK(hipMemset(t, 0, big));
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  for (int occ : {4, 8}) {
-    const int blocks = cus * occ;
-    run<1, 2>(t, big, blocks, 64, out, "hbm");
-    run<4, 2>(t, big, blocks, 32, out, "hbm");
-    run<8, 2>(t, big, blocks, 16, out, "hbm");
-    run<8, 4>(t, big, blocks, 16, out, "hbm64B");
-    run<8, 2>(t, 64ull << 20, blocks, 16, out, "mall64MB");
-    run<8, 2>(t, 2ull << 20, blocks, 16, out, "l2_2MB");
+  if (!quick) {
+    for (int occ : {4, 8}) {
+      const int blocks = cus * occ;
+      run<1, 2>(t, big, blocks, 64, out, "hbm");
+      run<8, 2>(t, big, blocks, 16, out, "hbm");
+      run<8, 4>(t, big, blocks, 16, out, "hbm64B");
+      run<8, 2>(t, 64ull << 20, blocks, 64, out, "mall64MB");
+      run<8, 4>(t, 64ull << 20, blocks, 64, out, "mall64MB");
+      run<8, 2>(t, 2ull << 20, blocks, 256, out, "l2_2MB");
+      run<8, 4>(t, 2ull << 20, blocks, 256, out, "l2_2MB");
+      run<8, 4>(t, 4ull << 20, blocks, 256, out, "l2_4MB");
+    }
   }
+  // dependent chains at the trace kernel's occupancy (6 workgroups of 256 per CU)
+  const int blocks = cus * 6;
+  run_chase<4>(t, 2ull << 20, blocks, 2048, out, "l2_2MB");
+  run_chase<4>(t, 4ull << 20, blocks, 2048, out, "l2_4MB");
+  run_chase<4>(t, 64ull << 20, blocks, 512, out, "mall64MB");
+  run_chase<4>(t, 1ull << 30, blocks, 256, out, "hbm1GB");
+  run_chase<2>(t, 2ull << 20, blocks, 2048, out, "l2_2MB");
   return 0;
 }
