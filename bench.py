@@ -112,7 +112,7 @@ def kernel_sha1():
 def profiled_traffic(workload=None):
     """HBM bytes per launch (per frame for the wavefront pipeline) of the
     current kernel source from the newest committed rocprofv3 PMC summary
-    (tools/gpu_profile.sh / tools/gpu_scene_profile.sh ->
+    (tools/profile_workload.sh ->
     tools/summarize_profile.py) whose pt_device.hip SHA-1 and workload match.
     None if there is none.  Returns the summary dict and its path."""
     import glob
@@ -280,7 +280,8 @@ SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 12, "sphere_1080p8", 3),
 # sphere (configs 3, 4) is L2-resident; the 10M cloud's 313-MB 64-B tree is
 # not (its leg keeps the HBM roofline primary; the chase ceiling is beside
 # it).
-GATHER_CASES = {"sphere_1080p8": ("l2_gather", "l2_4MB"), "sphere_4k16_d8": ("l2_gather", "l2_4MB")}
+GATHER_CASES = {"sphere_1080p8": ("l2_gather", "l2_4MB"), "sphere_4k16_d8": ("l2_gather", "l2_4MB"),
+                "synthetic10M_1080p8": ("hbm_gather", "hbm1GB")}
 
 
 def gather_roofline(workload):
@@ -476,6 +477,20 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
            "contexts": contexts,
            "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
     gather = gather_roofline(workload)
+    if gather is not None and gather["bound"] == "hbm_gather":
+        # beside the HBM roofline: the node fetches against the dependent
+        # 64-B gather ceiling of a 1-GB table (HBM-resident, one load in
+        # flight per lane at the trace kernel's occupancy)
+        visits = float(traced["nodes"])
+        ach = visits / (kernel_ms * 1e-3) / 1e9
+        out["roofline_gather"] = {"bound": "hbm_gather", "achieved": round(ach, 3), "peak": gather["Grec_per_s"],
+                                  "unit": "G wide-node fetches/s", "frac": round(ach / gather["Grec_per_s"], 4),
+                                  "node_visits_per_frame": int(visits), "peak_basis": gather["basis"]}
+        share = trace_share(prof)
+        if share is not None:
+            out["roofline_gather"]["trace_kernel_share"] = round(share, 4)
+            out["roofline_gather"]["frac_trace_kernel"] = round(ach / share / gather["Grec_per_s"], 4)
+        gather = None
     if gather is not None:
         # the wide walk's node fetches against the measured ceiling of
         # dependent 64-B gathers from a table of the tree's size (one fetch
@@ -783,6 +798,10 @@ class _StreamWork:
 
 
 def main():
+    if os.environ.get("PT_BENCH_TRACEBACK_AFTER_S"):
+        # diagnostics of a hung run: every thread's stack to stderr after N s
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["PT_BENCH_TRACEBACK_AFTER_S"]), exit=False)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # a box frame takes ~0.3 ms on one GPU and ~0.05 ms per step on 8: 200
@@ -832,7 +851,7 @@ def main():
         # while frame k's last workgroups drain (-5.4 %, tools/box_streams.py);
         # the long large-scene frames gain nothing from it and keep one.
         # N > 1: three frames in flight on the native loop's three render
-        # streams (emulated root step, tools/r03_native3.sh: N=8 0.0417 ->
+        # streams (emulated root step, DESIGN Appendix A.2: N=8 0.0417 ->
         # 0.0369 ms, N=4 0.0685 -> 0.0648, N=2 0.119 -> 0.1145 against two)
         multi = (int(os.environ.get("WORLD_SIZE", "1")) > 1
                  or int(os.environ.get("PT_BENCH_EMULATE_RANKS", "1")) > 1)

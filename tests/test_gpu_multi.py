@@ -125,3 +125,46 @@ def test_two_rank_scene_legs_reduce_bitwise():
         assert leg["n_gpus"] == 2
         assert leg["verified_bitwise_vs_single_gpu"] is True, key
         assert leg["config"]["rays_per_frame"] > 0 and leg["config"]["rays_traced"] > 0
+
+
+@pytest.mark.parametrize("streams", [2, 3])
+def test_native_loop_back_to_back_calls(streams):
+    """Two pt_dist_run calls with no synchronize in between: the
+    second call's first frames reuse the send slots, receive sets and frame
+    buffers the first call's last gathers and trailing assemblies may still
+    be using; pt_dist_run's entry barrier orders them.  A one-rank real RCCL
+    communicator in this process; every frame buffer must hold the
+    single-GPU frame afterwards.  (The two-process schedule runs through the
+    host-synchronous stand-in, which cannot show overlap hazards: they are
+    covered by this ordering and by the driver's multi-GPU runs.)"""
+    import numpy as np
+    import torch
+    import ptamd
+    import scenes
+    scene = ptamd.Scene.load_obj(scenes.BOX_OBJ).build_bvh()
+    v, i, n, _, _ = scene.arrays()
+
+    def setup():
+        r = ptamd.Renderer(0)
+        r.upload_scene(v, i, n)
+        r.upload_lights(scenes.REFERENCE_LIGHT)
+        r.set_camera(scenes.DEFAULT_CAMERA)
+        r.set_params(4, 3)
+        r.resize_and_clear(320, 200)
+        return r
+    one = setup()
+    one.render(0, 4)
+    want = one.read_accum().view(np.uint32)
+    r = setup()
+    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+    r.render(0, 4)   # fixes the item layout
+    r.dist_init(ptamd.Renderer.dist_unique_id(), 1, 0)
+    frames = torch.full((3, 200, 320, 4), float("nan"), dtype=torch.float32, device="cuda:0")
+    r.dist_run(4, 5, frames.data_ptr(), 3, n_streams=streams)
+    r.dist_run(4, 4, frames.data_ptr(), 3, n_streams=streams)
+    r.dist_wait(30000)
+    r.synchronize()
+    for f in range(3):
+        got = frames[f].cpu().numpy().reshape(-1).view(np.uint32)
+        assert np.array_equal(got, want), f"frame buffer {f}"
+    r.dist_finalize()
