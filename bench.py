@@ -1222,7 +1222,7 @@ def main():
     no_cull = None
     default_cfg = args.scene == "box" and (W, H, SPP, DEPTH, SSS) == (1920, 1080, 8, 4, 3)
     if args.compare_no_cull is None:
-        args.compare_no_cull = int(default_cfg and emu == 1 and not args.packed and not args.profile_run)
+        args.compare_no_cull = int(default_cfg and not args.packed and not args.profile_run)
     if args.compare_no_cull:
         nc = ctxs if (dist is None and emu == 1 and not args.packed) else [r]
         for c in nc:
@@ -1245,8 +1245,8 @@ def main():
             c.render(0, SPP)   # the item layout the exchange follows is the last render's (culled)
         no_cull = {"ms_per_step": round(dt_nc / nc_frames * 1e3, 4), "frames": nc_frames,
                    "basis": "runs of 16 frames, synchronized after each run" +
-                            (f"; rank {rank}'s tile share alone, no exchange" if world > 1 else "")}
-        if world == 1:
+                            (f"; rank {emu_rank}'s tile share alone, no exchange" if nparts > 1 else "")}
+        if nparts == 1:
             no_cull["value"] = round(rays_per_frame * nc_frames / dt_nc / 1e6, 3)
     run_steps(args.warmup)
     drain()

@@ -4,14 +4,17 @@
 // `spp` progressive 1-spp batches (or one fused launch) and writes a PFM.
 //
 //   pt_render scene.obj [-w 1920] [-h 1080] [-spp 8] [-depth 4] [-sss 3]
-//             [-fused] [-o out.pfm] [-png out.png] [-device 0] [-cache scene.ptscene]
-//             [-progressive N [-chunk K] [-orbit-at B]]
+//             [-fused] [-o out.pfm] [-png out.png] [-device 0 | -devices 0,1,..]
+//             [-cache scene.ptscene] [-progressive N [-chunk K] [-orbit-at B]]
 //
 // -progressive runs the reference's interactive loop (mainLoop, :717-865)
 // headless: up to N batches (cap 1024, :719) in launches of K, a readback of
 // every launch overlapped with the next one (double-buffered), and, with
 // -orbit-at, a camera change after B batches that restarts at batch 0.
 // -cache loads/saves the built scene (pt_scene_save) next to the OBJ.
+// -devices renders on several GPUs from this one thread (pt_create_multi:
+// each renders its screen tiles straight into the frame on the first one);
+// every other call is unchanged.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -42,6 +45,7 @@ int main(int argc, char** argv) {
   bool fused = false;
   int progressive = 0, chunk = 8, orbit_at = -1;
   std::string cache_path, png_path;
+  std::vector<int> devices;   // -devices: a multi-device context
   for (int i = 2; i < argc; ++i) {
     auto next = [&](void) { return (i + 1 < argc) ? argv[++i] : (char*)"0"; };
     if (!strcmp(argv[i], "-w")) W = atoi(next());
@@ -50,6 +54,13 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "-depth")) params.max_depth = atoi(next());
     else if (!strcmp(argv[i], "-sss")) params.sss_bounces = atoi(next());
     else if (!strcmp(argv[i], "-device")) device = atoi(next());
+    else if (!strcmp(argv[i], "-devices")) {
+      for (const char* p = next(); *p;) {
+        devices.push_back(atoi(p));
+        while (*p && *p != ',') ++p;
+        if (*p == ',') ++p;
+      }
+    }
     else if (!strcmp(argv[i], "-fused")) fused = true;
     else if (!strcmp(argv[i], "-o")) out_path = next();
     else if (!strcmp(argv[i], "-cache")) cache_path = next();
@@ -75,7 +86,14 @@ int main(int argc, char** argv) {
          cached ? "cache load" : "OBJ parse + BVH build", std::chrono::duration<double>(t1 - t0).count());
 
   pt_context* ctx = nullptr;
-  check(pt_create(device, &ctx), "create");
+  if (devices.empty()) {
+    check(pt_create(device, &ctx), "create");
+  } else {
+    check(pt_create_multi(devices.data(), (int)devices.size(), &ctx), "create_multi");
+    int peer = 0;
+    check(pt_group_info(ctx, nullptr, nullptr, 0, &peer), "group_info");
+    printf("devices: %zu (%s)\n", devices.size(), peer ? "peer stores into the first device's frame" : "packed tile copies");
+  }
   check(pt_scene_upload(ctx, scene), "upload scene");
   const float pos[3] = {0.0f, 2.0f, 0.0f}, nrm[3] = {0.0f, -1.0f, 0.0f}, inten[3] = {10.0f, 10.0f, 10.0f},
               size[2] = {2.5f, 2.5f};   // VulkanRayTracer.cpp:149-162

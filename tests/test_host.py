@@ -248,3 +248,31 @@ def test_partition_slots_masks_tile_the_frame():
     for n in (2, 3):   # one slot each is the plain partition
         for r in range(n):
             assert np.array_equal(ptamd.partition_owned(W, H, n, r, [1] * n), ptamd.partition_owned(W, H, n, r))
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
+def test_multi_device_members_cover_the_frame_once(n):
+    """pt_create_multi gives member r the tiles of rank r of an n-way
+    pt_set_partition: over the members every pixel is rendered exactly once
+    (the frame on the first device is then the single-GPU frame), for ragged
+    frame sizes too."""
+    for W, H in ((1920, 1080), (70, 45), (17, 300)):
+        cover = np.zeros((H, W), np.int32)
+        for r in range(n):
+            cover += ptamd.partition_owned(W, H, n, r).astype(np.int32)
+        assert np.all(cover == 1), (n, W, H)
+
+
+def test_create_multi_argument_errors_without_a_gpu():
+    """Bad member lists fail with an error, never a crash (this container has
+    no GPU: a valid list fails at device enumeration)."""
+    import ctypes
+    L = ptamd.lib()
+    out = ctypes.c_void_p()
+    none = np.zeros(0, np.int32)
+    assert L.pt_create_multi(None, 2, ctypes.byref(out)) < 0
+    assert L.pt_create_multi(none.ctypes.data, 0, ctypes.byref(out)) < 0
+    devs = np.array([0, 0], np.int32)
+    rc = L.pt_create_multi(devs.ctypes.data, 2, ctypes.byref(out))
+    assert rc < 0 and not out.value
+    assert L.pt_last_error()

@@ -93,8 +93,12 @@ def _read_pfm(path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("flags", [[], ["-fused"], ["-progressive", "8", "-chunk", "3"]])
+@pytest.mark.parametrize("flags", [[], ["-fused"], ["-progressive", "8", "-chunk", "3"],
+                                   ["-devices", "0,0,0", "-progressive", "8", "-chunk", "3"]])
 def test_pt_render_cpp_driver_matches_oracle(tmp_path, flags):
+    """The C++ driver as the reference's host would run it; with -devices, one
+    thread drives a multi-device context (pt_create_multi; the members share
+    this box's one GPU) through the same calls."""
     exe = os.path.join(PKG, "pt_render")
     if not os.path.exists(exe):
         subprocess.check_call(["make", "-s", "-C", PKG, "pt_render"])
