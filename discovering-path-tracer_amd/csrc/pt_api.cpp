@@ -750,8 +750,34 @@ struct Assembly {   // pt_render_packed's optional gathered frame to assemble
   size_t slot_floats = 0;
   void* frame = nullptr;
 };
+// The parameters of a path-recursive launch as render_impl made it, so that
+// pt_dist_run can launch the next frames of a run (same scene, camera,
+// options and item layout; only the packed output and the frame to assemble
+// change) without rebuilding them: the host cost of a frame is then the
+// launch and its events (relaunch).
+struct Launched {
+  ptd::RenderParams p;
+  bool lds = false, cnt = false, valid = false;
+};
+// One path-recursive launch of prepared parameters, timed as render_impl
+// times its launches (PT_OPT_LAUNCH_TIMING).
+int relaunch(pt_context* c, const ptd::RenderParams& p, bool lds, bool cnt) {
+  const int slot = c->ring_n % pt_context::kRing;
+  const bool timed = c->opt_timing > 0 && c->launch_n % c->opt_timing == 0;
+  if (timed) PT_HIP(hipEventRecord(c->ring[slot][0], c->stream));
+  PT_HIP(ptd::launch_render(p, false, lds, c->stream, cnt));
+  if (timed) {
+    PT_HIP(hipEventRecord(c->ring[slot][1], c->stream));
+    c->ring_launch[slot] = c->launch_n;
+    c->last_slot = slot;
+    c->ring_n++;
+    c->timed = true;
+  }
+  c->launch_n++;
+  return PT_OK;
+}
 int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4* pack_out,
-                const Assembly& as = Assembly()) {
+                const Assembly& as = Assembly(), Launched* launched = nullptr) {
   if (!c) return fail(PT_ERR_INVALID, "null context");
   if (!c->has_scene) return fail(PT_ERR_INVALID, "no scene uploaded");
   if (!c->has_camera) return fail(PT_ERR_INVALID, "no camera set");
@@ -980,6 +1006,12 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     PT_HIP(ptd::launch_wavefront(p, b, lds, c->stream, cnt, two ? c->wf_stream2 : nullptr, c->wf_fork, c->wf_join));
   } else {
     PT_HIP(ptd::launch_render(p, c->stats_mode, lds, c->stream, cnt));
+    if (launched && pack_out && !c->stats_mode) {
+      launched->p = p;
+      launched->lds = lds;
+      launched->cnt = cnt;
+      launched->valid = true;
+    }
   }
   if (shared) {
     const int rm = mark_shared(c);
@@ -2271,7 +2303,10 @@ int dist_layout(pt_context* c) {
   DistState* d = c->dist;
   std::vector<float> key;
   frame_key(c, c->last, &key);
-  if (key == d->layout_key && d->send[0]) return PT_OK;
+  // (the root has no send slots: its layout is valid once any buffer was
+  // sized for it; testing send[0] made the root rebuild every rank's item
+  // lists on every call, ~0.45 ms of host time per call at N = 8)
+  if (key == d->layout_key && d->cap_floats > 0) return PT_OK;
   size_t live_max = 0;
   std::vector<int> live, culled;
   for (int r = 0; r < c->nranks; ++r) {
@@ -2407,6 +2442,10 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, 
         if (all[e] != d->streams[s]) PT_HIP(hipStreamWaitEvent(d->streams[s], d->entry[e], 0));
   }
   c->in_dist = true;
+  // frames after the first of each kind (with and without an assembly) reuse
+  // its launch parameters: nothing but the output and the assembled frame
+  // change within a call (relaunch)
+  Launched tmpl[2];
   for (int k = 0; k < n_frames && rc == PT_OK; ++k) {
     const int b = k % nsets;
     c->stream = d->streams[k % n_streams];
@@ -2420,7 +2459,17 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, 
         as.frame = (float*)frames + (size_t)((k - D) % n_frame_bufs) * frame_f;
       }
     }
-    rc = render_impl(c, 0, n_batches, (float4*)(d->rank == 0 ? d->recv[b] : d->send[k % D]), as);
+    float4* out = (float4*)(d->rank == 0 ? d->recv[b] : d->send[k % D]);
+    Launched& t = tmpl[as.src ? 1 : 0];
+    if (t.valid) {
+      ptd::RenderParams p = t.p;
+      p.pack_out = out;
+      p.unpack_src = (const float4*)as.src;
+      p.unpack_frame = (float4*)as.frame;
+      rc = relaunch(c, p, t.lds, t.cnt);
+    } else {
+      rc = render_impl(c, 0, n_batches, out, as, &t);
+    }
     if (rc) break;
     PT_HIP(hipEventRecord(d->render_done[b], c->stream));
     PT_HIP(hipStreamWaitEvent(d->comm_stream, d->render_done[b], 0));

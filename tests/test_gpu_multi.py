@@ -20,6 +20,19 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _run(cmd, env, timeout=180):
+    """subprocess.run with the children's stacks on a hang: bench.py dumps
+    every thread's stack to stderr after PT_BENCH_TRACEBACK_AFTER_S, and a
+    timeout reports the tail of what the children wrote."""
+    env = dict(env, PT_BENCH_TRACEBACK_AFTER_S=str(timeout - 30))
+    try:
+        return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired as e:
+        def tail(x):
+            return (x.decode(errors="replace") if isinstance(x, bytes) else (x or ""))[-6000:]
+        raise AssertionError(f"timed out after {timeout} s\nstdout:\n{tail(e.stdout)}\nstderr:\n{tail(e.stderr)}")
+
+
 # torchrun --standalone binds its rendezvous store to a port of its own
 # choosing (a port picked here and handed over could be taken in between:
 # EADDRINUSE); the single-rank native test sets MASTER_PORT itself.
@@ -47,7 +60,7 @@ def test_two_rank_bench_verifies_bitwise(collective, extra):
            "--standalone", "--local-addr", "127.0.0.1",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2", "--verify",
            "--no-scene-legs", "--collective", collective] + extra
-    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    res = _run(cmd, env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
     lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
     assert lines, res.stdout[-2000:]
@@ -68,7 +81,7 @@ def test_native_step_loop_single_rank_rccl(streams):
                WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "7", "--warmup", "3", "--verify",
            "--no-scene-legs", "--no-cpu-baseline", "--streams", str(streams)]
-    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    res = _run(cmd, env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
     out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
     assert out["config"]["step_loop"].startswith("native"), res.stderr[-2000:]
@@ -95,7 +108,7 @@ def test_native_step_loop_two_ranks_grouped_send_recv(streams):
            "--standalone", "--local-addr", "127.0.0.1",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "6", "--warmup", "3", "--verify",
            "--no-scene-legs", "--streams", str(streams)]
-    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    res = _run(cmd, env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
     out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
     assert out["n_gpus"] == 2
@@ -115,7 +128,7 @@ def test_two_rank_scene_legs_reduce_bitwise():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--standalone", "--local-addr", "127.0.0.1",
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1"]
-    res = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    res = _run(cmd, env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
     out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
     legs = out["configs"]
