@@ -33,9 +33,13 @@
 #include "pt_group.h"
 
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -78,6 +82,20 @@ struct pt_group {
   float prog_cam[16] = {0};
   bool prog_has_cam = false;
   uint32_t prog_batch = 0;
+  // Enqueue threads: with three or more members, members 1..n-1 enqueue
+  // their launches from threads of their own (one per member, parked on a
+  // condition variable), so a frame's host cost is one member's enqueue
+  // (~10-15 us) rather than n of them; member 0 enqueues on the caller's
+  // thread.
+  std::vector<std::thread> workers;
+  std::mutex mu;
+  std::condition_variable cv_job, cv_done;
+  std::function<int(int)> job;
+  uint64_t gen = 0;
+  int pending = 0;
+  bool stop = false;
+  std::vector<int> job_rc;
+  std::vector<std::string> job_err;
 };
 
 namespace {
@@ -115,6 +133,60 @@ template <class F>
 int each(pt_group* g, F f) {
   for (int r = 0; r < g->n; ++r) G_RC(f(r));
   return PT_OK;
+}
+
+void worker_main(pt_group* g, int r) {
+  (void)hipSetDevice(g->dev[(size_t)r]);
+  uint64_t seen = 0;
+  for (;;) {
+    std::function<int(int)> f;
+    {
+      std::unique_lock<std::mutex> lk(g->mu);
+      g->cv_job.wait(lk, [&] { return g->stop || g->gen != seen; });
+      if (g->stop) return;
+      seen = g->gen;
+      f = g->job;
+    }
+    const int rc = f(r);
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->job_rc[(size_t)r] = rc;
+    if (rc) g->job_err[(size_t)r] = pt_last_error();
+    if (--g->pending == 0) g->cv_done.notify_one();
+  }
+}
+
+// f(r) for every member: members 1..n-1 on their enqueue threads (when the
+// group has them), member 0 on the caller's; the first failure is returned.
+int each_member(pt_group* g, const std::function<int(int)>& f) {
+  if (g->workers.empty()) return each(g, f);
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->job = f;
+    g->pending = g->n - 1;
+    std::fill(g->job_rc.begin(), g->job_rc.end(), PT_OK);
+    ++g->gen;
+  }
+  g->cv_job.notify_all();
+  const int rc0 = f(0);
+  const std::string err0 = rc0 ? pt_last_error() : "";
+  std::unique_lock<std::mutex> lk(g->mu);
+  g->cv_done.wait(lk, [&] { return g->pending == 0; });
+  if (rc0) return pt_fail_internal(rc0, err0);
+  for (int r = 1; r < g->n; ++r)
+    if (g->job_rc[(size_t)r])
+      return pt_fail_internal(g->job_rc[(size_t)r], "member " + std::to_string(r) + ": " + g->job_err[(size_t)r]);
+  return PT_OK;
+}
+
+void stop_workers(pt_group* g) {
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->stop = true;
+  }
+  g->cv_job.notify_all();
+  for (auto& t : g->workers)
+    if (t.joinable()) t.join();
+  g->workers.clear();
 }
 
 void free_exchange(pt_group* g) {
@@ -214,12 +286,18 @@ int make(const int* ordinals, int n, pt_group** out) {
   if (hipSetDevice(g->dev[0]) != hipSuccess ||
       hipEventCreateWithFlags(&g->start, hipEventDisableTiming) != hipSuccess)
     return bail(pt_fail_internal(PT_ERR_HIP, "pt_create_multi: event setup failed"));
+  g->job_rc.assign((size_t)n, PT_OK);
+  g->job_err.assign((size_t)n, std::string());
+  const char* th = getenv("PT_GROUP_THREADS");   // 0: enqueue every member on the caller's thread
+  if (n >= 3 && !(th && th[0] == '0'))
+    for (int r = 1; r < n; ++r) g->workers.emplace_back(worker_main, g, r);
   *out = g;
   return PT_OK;
 }
 
 int destroy(pt_group* g) {
   if (!g) return PT_OK;
+  stop_workers(g);
   for (int r = 0; r < g->n; ++r)
     if (g->s[(size_t)r]) {
       (void)hipSetDevice(g->dev[(size_t)r]);
@@ -321,7 +399,8 @@ int render(pt_group* g, uint32_t first_batch, uint32_t n_batches) {
   // the members start after the group stream's earlier work (clear, readback)
   G_HIP(hipSetDevice(g->dev[0]));
   G_HIP(hipEventRecord(g->start, g->s[0]));
-  for (int r = 1; r < g->n; ++r) {
+  G_RC(each_member(g, [&](int r) -> int {
+    if (r == 0) return pt_render(g->m[0], first_batch, n_batches);
     G_HIP(hipSetDevice(g->dev[(size_t)r]));
     G_HIP(hipStreamWaitEvent(g->s[(size_t)r], g->start, 0));
     G_RC(pt_render(g->m[(size_t)r], first_batch, n_batches));
@@ -333,8 +412,8 @@ int render(pt_group* g, uint32_t first_batch, uint32_t n_batches) {
     }
     G_HIP(hipSetDevice(g->dev[(size_t)r]));
     G_HIP(hipEventRecord(g->done[(size_t)r], g->s[(size_t)r]));
-  }
-  G_RC(pt_render(g->m[0], first_batch, n_batches));
+    return PT_OK;
+  }));
   G_HIP(hipSetDevice(g->dev[0]));
   for (int r = 1; r < g->n; ++r) {
     G_HIP(hipStreamWaitEvent(g->s[0], g->done[(size_t)r], 0));

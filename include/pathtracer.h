@@ -110,6 +110,9 @@ int pt_create(int device_ordinal, pt_context** out);
  * over xGMI (peer access), or -- when a member cannot map it, or with
  * PT_OPT_GROUP_EXCHANGE 1 -- ship them as packed tiles copied to the first
  * device.  An ordinal may repeat (several members on one device: tests).
+ * With three or more members, members 1..n-1 enqueue their launches from
+ * threads of their own (environment PT_GROUP_THREADS=0: all on the calling
+ * thread), so a render costs the caller about one member's host time.
  * Calls on a member's share (pt_set_partition*, pt_tiles_*, pt_items_*,
  * pt_render_packed, pt_dist_*) return PT_ERR_UNSUPPORTED on such a context;
  * the launch-timing calls report the first device's launches.  pt_destroy
