@@ -1256,7 +1256,7 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   }
   PT_HIP(hipStreamSynchronize(c->stream));
   c->n_wide = wide_reason.empty() ? wide.n_nodes : 0;
-  c->wide_stack = ptd::wide_stack_entries(wide.stack_cap);
+  c->wide_stack = wide.stack_cap;
   c->wide_reason = wide_reason;
   c->n_nodes = (int)(collapsed.size() / 2) - 1;
   c->n_nodes_full = (int)(threaded.size() / 2) - 1;

@@ -205,7 +205,6 @@ hipError_t launch_wavefront(const RenderParams& p, const WfBuffers& b, bool lds_
                             hipEvent_t ev_join = nullptr);
 // lanes of the wide walk's persistent grid on this device (overflow areas to allocate)
 long long wide_trace_lanes();
-int wide_stack_entries(int cap);
 // triangle records by rank: dst[r] = tris[tri_of[r]]
 hipError_t launch_gather_tris(const float4* tris, const int* tri_of, int n, float4* dst, hipStream_t stream);
 hipError_t launch_math(int fn, const float* x, float* y, size_t n, hipStream_t stream);

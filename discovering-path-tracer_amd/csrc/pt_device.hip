@@ -1949,16 +1949,11 @@ constexpr int kWideG = PT_WIDE_G;
 #ifndef PT_WIDE_FLUSH_T
 #define PT_WIDE_FLUSH_T 1
 #endif
-// PT_WIDE_DUAL: two nodes per walk step (wide_step2): the node to expand and
-// the stack's top entry, both fetched before either is tested.
-#ifndef PT_WIDE_DUAL
-#define PT_WIDE_DUAL 0
-#endif
 #ifndef PT_WIDE_MIN_BLOCKS
 // 6: the LDS stack and leaf queue (96 B per lane) fit 6 workgroups per CU;
 // 79 VGPRs, no spills.  8 workgroups with a 6-entry stack ring (80 B per lane,
 // 64 VGPRs, 60 B spilled): sphere +6.5 %, 10M cloud +5.4 %; with 7: +1 %.
-#define PT_WIDE_MIN_BLOCKS (PT_WIDE_DUAL ? 5 : 6)
+#define PT_WIDE_MIN_BLOCKS 6
 #endif
 // PT_OPT_WF_FUSE: the shadow ray pathTrace traces right after closest hit
 // (t, rank) of ray (o, d), from the path's RNG state `rng` -- light 0's
@@ -2205,13 +2200,9 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
         }
       } else {
         // fin: the walk has no node left (its queue may still hold candidates)
-        if (p >= 0 && !fin) {
-          if constexpr (PT_WIDE_DUAL && QN)
-            fin = wide_step2<CNT>(R, P.wide, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes, cand);
-          else
-            fin = wide_step<CNT, true, QN>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
-                                           &c.leaves, cand, P.wide_leafbox);
-        }
+        if (p >= 0 && !fin)
+          fin = wide_step<CNT, true, QN>(R, P.wide, P.wide_tris, lds, 64, ovf, os, P.wide_stack, &exact, &c.nodes,
+                                         &c.leaves, cand, P.wide_leafbox);
         if (exact) {
           R.nc = 0;
           // a fused shadow ray the walk cannot take goes to the shading's next round
@@ -2693,13 +2684,6 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, hipS
   if (grid > 0) hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(256), lds, stream, p);
   return hipGetLastError();
 }
-
-// Overflow-stack entries per lane the trace kernel needs for a tree whose
-// one-node walk holds at most `cap` (wide_bvh.cpp's bound): the two-node step
-// expands the stack's top early, so its stack can grow past the bound
-// (wide_step2 checks against what the area holds and hands the ray to the
-// exact walk beyond it).
-int wide_stack_entries(int cap) { return PT_WIDE_DUAL ? 2 * cap + 4 : cap; }
 
 long long wide_trace_lanes() {
   int dev = 0, cus = 0, per_cu = 0;

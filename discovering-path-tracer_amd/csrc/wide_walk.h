@@ -397,132 +397,4 @@ PT_FN bool wide_step(WideRay& R, const float4* __restrict__ nodes, const float4*
   return false;
 }
 
-// One 64-B node's children (QN layout): refs, slab hits after the cull, and
-// t_near / cull thresholds, as wide_step computes them.
-struct WideKids {
-  int c[4];
-  bool h[4];
-  float n[4], th[4];
-};
-PT_FN void wide_kids(const WideRay& R, float4 q0, float4 q1, float4 q2, float4 cf, WideKids* K) {
-  const uint32_t meta = f2u(q0.w);
-  const float sx = wq_scale(meta, 0), sy = wq_scale(meta, 1), sz = wq_scale(meta, 2);
-  const uint32_t a0 = f2u(q1.x), a1 = f2u(q1.y), a2 = f2u(q1.z), a3 = f2u(q1.w), a4 = f2u(q2.x), a5 = f2u(q2.y);
-  const uint32_t e01 = f2u(q2.w);
-  const float4 kf = make_float4(q2.z, u2f(e01 << 16), u2f(e01 & 0xffff0000u), 0.0f);
-  const v3 ainv = wide_ainv(R);
-  K->c[0] = (int)f2u(cf.x);
-  K->c[1] = (int)f2u(cf.y);
-  K->c[2] = (int)f2u(cf.z);
-  K->c[3] = (int)f2u(cf.w);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    bool h;
-    wide_child(R, ainv, wq_dec(a0, j, sx, q0.x), wq_dec(a1, j, sx, q0.x), wq_dec(a2, j, sy, q0.y),
-               wq_dec(a3, j, sy, q0.y), wq_dec(a4, j, sz, q0.z), wq_dec(a5, j, sz, q0.z), kf, &h, &K->n[j], &K->th[j]);
-    K->h[j] = h && K->c[j] != kWideEmpty && !(R.lim < K->th[j]);
-  }
-}
-PT_FN int pick4(const int* a, int i) { return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3]; }
-PT_FN float pick4(const float* a, int i) { return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3]; }
-// Queues the node's hit leaves (PT_WIDE_QUEUE) and returns its live inner
-// children as a mask, their keys (t_near, +inf when not live) sorted with
-// their slots s[] nearest first.
-PT_FN uint32_t wide_sort_kids(WideRay& R, const WideKids& K, int* cand, int* s) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    cand[R.nc * 64] = ~K.c[j];
-    R.nc += (K.h[j] && K.c[j] < 0) ? 1 : 0;
-  }
-  const uint32_t live = (K.h[0] && K.c[0] >= 0 ? 1u : 0u) | (K.h[1] && K.c[1] >= 0 ? 2u : 0u) |
-                        (K.h[2] && K.c[2] >= 0 ? 4u : 0u) | (K.h[3] && K.c[3] >= 0 ? 8u : 0u);
-  float k0 = (live & 1u) ? K.n[0] : __builtin_inff();
-  float k1 = (live & 2u) ? K.n[1] : __builtin_inff();
-  float k2 = (live & 4u) ? K.n[2] : __builtin_inff();
-  float k3 = (live & 8u) ? K.n[3] : __builtin_inff();
-  int s0 = 0, s1 = 1, s2 = 2, s3 = 3;
-#define PT_CE(ka, sa, kb, sb)              \
-  if (kb < ka) {                           \
-    const float tk = ka; ka = kb; kb = tk; \
-    const int ts = sa; sa = sb; sb = ts;   \
-  }
-  PT_CE(k0, s0, k1, s1)
-  PT_CE(k2, s2, k3, s3)
-  PT_CE(k0, s0, k2, s2)
-  PT_CE(k1, s1, k3, s3)
-  PT_CE(k1, s1, k2, s2)
-#undef PT_CE
-  s[0] = s0;
-  s[1] = s1;
-  s[2] = s2;
-  s[3] = s3;
-  return live;
-}
-
-// PT_WIDE_DUAL: two nodes per step.  With the node to expand (A) the walk
-// also pops the stack's top entry (B) -- dropped if the cull already rules
-// it out, which it would also do at B's own pop, the limit only falling --
-// and loads both nodes before either is tested, so a lane has two node
-// fetches in flight instead of one.  B's live inner children go onto the
-// stack first, all of them (farthest first), then A's except its nearest,
-// which is expanded next: A's subtree is still walked before B's, as in
-// wide_step; only B's own test comes early (with a looser limit, so it may
-// keep children the serial walk would not have reached; their thresholds
-// are checked again at their pops).  Leaves of both go to the queue, which
-// needs room for eight (R.nc <= kWideQ - 8, else no B this step).  The
-// answer does not depend on the order nodes are visited in (wide_walk.h's
-// header), so it is wide_step's.
-template <bool CNT>
-PT_FN bool wide_step2(WideRay& R, const float4* __restrict__ nodes, int2* lds, int ls, int2* ovf, long long os,
-                      int stack_cap, bool* exact, uint32_t* cn, int* cand) {
-  while (R.cur < 0) {
-    if (R.sp == 0) return true;
-    const int2 e = wide_pop(R, lds, ls, ovf, os);
-    if (!(R.lim < u2f((uint32_t)e.y))) R.cur = e.x;
-  }
-  int b = -1;
-  if (R.sp > 0 && R.nc <= kWideQ - 8) {
-    const int2 e = wide_pop(R, lds, ls, ovf, os);
-    if (!(R.lim < u2f((uint32_t)e.y))) b = e.x;
-  }
-  const float4* na = nodes + (size_t)R.cur * kWideQNodeF4;
-  const float4* nb = nodes + (size_t)(b >= 0 ? b : R.cur) * kWideQNodeF4;
-  const float4 a0 = na[0], a1 = na[1], a2 = na[2], a3 = na[3];
-  const float4 b0 = nb[0], b1 = nb[1], b2 = nb[2], b3 = nb[3];
-  int s[4];
-  if (b >= 0) {
-    if (CNT) ++*cn;
-    WideKids K;
-    wide_kids(R, b0, b1, b2, b3, &K);
-    const uint32_t live = wide_sort_kids(R, K, cand, s);
-    if (R.sp + __builtin_popcount(live) > stack_cap) {   // memory-safe: hand the ray to the exact walk
-      *exact = true;
-      return true;
-    }
-#pragma unroll
-    for (int i = 3; i >= 0; --i)
-      if ((live >> s[i]) & 1u) wide_push(R, make_int2(pick4(K.c, s[i]), (int)f2u(pick4(K.th, s[i]))), lds, ls, ovf, os);
-  }
-  if (CNT) ++*cn;
-  WideKids K;
-  wide_kids(R, a0, a1, a2, a3, &K);
-  const uint32_t live = wide_sort_kids(R, K, cand, s);
-  R.cur = -1;
-  const int n_live = __builtin_popcount(live);
-  if (n_live == 0) return false;
-  if (R.sp + n_live - 1 > stack_cap) {
-    *exact = true;
-    return true;
-  }
-  int first = -1;
-#pragma unroll
-  for (int i = 3; i >= 0; --i) {
-    if (!((live >> s[i]) & 1u)) continue;
-    if (first >= 0) wide_push(R, make_int2(pick4(K.c, first), (int)f2u(pick4(K.th, first))), lds, ls, ovf, os);
-    first = s[i];
-  }
-  R.cur = pick4(K.c, first);
-  return false;
-}
-
 }  // namespace ptd

@@ -21,10 +21,7 @@ namespace {
 int g_mode = pt::WIDE_SAH;   // wide_set_mode
 int g_node = 128;            // wide_set_variant: node bytes (64: the quantized layout with exact leaf tests)
 int g_queue = 0;             // ... and 1: the queued leaf tests with per-lane flushes; 2: with the wave-wide flush's
-                             // merge (flush_lexmin, the trace kernel's default); 3: as 2 with two nodes per step
-                             // (wide_step2, PT_WIDE_DUAL; 64-B nodes)
-unsigned long long g_steps = 0;   // walk steps (wide_step / wide_step2 calls) since wide_set_variant
-unsigned long long g_deep = 0;    // ... of them ending with stack entries in the overflow area
+                             // merge (flush_lexmin, the trace kernel's default)
 
 struct Built {
   pt::WideBVH w;
@@ -108,18 +105,12 @@ void walk(WideRay& R, const Built& b, int2* lds, int2* ovf, bool* exact, uint32_
   std::vector<int> cand(kWideQ * 64, -1);
   bool fin = false;
   for (;;) {
-    if (!fin) {
-      ++g_steps;
-      if (QN && g_queue == 3)
-        fin = wide_step2<true>(R, nodes, lds, 1, ovf, 1, 2 * b.w.stack_cap + 4, exact, cn, cand.data());
-      else
-        fin = wide_step<true, true, QN>(R, nodes, b.tris.data(), lds, 1, ovf, 1, b.w.stack_cap, exact, cn, cl,
-                                        cand.data(), leafbox);
-      g_deep += R.lo > 0 ? 1 : 0;
-    }
+    if (!fin)
+      fin = wide_step<true, true, QN>(R, nodes, b.tris.data(), lds, 1, ovf, 1, b.w.stack_cap, exact, cn, cl,
+                                      cand.data(), leafbox);
     if (*exact) return;
     if (R.nc > kWideQ - 4 || (fin && R.nc > 0)) {
-      if (g_queue >= 2 ? flush_lexmin<QN>(R, b.tris.data(), cand.data(), cl, leafbox)
+      if (g_queue == 2 ? flush_lexmin<QN>(R, b.tris.data(), cand.data(), cl, leafbox)
                        : wide_flush<true, QN>(R, b.tris.data(), cand.data(), cl, leafbox)) {   // occluded
         fin = true;
         R.sp = 0;
@@ -141,11 +132,7 @@ void wide_set_mode(int mode) { g_mode = mode; }
 void wide_set_variant(int node_bytes, int queue) {
   g_node = node_bytes;
   g_queue = queue;
-  g_steps = 0;
-  g_deep = 0;
 }
-unsigned long long wide_steps() { return g_steps; }
-unsigned long long wide_deep_steps() { return g_deep; }
 
 // info[0] wide nodes, info[1] stack bound.  Returns 0, or 1 with the reason in err.
 int wide_info(const float* V, size_t nvf, const uint32_t* I, size_t nt, const float* N, size_t nn, int int_bits,
@@ -194,7 +181,7 @@ int wide_check(const float* V, size_t nvf, const uint32_t* I, size_t nt, const f
     snprintf(err, errlen, "%s", why.c_str());
     return 1;
   }
-  std::vector<int2> lds(kWideLds), ovf((size_t)(2 * b.w.stack_cap + 5));
+  std::vector<int2> lds(kWideLds), ovf((size_t)(size_t)b.w.stack_cap + 1);
   memset(stats, 0, 8 * sizeof(uint64_t));
   stats[7] = ~0ull;
   for (size_t i = 0; i < n; ++i) {
@@ -271,7 +258,7 @@ int wide_counts(const float* V, size_t nvf, const uint32_t* I, size_t nt, const 
     snprintf(err, errlen, "%s", why.c_str());
     return 1;
   }
-  std::vector<int2> lds(kWideLds), ovf((size_t)(2 * b.w.stack_cap + 5));
+  std::vector<int2> lds(kWideLds), ovf((size_t)(size_t)b.w.stack_cap + 1);
   for (size_t i = 0; i < n; ++i) {
     const float* r = rays + 8 * i;
     WideRay R;
