@@ -1836,7 +1836,7 @@ int pt_selftest_math(int device, int fn, const float* x, float* y, size_t n) {
 
 int pt_selftest_exhaustive(int device, int fn, unsigned long long* mismatches, uint32_t* first_bad) {
   if (!mismatches || !first_bad) return fail(PT_ERR_INVALID, "null argument");
-  if (fn < 0 || fn > 5) return fail(PT_ERR_INVALID, "fn must be 0..5");
+  if (fn < 0 || fn > 3) return fail(PT_ERR_INVALID, "fn must be 0..3");
   PT_HIP(hipSetDevice(device));
   unsigned long long* d_bad = nullptr;
   PT_HIP(hipMalloc((void**)&d_bad, 16));

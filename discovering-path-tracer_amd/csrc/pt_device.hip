@@ -526,8 +526,7 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
         }
       }
       rad = add(rad, muls(mul(mul(thr, sss_thr), sl), 1.0f + sss_radius * 0.5f));
-      // -travel / (sss_radius * 1.5) with sss_radius = 1 (div_1p5_: the IEEE quotient)
-      sss_thr = mul(sss_thr, muls(sss_albedo, exp_(div_1p5_(-travel))));
+      sss_thr = mul(sss_thr, muls(sss_albedo, exp_(-travel / (sss_radius * 1.5f))));
       so = sub(cp, muls(sn, OFFSET));
       sd = sample_sphere(&rng);
     }
@@ -655,8 +654,7 @@ __device__ v3 path_trace_fused(const RenderParams& P, v3 ro, v3 rd, uint32_t see
         }
       }
       const v3 thr_k = mul(thr, sss_thr);
-      // -travel / (sss_radius * 1.5) with sss_radius = 1 (div_1p5_: the IEEE quotient)
-      sss_thr = mul(sss_thr, muls(sss_albedo, exp_(div_1p5_(-travel))));
+      sss_thr = mul(sss_thr, muls(sss_albedo, exp_(-travel / (sss_radius * 1.5f))));
       so = sub(cp, muls(sn, OFFSET));
       sd = sample_sphere(&rng);
       PT_WALK4(PARK, walk_pair<CNT>(P, NL > 0 && s_need, s_o, s_d, s_lim, &occ, k + 1 < P.sss_bounces, so, sd, cand, &sh, c));
@@ -1126,8 +1124,7 @@ __global__ __launch_bounds__(256) void math_kernel(int fn, const float* __restri
 // Exhaustive equivalence of the device's fast-quotient math with the IEEE
 // definitions (pt_math.h): every one of the 2^32 input bit patterns.
 // fn 0 rcp_ vs 1/x, 1 log_, 2 exp_, 3 acos_ (each vs its FAST=false
-// form), 4 sqrt_ vs the IEEE square root, 5 div_1p5_ vs x / 1.5f.  NaN
-// results compare equal when both are NaN.
+// form).  NaN results compare equal when both are NaN.
 __global__ __launch_bounds__(256) void exhaustive_kernel(int fn, unsigned long long* bad, uint32_t* first_bad) {
   unsigned long long nbad = 0;
   uint32_t first = 0xffffffffu;
@@ -1139,9 +1136,7 @@ __global__ __launch_bounds__(256) void exhaustive_kernel(int fn, unsigned long l
       case 0: a = rcp_(x); b = 1.0f / x; break;
       case 1: a = log_(x); b = log_impl<false>(x); break;
       case 2: a = exp_(x); b = exp_impl<false>(x); break;
-      case 3: a = acos_(x); b = acos_impl<false>(x); break;
-      case 4: a = sqrt_(x); b = sqrt_ieee_(x); break;
-      default: a = div_1p5_(x); b = x / 1.5f; break;
+      default: a = acos_(x); b = acos_impl<false>(x); break;
     }
     const bool same = __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
     if (!same) {
@@ -1435,8 +1430,7 @@ __device__ bool path_step(const RenderParams& P, const CamFrame& F, PathSt& S, T
           return true;
         }
         S.rad = add(S.rad, muls(mul(mul(S.thr, S.sss_thr), S.acc3), 1.0f + sss_radius * 0.5f));
-        // -travel / (sss_radius * 1.5) with sss_radius = 1 (div_1p5_: the IEEE quotient)
-        S.sss_thr = mul(S.sss_thr, muls(sss_albedo, exp_(div_1p5_(-S.travel))));
+        S.sss_thr = mul(S.sss_thr, muls(sss_albedo, exp_(-S.travel / (sss_radius * 1.5f))));
         S.so = sub(S.cp, muls(S.sn, OFFSET));
         S.sd = sample_sphere(&S.rng);
         S.k++;

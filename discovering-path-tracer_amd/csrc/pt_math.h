@@ -35,7 +35,7 @@ PT_FN float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 PT_FN float fmin_(float a, float b) { return __builtin_fminf(a, b); }
 PT_FN float fmax_(float a, float b) { return __builtin_fmaxf(a, b); }
 PT_FN float fabs_(float a) { return __builtin_fabsf(a); }
-PT_FN float sqrt_ieee_(float a) { return __builtin_sqrtf(a); }
+PT_FN float sqrt_(float a) { return __builtin_sqrtf(a); }
 PT_FN float floor_(float a) { return __builtin_floorf(a); }
 // explicit fused multiply-add (one rounding; -ffp-contract=off never forms it)
 PT_FN float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
@@ -82,42 +82,6 @@ PT_FN float qdiv_(float a, float b) {
 #endif
 }
 #define PT_DIV(FAST, a, b) ((FAST) ? qdiv_((a), (b)) : (a) / (b))
-
-// RN(sqrt(x)).  Device, x in [2^-96, FLT_MAX]: the hardware square root
-// (about 1 ulp) corrected by the residuals of its two neighbours, the
-// correction of the compiler's own IEEE sequence without its scaling of small
-// inputs and its zero/infinity fix-up, which this range does not need; other
-// inputs (zero, tiny, infinite, negative, NaN) take the IEEE square root.
-// Checked against the IEEE square root for all 2^32 inputs
-// (pt_selftest_exhaustive).
-PT_FN float sqrt_(float x) {
-#if PT_FAST_DEV
-  if (f2u(x) - 0x0f800000u <= 0x7f7fffffu - 0x0f800000u) {
-    const float y = __builtin_amdgcn_sqrtf(x);
-    const float dn = u2f(f2u(y) - 1u), up = u2f(f2u(y) + 1u);
-    const float r = __builtin_fmaf(-dn, y, x) <= 0.0f ? dn : y;
-    return __builtin_fmaf(-up, y, x) > 0.0f ? up : r;
-  }
-#endif
-  return __builtin_sqrtf(x);
-}
-
-// RN(x / 1.5), the SSS throughput's exponent -travel / (sss_radius * 1.5)
-// (raytrace_comp.comp:405, sss_radius = 1): on the device, for |x| in
-// [2^-124, 2^127], x * RN(2/3) and one remainder correction; elsewhere IEEE
-// division.  Checked against x / 1.5f for all 2^32 inputs
-// (pt_selftest_exhaustive).
-PT_FN float div_1p5_(float x) {
-#if PT_FAST_DEV
-  const float ax = __builtin_fabsf(x);
-  if (ax >= 0x1p-124f && ax <= 0x1p127f) {
-    const float q = x * 0x1.555556p-1f;
-    const float r = __builtin_fmaf(-q, 1.5f, x);
-    return __builtin_fmaf(r, 0x1.555556p-1f, q);
-  }
-#endif
-  return x / 1.5f;
-}
 
 // ---------------------------------------------------------------- logf ----
 // fdlibm e_logf.c algorithm: x = 2^k (1+f), f in [sqrt(2)/2-1, sqrt(2)-1),

@@ -440,8 +440,7 @@ int pt_reset_launch_times(pt_context* ctx);
  * 7 first RNG draw from the seed given as the float's bits, 8 reciprocal. */
 int pt_selftest_math(int device_ordinal, int fn, const float* x, float* y, size_t n);
 /* Exhaustive check of the device's fast-quotient math against its IEEE
- * definitions over all 2^32 inputs: fn 0 rcp (1/x), 1 log, 2 exp, 3 acos,
- * 4 sqrt, 5 x / 1.5.
+ * definitions over all 2^32 inputs: fn 0 rcp (1/x), 1 log, 2 exp, 3 acos.
  * Writes the number of differing inputs and the smallest such
  * input's bit pattern (0xffffffff if none). */
 int pt_selftest_exhaustive(int device, int fn, unsigned long long* mismatches, uint32_t* first_bad);
