@@ -22,6 +22,7 @@ int g_mode = pt::WIDE_SAH;   // wide_set_mode
 int g_node = 128;            // wide_set_variant: node bytes (64: the quantized layout with exact leaf tests)
 int g_queue = 0;             // ... and 1: the queued leaf tests with per-lane flushes; 2: with the wave-wide flush's
                              // merge (flush_lexmin, the trace kernel's default)
+unsigned long long g_steps = 0;   // walk steps (wide_step calls) since wide_set_variant (tools/walk_counts.py)
 
 struct Built {
   pt::WideBVH w;
@@ -105,7 +106,7 @@ void walk(WideRay& R, const Built& b, int2* lds, int2* ovf, bool* exact, uint32_
   std::vector<int> cand(kWideQ * 64, -1);
   bool fin = false;
   for (;;) {
-    if (!fin)
+    if (!fin && ++g_steps)
       fin = wide_step<true, true, QN>(R, nodes, b.tris.data(), lds, 1, ovf, 1, b.w.stack_cap, exact, cn, cl,
                                       cand.data(), leafbox);
     if (*exact) return;
@@ -132,7 +133,9 @@ void wide_set_mode(int mode) { g_mode = mode; }
 void wide_set_variant(int node_bytes, int queue) {
   g_node = node_bytes;
   g_queue = queue;
+  g_steps = 0;
 }
+unsigned long long wide_steps() { return g_steps; }
 
 // info[0] wide nodes, info[1] stack bound.  Returns 0, or 1 with the reason in err.
 int wide_info(const float* V, size_t nvf, const uint32_t* I, size_t nt, const float* N, size_t nn, int int_bits,
