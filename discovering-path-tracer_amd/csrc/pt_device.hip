@@ -2008,18 +2008,25 @@ constexpr int kFuseWalk = 16;   // lane state: walking the fused shadow ray
 #ifndef PT_WIDE_FLUSH_WAVE
 #define PT_WIDE_FLUSH_WAVE 1
 #endif
+// Inclusive prefix sum over the wave's 64 lanes (every lane active) by DPP
+// row shifts within each row of 16 and row broadcasts across rows: six VALU
+// steps, where __shfl_up made six dependent LDS-crossbar round trips.
+__device__ __forceinline__ int wave_incl_sum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 into rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 into rows 2, 3
+  return v;
+}
 template <bool CNT, bool QN>
 __device__ __forceinline__ bool wide_flush_wave(WideRay& R, bool mine, const float4* __restrict__ tris, const int* cand,
                                                 unsigned long long* keys, int lane, uint32_t* cl,
                                                 const float4* __restrict__ leaf_box) {
   const int n = mine ? R.nc : 0;
-  int incl = n;   // inclusive prefix sum of the queue lengths
-#pragma unroll
-  for (int s = 1; s < 64; s <<= 1) {
-    const int v = __shfl_up(incl, (unsigned)s);
-    if (lane >= s) incl += v;
-  }
-  const int total = __shfl(incl, 63);
+  const int incl = wave_incl_sum(n);   // inclusive prefix sum of the queue lengths
+  const int total = __builtin_amdgcn_readlane(incl, 63);
   const int off = incl - n;
   keys[lane] = ~0ull;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2282,7 +2289,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
 // phase and octant 65.7 / 159.1.  (With the exhaustive walks and refill
 // groups of round 2's first half, kind and octant had measured sphere -0.5 %,
 // 10M cloud +3.5 %; the exhaustive walk keeps the unsorted lists.)
-__device__ __forceinline__ int ray_bin(const Trav& T) {
+[[maybe_unused]] __device__ __forceinline__ int ray_bin(const Trav& T) {
   const int oct = (T.d.x < 0.0f ? 1 : 0) | (T.d.y < 0.0f ? 2 : 0) | (T.d.z < 0.0f ? 4 : 0);
   return (T.shadow ? 8 : 0) | oct;
 }

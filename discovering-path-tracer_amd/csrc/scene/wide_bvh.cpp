@@ -105,18 +105,25 @@ WideCoeffs coeff_max(const WideCoeffs& a, const WideCoeffs& b) {
 // Margins: the float slab's t_near is within (1+u)^3 of the exact entry;
 // S <= (1 + 3u) Smax (Smax from the slab's own differences); |1/d| within 2u
 // of the float reciprocal; each float op of the evaluation rounds once --
-// all covered by the 2^-18 and 2^-20 factors.  A triangle without a bound
-// (k1 infinite) gives c1 = 0: th = 0 culls nothing a hit (t > 1e-6) could need.
+// all covered by the 2^-18 and 2^-20 factors.  The device evaluates the same
+// bound with the t_near factor moved into the constants:
+//   th = c1' * (t_near - (E0' + E1' Smax) (|1/d| + 1)),
+//   c1' = c1 (1 - 2^-20) rounded down, E' = E / (1 - 2^-20) rounded up,
+// which is c1 * (t_near (1 - 2^-20) - (E0 + E1 Smax) ...) exactly in real
+// arithmetic (c1' E' = c1 E), with one float rounding fewer per axis.  A
+// triangle without a bound (k1 infinite) gives c1 = 0: th = 0 culls nothing
+// a hit (t > 1e-6) could need.
 void node_cull_consts(const WideCoeffs& co, float* out) {
   out[3] = 0.0f;
   if (!(co.k1 <= 0.5) || !(co.eps0 < 1e30) || !(co.eps1 < 1e30) || !(co.k2 < 1e30)) {
     out[0] = out[1] = out[2] = 0.0f;
     return;
   }
+  const double k = 1.0 - 0x1p-20;   // the t_near factor
   const double c1 = down_f((1.0 - co.k1) / (1.0 + gam(3)) * (1.0 - 0x1p-20));
-  out[0] = (float)c1;
-  out[1] = up_f(co.eps0 * (1.0 + 0x1p-18));
-  out[2] = up_f(std::max(co.eps1, co.k2 / c1) * (1.0 + 3.0 * kU) * (1.0 + 0x1p-18));
+  out[0] = (float)down_f(c1 * k);
+  out[1] = up_f(co.eps0 * (1.0 + 0x1p-18) / k);
+  out[2] = up_f(std::max(co.eps1, co.k2 / c1) * (1.0 + 3.0 * kU) * (1.0 + 0x1p-18) / k);
 }
 
 // Error bound of intersectTriangle (raytrace_comp.comp:114-157) as the
