@@ -181,6 +181,15 @@ def test_coefficients_bound_shape():
     assert 0 < k1 < 1e-3 and 0 < k2 < 1e-3 and eps0 < 1e-5 and eps1 < 1e-3
     c1, E0, E1, _ = node
     assert 0.999 < c1 < 1.0 and E0 >= eps0 and E1 >= eps1 and E1 >= k2 / c1
+    # the device evaluates c1' (t_near - E' Smax ...) with the (1 - 2^-20)
+    # t_near factor folded into the constants (node_cull_consts): c1' is at
+    # most c1 k and each E' at least E / k, so the threshold is never above
+    # c1 (t_near k - E Smax ...) of the unfolded bound
+    k, u = 1.0 - 2.0 ** -20, 2.0 ** -24
+    c1_unfolded = (1.0 - k1) / (1.0 + 3 * u / (1 - 3 * u)) * k
+    assert float(c1) <= c1_unfolded * k
+    assert float(E0) >= eps0 * (1.0 + 2.0 ** -18) / k
+    assert float(E1) >= max(eps1, k2 / c1_unfolded) * (1.0 + 2.0 ** -18) / k
     assert lib().wide_coeffs(np.float32([2, 0, 0]), np.float32([0, 2, 0]), co, node) == 1
 
 
