@@ -244,7 +244,10 @@ def roofline_block(prof, time_ms, alg_bytes, kernel, kernel_ms, interval_ms, n_t
            "frac_of_achievable": None if achieved is None else round(achieved / HBM_ACHIEVABLE_GBS, 5),
            "achievable_GBps": HBM_ACHIEVABLE_GBS,
            "traffic_basis": "rocprofv3 FETCH_SIZE x2 + WRITE_SIZE per launch (every gfx950 fabric read request is a "
-                            "128-B line tallied at 64 B: profiles/r02/fetch_calibration.json)"}
+                            "128-B line tallied at 64 B: profiles/r02/fetch_calibration.json)",
+           "traffic_label": "L2-miss fabric bytes: HBM plus Infinity-Cache (MALL) hits, which FETCH_SIZE counts "
+                            "(MI355X_MICROARCH.md, HBM section); an upper bound on HBM bytes, so frac bounds the HBM "
+                            "fraction from above"}
     if prof is not None:
         hb = prof[1]["hbm_bytes_per_launch"]
         if "raw_fetch_kib" in hb:
@@ -398,17 +401,62 @@ def spread(ms):
             "max": round(float(np.max(ms)), 3), "frames": int(ms.size)}
 
 
+def price_leg(out, workload, traced, kernel_ms, alg, ref_rays):
+    """The leg's rooflines from the committed profile of `workload` (this
+    kernel source and camera): HBM (roofline_block), the wide walk's node
+    fetches against the measured gather ceiling (configs 3/4 primary, config
+    5 beside HBM) and VALU issue."""
+    prof = profiled_traffic(workload)
+    gather = gather_roofline(workload)
+    if gather is not None:
+        # the wide walk's node fetches against the measured ceiling of
+        # dependent 64-B gathers from a table of the tree's size at the trace
+        # kernel's occupancy and memory-level parallelism (tools/gather_roof.hip)
+        visits = float(traced["nodes"])
+        ach = visits / (kernel_ms * 1e-3) / 1e9
+        roof = {"bound": gather["bound"], "achieved": round(ach, 3), "peak": gather["Grec_per_s"],
+                "unit": "G wide-node fetches/s", "frac": round(ach / gather["Grec_per_s"], 4),
+                "node_visits_per_frame": int(visits), "peak_basis": gather["basis"],
+                "time_basis": out["roofline"]["time_basis"] + "; every kernel of the frame"}
+        share = trace_share(prof)
+        if share is not None:
+            # the trace kernel's own time: its share of the frame's kernel
+            # time in the committed profile of this source and workload
+            roof["trace_kernel_share"] = round(share, 4)
+            roof["achieved_trace_kernel"] = round(ach / share, 3)
+            roof["frac_trace_kernel"] = round(ach / share / gather["Grec_per_s"], 4)
+        if gather["bound"] == "hbm_gather":
+            out["roofline_gather"] = roof   # beside the fabric-bytes roofline (config 5)
+        else:
+            roof["traffic"] = out["roofline"]["traffic"]
+            roof["hbm"] = {k: out["roofline"][k] for k in ("achieved", "peak", "unit", "frac", "traffic",
+                                                           "traffic_source", "traffic_label")}
+            out["roofline"] = roof
+    if prof is not None and prof[1].get("sq_per_launch", {}).get("SQ_INSTS_VALU"):
+        # the same frame against the VALU issue peak (committed PMC profile)
+        valu = prof[1]["sq_per_launch"]["SQ_INSTS_VALU"]
+        gi = valu / (kernel_ms * 1e-3) / 1e9
+        out["roofline_valu"] = {"achieved": round(gi, 2), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
+                                "frac": round(gi / VALU_PEAK_GINST, 4), "valu_wave_instr_per_frame": int(valu),
+                                "source": prof[0],
+                                "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 f32 instruction"}
+
+
 def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaustive_too=False, contexts=1):
-    """One BASELINE config on one GPU (N = 1 only): the reference rays of a
-    stats-mode frame, the walks of a counting frame, `steps` timed frames
-    after one warmup, and the roofline priced from the committed profile of
-    this workload (tools/profile_workload.sh).  exhaustive_too: one more frame
-    with PT_OPT_WIDE 0 -- the threaded exhaustive walk, the reference's own
-    traversal shape -- reported as `exhaustive_walk` (workload + "_exhaustive").
-    contexts > 1: the timed frames alternate between that many contexts
-    (own stream, accumulation and wavefront buffers each), two frames in
-    flight; ms per frame is then the wall time of a run over its frames, and
-    the contexts' frames are checked bitwise equal."""
+    """One BASELINE config on one GPU (N = 1 only), at two cameras: BASELINE's
+    (0,0,5) (Camera.cpp:7-9, Camera.h:34-36) leads -- its
+    numbers are the leg's `value` and `roofline`, priced from the committed
+    profile of `workload + "_refcam"` -- and the scene's frame-filling camera
+    (load_scene) follows as `frame_filling_camera`, priced from `workload`.
+    At each: the reference rays of a stats-mode frame, the walks of a
+    counting frame, `steps` timed frames after one warmup frame per context.
+    exhaustive_too: one more frame at the frame-filling camera with
+    PT_OPT_WIDE 0 -- the threaded exhaustive walk, the reference's own
+    traversal shape -- reported as `exhaustive_walk` (workload +
+    "_exhaustive").  contexts > 1: the timed frames alternate between that
+    many contexts (own stream, accumulation and wavefront buffers each),
+    frames in flight; ms per frame is then the wall time of a run over its
+    frames, and the contexts' frames are checked bitwise equal."""
     import ptamd
     import scenes
     import torch
@@ -422,13 +470,11 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
         x = ptamd.Renderer(device)
         x.upload_scene(v, i, n, int_bits=int_bits)
         x.upload_lights(scenes.REFERENCE_LIGHT)
-        x.set_camera(cam)
         x.set_params(depth, sss)
         if contexts > 1:
             # the other frames fill a frame's last ray rounds: the tail kernel
             # (PT_OPT_WF_TAIL, for a frame alone) then costs more than it saves
             x.set_option(ptamd.PT_OPT_WF_TAIL, 0)
-        if contexts > 1:
             hs = HipStream(device)
             hip_streams.append(hs)
             x.set_stream(hs.handle)
@@ -441,88 +487,53 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
     ntri = i.size // 3
     del v, i, n
     setup_s = time.perf_counter() - t_setup
-    t0 = time.perf_counter()
-    ref, traced = reference_and_traced_counts(r, spp)
-    counts_s = time.perf_counter() - t0
-    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
-    for x in ctxs:
-        x.render(0, spp)
-    torch.cuda.synchronize()
-    if contexts > 1:
-        walls = time_frames_pipelined(ctxs, spp, steps)
-        kt = walls
-        want = r.read_accum().view(np.uint32)
-        for x in ctxs[1:]:
-            if not np.array_equal(x.read_accum().view(np.uint32), want):
-                raise SystemExit(f"bench: {scene_name} leg: the pipelined contexts' frames differ")
-    else:
-        walls, kt = time_frames(r, spp, steps)
-    dt = float(np.median(walls)) * 1e-3   # the median frame (min/max beside it)
-    kernel_ms = float(np.median(kt)) if kt.size else float("nan")
-    alg = algorithmic_bytes({"nodes": ref[1], "leaf_tests": ref[2], "samples": ref[3]})
-    prof = profiled_traffic(workload)
-    cfg = {"workload": f"{desc} {W}x{H} {spp}spp {depth} bounces {sss} sss", "triangles": int(ntri),
-           "int_bits_nodes": bool(int_bits), "rays_per_frame": int(ref[0])}
-    add_traced(cfg, traced, dt)
-    out = {"metric": "Mrays/s (reference-equivalent traceRay calls)", "value": round(ref[0] / dt / 1e6, 3),
-           "unit": "Mrays/s", "ms_per_step": round(dt * 1e3, 2), "steps": steps, "warmup": 1,
-           "ms_per_frame": spread(walls), "kernel_ms_per_frame": spread(kt) if kt.size else None,
-           "kernel": KERNEL_NAMES.get(r.last_kernel(), "?"), "config": cfg,
-           "roofline": roofline_block(prof, kernel_ms, alg, KERNEL_NAMES.get(r.last_kernel(), "?"), kernel_ms,
-                                      kernel_ms, int(kt.size),
-                                      f"median wall ms per frame of runs of {steps} frames alternating over "
-                                      f"{contexts} contexts (frames overlap)" if contexts > 1 else
-                                      "median kernel_ms (HIP events around each frame's launches on the render "
-                                      "stream)"),
-           "contexts": contexts,
-           "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
-    gather = gather_roofline(workload)
-    if gather is not None and gather["bound"] == "hbm_gather":
-        # beside the HBM roofline: the node fetches against the dependent
-        # 64-B gather ceiling of a 1-GB table (HBM-resident, one load in
-        # flight per lane at the trace kernel's occupancy)
-        visits = float(traced["nodes"])
-        ach = visits / (kernel_ms * 1e-3) / 1e9
-        out["roofline_gather"] = {"bound": "hbm_gather", "achieved": round(ach, 3), "peak": gather["Grec_per_s"],
-                                  "unit": "G wide-node fetches/s", "frac": round(ach / gather["Grec_per_s"], 4),
-                                  "node_visits_per_frame": int(visits), "peak_basis": gather["basis"]}
-        share = trace_share(prof)
-        if share is not None:
-            out["roofline_gather"]["trace_kernel_share"] = round(share, 4)
-            out["roofline_gather"]["frac_trace_kernel"] = round(ach / share / gather["Grec_per_s"], 4)
-        gather = None
-    if gather is not None:
-        # the wide walk's node fetches against the measured ceiling of
-        # dependent 64-B gathers from a table of the tree's size (one fetch
-        # in flight per lane, the trace kernel's occupancy): the tree of
-        # configs 3/4 (2.6 MB) lives in L2, so HBM is not its bound
-        visits = float(traced["nodes"])
-        ach = visits / (kernel_ms * 1e-3) / 1e9
-        roof = {"bound": gather["bound"], "achieved": round(ach, 3), "peak": gather["Grec_per_s"],
-                "unit": "G wide-node fetches/s", "frac": round(ach / gather["Grec_per_s"], 4),
-                "traffic": out["roofline"]["traffic"], "node_visits_per_frame": int(visits),
-                "time_basis": out["roofline"]["time_basis"] + "; every kernel of the frame",
-                "peak_basis": gather["basis"], "hbm": {k: out["roofline"][k] for k in
-                                                       ("achieved", "peak", "unit", "frac", "traffic",
-                                                        "traffic_source")}}
-        share = trace_share(prof)
-        if share is not None:
-            # the trace kernel's own time: its share of the frame's kernel
-            # time in the committed profile of this source and workload
-            roof["trace_kernel_share"] = round(share, 4)
-            roof["achieved_trace_kernel"] = round(ach / share, 3)
-            roof["frac_trace_kernel"] = round(ach / share / gather["Grec_per_s"], 4)
-        out["roofline"] = roof
-    if prof is not None and prof[1].get("sq_per_launch", {}).get("SQ_INSTS_VALU"):
-        # the same frame against the VALU issue peak (committed PMC profile):
-        # the traversal of an L2/MALL-resident tree is bound by issue and
-        # dependent latency, not by HBM
-        valu = prof[1]["sq_per_launch"]["SQ_INSTS_VALU"]
-        gi = valu / (kernel_ms * 1e-3) / 1e9
-        out["roofline_valu"] = {"achieved": round(gi, 2), "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
-                                "frac": round(gi / VALU_PEAK_GINST, 4), "valu_wave_instr_per_frame": int(valu),
-                                "source": prof[0],
-                                "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 f32 instruction"}
+    base = desc.split(", camera")[0]
+
+    def measure(camera, cam_desc, wl):
+        for x in ctxs:
+            x.set_camera(camera)
+        t0 = time.perf_counter()
+        r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 0)
+        ref, traced = reference_and_traced_counts(r, spp)
+        counts_s = time.perf_counter() - t0
+        r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+        for x in ctxs:
+            x.render(0, spp)
+        torch.cuda.synchronize()
+        if contexts > 1:
+            walls = time_frames_pipelined(ctxs, spp, steps)
+            kt = walls
+            want = r.read_accum().view(np.uint32)
+            for x in ctxs[1:]:
+                if not np.array_equal(x.read_accum().view(np.uint32), want):
+                    raise SystemExit(f"bench: {scene_name} leg: the pipelined contexts' frames differ")
+        else:
+            walls, kt = time_frames(r, spp, steps)
+        dt = float(np.median(walls)) * 1e-3   # the median frame (min/max beside it)
+        kernel_ms = float(np.median(kt)) if kt.size else float("nan")
+        alg = algorithmic_bytes({"nodes": ref[1], "leaf_tests": ref[2], "samples": ref[3]})
+        cfg = {"workload": f"{base}, {cam_desc} {W}x{H} {spp}spp {depth} bounces {sss} sss", "triangles": int(ntri),
+               "int_bits_nodes": bool(int_bits), "rays_per_frame": int(ref[0]), "profile_workload": wl}
+        add_traced(cfg, traced, dt)
+        kname = KERNEL_NAMES.get(r.last_kernel(), "?")
+        out = {"metric": "Mrays/s (reference-equivalent traceRay calls)", "value": round(ref[0] / dt / 1e6, 3),
+               "unit": "Mrays/s", "ms_per_step": round(dt * 1e3, 2), "steps": steps, "warmup": 1,
+               "ms_per_frame": spread(walls), "kernel_ms_per_frame": spread(kt) if kt.size else None,
+               "kernel": kname, "config": cfg,
+               "roofline": roofline_block(profiled_traffic(wl), kernel_ms, alg, kname, kernel_ms, kernel_ms,
+                                          int(kt.size),
+                                          f"median wall ms per frame of runs of {steps} frames alternating over "
+                                          f"{contexts} contexts (frames overlap)" if contexts > 1 else
+                                          "median kernel_ms (HIP events around each frame's launches on the render "
+                                          "stream)"),
+               "contexts": contexts, "counting_passes_s": round(counts_s, 2)}
+        price_leg(out, wl, traced, kernel_ms, alg, ref[0])
+        return out, ref, alg
+
+    out, _, _ = measure(scenes.DEFAULT_CAMERA, "camera (0,0,5) fov 60 (BASELINE.md §3)", workload + "_refcam")
+    out["setup_s"] = round(setup_s, 2)
+    ff, ref_ff, alg_ff = measure(cam, "camera" + desc.split(", camera")[1], workload)
+    ff["note"] = "the scene's frame-filling camera (more pixels on geometry than BASELINE's (0,0,5))"
     if exhaustive_too:
         r.set_option(ptamd.PT_OPT_WIDE, 0)
         r.reset_launch_times()
@@ -533,36 +544,14 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
         kt0 = r.launch_times_ms()
         k0 = float(np.mean(kt0)) if kt0.size else float("nan")
         name0 = "wavefront pipeline, threaded exhaustive walk (PT_OPT_WIDE 0), per frame"
-        out["exhaustive_walk"] = {
-            "value": round(ref[0] / dt0 / 1e6, 3), "unit": "Mrays/s", "ms_per_step": round(dt0 * 1e3, 2),
+        ff["exhaustive_walk"] = {
+            "value": round(ref_ff[0] / dt0 / 1e6, 3), "unit": "Mrays/s", "ms_per_step": round(dt0 * 1e3, 2),
             "steps": 1, "note": "the reference's traversal shape (every box a ray passes, visit order kept); "
                                 "same frame bit for bit",
-            "roofline": roofline_block(profiled_traffic(workload + "_exhaustive"), k0, alg, name0, k0, k0,
+            "roofline": roofline_block(profiled_traffic(workload + "_exhaustive"), k0, alg_ff, name0, k0, k0,
                                        int(kt0.size), "kernel_ms (HIP events around the frame's launches)")}
         r.set_option(ptamd.PT_OPT_WIDE, 1)
-    # the same scene at the reference's default camera (Camera.cpp:7-9,
-    # Camera.h:34-36: pos (0,0,5) looking at the origin, fov 60)
-    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 0)
-    r.set_camera(scenes.DEFAULT_CAMERA)
-    ref2, traced2 = reference_and_traced_counts(r, spp)
-    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
-    for x in ctxs[1:]:
-        x.set_camera(scenes.DEFAULT_CAMERA)
-    for x in ctxs:
-        x.render(0, spp)
-    torch.cuda.synchronize()
-    if contexts > 1:
-        walls2 = time_frames_pipelined(ctxs, spp, steps)
-        kt2 = walls2
-    else:
-        walls2, kt2 = time_frames(r, spp, steps)
-    dt2 = float(np.median(walls2)) * 1e-3
-    cfg2 = {"workload": cfg["workload"].replace(desc, desc.split(", camera")[0] + ", camera (0,0,5) fov 60"),
-            "rays_per_frame": int(ref2[0])}
-    add_traced(cfg2, traced2, dt2)
-    out["reference_camera"] = {"value": round(ref2[0] / dt2 / 1e6, 3), "unit": "Mrays/s",
-                               "ms_per_step": round(dt2 * 1e3, 2), "ms_per_frame": spread(walls2),
-                               "kernel_ms_per_frame": spread(kt2) if kt2.size else None, "config": cfg2}
+    out["frame_filling_camera"] = ff
     del r, ctxs
     torch.cuda.synchronize()
     for hs in hip_streams:
@@ -605,7 +594,10 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
     ctxs = []   # (renderer, stream, accumulation buffer)
     hip_streams = []
     try:
-        scene, cam, int_bits, desc = load_scene(scene_name)
+        scene, _, int_bits, desc = load_scene(scene_name)
+        # BASELINE's camera for every config (Camera.cpp:7-9)
+        cam = scenes.DEFAULT_CAMERA
+        desc = desc.split(", camera")[0] + ", camera (0,0,5) fov 60"
         v, i, n, _, _ = scene.arrays()
         del scene
         for _ in range(contexts):
@@ -642,14 +634,20 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
     setup_s = time.perf_counter() - t_setup
     r0 = ctxs[0][0]
 
-    def reduce_sum(t):
+    def reduce_sum(r, stream, t):
         if backend == "nccl":
-            dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)   # the current stream waits for it
+            with torch.cuda.stream(stream):   # the reduce follows this context's render
+                dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)
         else:
-            c = t.cpu()
+            # gloo (the one-GPU rehearsal): the render is waited for on its own
+            # stream, then the buffer is staged through the host by the
+            # renderer (pt_read_accum), with no torch stream in between
+            c = torch.from_numpy(r.read_accum())
             dist.reduce(c, dst=0, op=dist.ReduceOp.SUM)
             if rank == 0:
-                t.copy_(c)
+                with torch.cuda.stream(stream):
+                    t.view(-1).copy_(c.to(dev))
+                stream.synchronize()
 
     def allreduce(vals, op):
         t = torch.tensor(np.asarray(vals, np.float64), dtype=torch.float64, device=coll)
@@ -657,7 +655,7 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
         return t.cpu().numpy()
 
     # reference traceRay calls of the whole frame: each rank counts its share
-    torch.cuda.set_stream(ctxs[0][1])
+    log(f"{scene_name} leg: counting passes")
     t0 = time.perf_counter()
     mine, traced = reference_and_traced_counts(r0, spp)
     ref = allreduce(mine, dist.ReduceOp.SUM)
@@ -667,14 +665,15 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
 
     def frame_once(j):
         r, stream, frame = ctxs[j % len(ctxs)]
-        torch.cuda.set_stream(stream)   # the reduce follows this context's render
         r.clear()                       # +0 owned, -0 elsewhere
         r.render(0, spp)
-        reduce_sum(frame)
+        reduce_sum(r, stream, frame)
 
+    log(f"{scene_name} leg: warmup")
     for j in range(len(ctxs)):   # warmup
         frame_once(j)
     torch.cuda.synchronize(dev)
+    log(f"{scene_name} leg: timed runs")
     walls = []
     for _ in range(3):
         dist.barrier()
@@ -689,6 +688,7 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
     wmin = allreduce(walls, dist.ReduceOp.MIN)
     out = None
     if rank == 0:
+        log(f"{scene_name} leg: whole-frame check on rank 0")
         got = [f.cpu().numpy().reshape(-1).copy() for _, _, f in ctxs]
         # the whole frame on this GPU alone, same context and kernels
         r0.set_partition(1, 0)
@@ -713,7 +713,6 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
                "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
     del r0, ctxs
     torch.cuda.synchronize(dev)
-    torch.cuda.set_stream(torch.cuda.default_stream(dev))
     for hs in hip_streams:
         hs.close()
     dist.barrier()
@@ -797,6 +796,163 @@ class _StreamWork:
         torch.cuda.current_stream().wait_event(self.ev)
 
 
+def log(msg):
+    """A progress line on stderr, tagged with the rank and the seconds since
+    start: a run that stops shows where."""
+    print(f"bench[{os.environ.get('RANK', '0')}] {time.perf_counter() - T_START:7.1f}s: {msg}", file=sys.stderr,
+          flush=True)
+
+
+def spawn_ranks(n):
+    """`python bench.py --gpus N` without a launcher: start N ranks with
+    torch.distributed.run as a child process (one process per GPU, rendezvous
+    on 127.0.0.1) and return its exit code.  Called before anything touches
+    the GPU; the parent never execs (a GPU-initialised process must not be
+    replaced) and only waits.  Rank 0's JSON line reaches the parent's stdout
+    unchanged."""
+    import subprocess
+    env = dict(os.environ, PT_BENCH_SPAWNED="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--standalone",
+           "--local-addr", "127.0.0.1", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"--gpus {n} without a launcher: spawning {n} ranks ({' '.join(cmd[1:6])} ...)")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(world, rank, backend):
+    """--dry-run: the process-group plumbing of an N-rank run without a GPU
+    call -- every rank joins the group and contributes its rank; rank 0
+    prints one JSON line (the CPU test of the launcher)."""
+    import datetime
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=float(os.environ.get("PT_BENCH_PG_TIMEOUT_S", "60"))))
+    if int(os.environ.get("PT_BENCH_DRY_STALL_RANK", "-1")) == rank:
+        # test hook: this rank never reaches the collective (a stuck rank);
+        # the others must fail within the process-group timeout, not hang
+        time.sleep(3600)
+    t = torch.zeros(world, dtype=torch.int64)
+    t[rank] = rank + 1
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": [int(x) - 1 for x in t.tolist()],
+                          "launcher": "spawned" if os.environ.get("PT_BENCH_SPAWNED") == "1" else "external",
+                          "backend_requested": backend}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def group_leg(devices, v, i, n, int_bits, light, cam, W, H, spp, depth, sss, steps, rays_per_frame):
+    """The drop-in multi-GPU path (SURVEY §8b create(device_ordinals[], n)):
+    one process, one context over `devices` (pt_create_multi), driven as the
+    reference drives its one GPU from one thread (VulkanRenderer.cpp:643-647,
+    mainLoop VulkanRayTracer.cpp:717-865).  Each step is pt_render of the
+    whole frame from batch 0; the members' tiles reach the frame on
+    devices[0] by peer stores (PT_OPT_GROUP_EXCHANGE 0, after the context's
+    own probe check on distinct devices, pt_group_check) and then by staged
+    packed copies (exchange 1).  Both are timed over `steps` frames and the
+    last frame of each is checked bit for bit against a one-GPU render of the
+    same frame on devices[0]."""
+    import ptamd
+    ref = ptamd.Renderer(devices[0])
+    ref.upload_scene(v, i, n, int_bits=int_bits)
+    ref.upload_lights(light)
+    ref.set_camera(cam)
+    ref.set_params(depth, sss)
+    ref.resize_and_clear(W, H)
+    ref.render(0, spp)
+    want = ref.read_accum().view(np.uint32).copy()
+    ref.close()
+    t_setup = time.perf_counter()
+    g = ptamd.Renderer(devices=list(devices))
+    g.upload_scene(v, i, n, int_bits=int_bits)
+    g.upload_lights(light)
+    g.set_camera(cam)
+    g.set_params(depth, sss)
+    g.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+    g.resize_and_clear(W, H)
+    setup_s = time.perf_counter() - t_setup
+    g.render(0, spp)   # runs the peer-store probe check first when members span devices
+    g.synchronize()
+    state, ms_peer, ms_staged = g.group_check()
+    devs, peer = g.group_info()
+    out = {"devices": devs, "setup_s": round(setup_s, 2),
+           "peer_store_check": {"state": {-1: "not run", 0: "matched", 1: "mismatch: staged copies in force",
+                                          -2: "armed"}.get(state, state),
+                                "probe_ms_peer": round(ms_peer, 3), "probe_ms_staged": round(ms_staged, 3)},
+           "peer_stores_in_force": bool(peer),
+           "note": "one process, one thread, pt_create_multi over the devices (the reference's single-thread "
+                   "drop-in); frames whole from batch 0, enqueued back to back, synchronized at the end"}
+    for exch in (0, 1):
+        g.set_option(ptamd.PT_OPT_GROUP_EXCHANGE, exch)
+        for _ in range(3):
+            g.render(0, spp)
+        g.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            g.render(0, spp)
+        g.synchronize()
+        dt = (time.perf_counter() - t0) / steps
+        got = g.read_accum().view(np.uint32)
+        same = bool(np.array_equal(got, want))
+        _, peer = g.group_info()
+        out[f"exchange{exch}"] = {
+            "exchange": "peer stores into the first device's frame" if peer else "staged packed copies (pt_tiles_pack, "
+                                                                                  "hipMemcpyPeerAsync, pt_tiles_unpack)",
+            "ms_per_step": round(dt * 1e3, 4), "steps": steps,
+            "value": None if rays_per_frame != rays_per_frame else round(rays_per_frame / dt / 1e6, 3),
+            "unit": "Mrays/s", "verified_bitwise_vs_single_gpu": same}
+    g.close()
+    return out
+
+
+def group_leg_child(gdevs, args, rays_per_frame):
+    """The group leg in a child process of its own (`bench.py --group-only`):
+    it opens every device of the group, and whatever happens there -- the
+    first cross-device peer stores this build runs -- this run's line is
+    still printed.  Returns the child's JSON (or an error record)."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--group-only", "--group-devices", gdevs,
+           "--steps", str(max(args.steps, 20)), "--scene", args.scene, "--width", str(args.width),
+           "--height", str(args.height), "--spp", str(args.spp), "--depth", str(args.depth), "--sss", str(args.sss),
+           "--camera", args.camera, "--group-rays", repr(float(rays_per_frame))]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    log(f"group leg: pt_create_multi over devices {gdevs} (child process)")
+    try:
+        res = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    except subprocess.TimeoutExpired:
+        return {"error": "group leg: timed out after 300 s"}
+    sys.stderr.write(res.stderr[-4000:])
+    lines = [x for x in res.stdout.splitlines() if x.startswith("{")]
+    if res.returncode != 0 or not lines:
+        return {"error": f"group leg: exit {res.returncode}", "stderr_tail": res.stderr[-1500:]}
+    return json.loads(lines[-1])
+
+
+def group_only(args):
+    """--group-only: the one-process pt_create_multi leg alone (run by
+    group_leg_child)."""
+    import torch  # noqa: F401 -- torch's HIP runtime first (libptamd binds to it)
+    import ptamd
+    import scenes
+    devices = [int(x) for x in args.group_devices.split(",")]
+    visible = torch.cuda.device_count()
+    if max(devices) >= visible:
+        print(json.dumps({"devices": devices, "skipped": f"{visible} devices visible to the group leg's process"}),
+              flush=True)
+        return
+    scene, cam, int_bits, _ = load_scene(args.scene)
+    if args.camera == "reference":
+        cam = scenes.DEFAULT_CAMERA
+    v, i, n, _, _ = scene.arrays()
+    try:
+        out = group_leg(devices, v, i, n, int_bits, scenes.REFERENCE_LIGHT, cam, args.width, args.height, args.spp,
+                        args.depth, args.sss, args.steps, args.group_rays)
+    except ptamd.PTError as e:
+        out = {"devices": devices, "error": str(e)}
+    print(json.dumps(out), flush=True)
+
+
 def main():
     if os.environ.get("PT_BENCH_TRACEBACK_AFTER_S"):
         # diagnostics of a hung run: every thread's stack to stderr after N s
@@ -840,6 +996,15 @@ def main():
     ap.add_argument("--no-scene-legs", action="store_true",
                     help="skip the scene legs (`configs` in the JSON line): configs 3, 4 and 5 on one GPU at "
                          "N=1, configs 4 and 5 across the N GPUs at N>1")
+    ap.add_argument("--camera", choices=["scene", "reference"], default="scene",
+                    help="reference: BASELINE's camera (0,0,5) fov 60 for any --scene (profile runs of the legs)")
+    ap.add_argument("--group-devices", default=None,
+                    help="comma-separated ordinals: also run the one-process pt_create_multi leg over them "
+                         "(default at N > 1: the N devices, from rank 0; 'none' skips it)")
+    ap.add_argument("--group-only", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--group-rays", type=float, default=float("nan"), help=argparse.SUPPRESS)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="the process-group plumbing only (no GPU): every rank joins, rank 0 prints a line")
     ap.add_argument("--profile-run", action="store_true",
                     help="only the warmup and timed frames (no stats/counting passes, legs or CPU baseline): "
                          "the command tools/gpu_*profile.sh runs under rocprofv3")
@@ -864,11 +1029,20 @@ def main():
         args.timing_every = max(args.timing_every, -(-args.steps // 400))
     DEPTH, SSS = args.depth, args.sss
 
+    if args.group_only:
+        group_only(args)
+        return
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: N ranks of this same command under torch.distributed.run
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        dry_run(world, rank, os.environ.get("PT_BENCH_BACKEND", "nccl"))
+        return
     # PT_BENCH_EMULATE_RANKS=N (1-GPU box only): rank 0's step of an N-GPU
     # gather run -- its tile share, pack, the root's unpack of N slots -- with
     # the collective replaced by a device copy of its own slot.  A rehearsal of
@@ -901,7 +1075,14 @@ def main():
             opts = dist.ProcessGroupNCCL.Options()
             opts.is_high_priority_stream = True
             kw = {"device_id": dev, "pg_options": opts}
+        # a collective that one rank never reaches fails after this long
+        # instead of holding every other rank for the default 30 minutes
+        # (VERDICT r04 item 1); sized above the longest rank-0-only stretch
+        # (a whole-frame check render of config 4, the group leg)
+        import datetime
+        kw["timeout"] = datetime.timedelta(seconds=float(os.environ.get("PT_BENCH_PG_TIMEOUT_S", "900")))
         dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+        log(f"process group up ({backend}, {world} ranks)")
 
     def allreduce_max(t):
         if backend == "nccl":
@@ -912,6 +1093,9 @@ def main():
         return c
 
     scene, cam, int_bits, scene_desc = load_scene(args.scene)
+    if args.camera == "reference":
+        cam = scenes.DEFAULT_CAMERA
+        scene_desc = scene_desc.split(", camera")[0] + ", camera (0,0,5) fov 60"
     v, i, n, _, _ = scene.arrays()
     light = scenes.REFERENCE_LIGHT
     r = ptamd.Renderer(device)
@@ -1217,7 +1401,7 @@ def main():
     # least --no-cull-min-ms have passed.  They run here, right before the
     # warmup, so the timed region starts on a GPU that has been busy: from
     # idle the GPU's clocks take ~15 ms of load to ramp up (tools/r04_step_probe.py,
-    # profiles/r04a/probe.log: 20-frame runs 0.2512 ms per frame after 300 ms
+    # profiles/r04/step_probe.log: 20-frame runs 0.2512 ms per frame after 300 ms
     # idle, 0.2374 -> 0.2302 -> 0.2216 in back-to-back runs, 0.2198 over 200).
     no_cull = None
     default_cfg = args.scene == "box" and (W, H, SPP, DEPTH, SSS) == (1920, 1080, 8, 4, 3)
@@ -1232,7 +1416,9 @@ def main():
         torch.cuda.synchronize(dev)
         nc_frames = 0
         t1 = time.perf_counter()
-        while True:
+        # bounded: at most 64 runs of 16 frames (a slow or shared GPU still
+        # reaches the barrier below)
+        for _ in range(64):
             for _ in range(16):
                 nc[nc_frames % len(nc)].render(0, SPP)
                 nc_frames += 1
@@ -1248,6 +1434,10 @@ def main():
                             (f"; rank {emu_rank}'s tile share alone, no exchange" if nparts > 1 else "")}
         if nparts == 1:
             no_cull["value"] = round(rays_per_frame * nc_frames / dt_nc / 1e6, 3)
+        log(f"culling-off frames: {nc_frames} in {dt_nc * 1e3:.1f} ms")
+    if dist is not None:
+        dist.barrier()   # every rank leaves its own pre-warm before the first collective of the step
+    log("warmup")
     run_steps(args.warmup)
     drain()
     if native is not None and native.get("emulated"):
@@ -1257,6 +1447,7 @@ def main():
     if dist is not None:
         dist.barrier()
     r.reset_launch_times()
+    log(f"timed region: {args.steps} steps")
     t0 = time.perf_counter()
     run_steps(args.steps)
     t_enq = time.perf_counter() - t0   # host time to issue the steps (no sync inside)
@@ -1325,6 +1516,9 @@ def main():
                              f"floats; first at pixel {bad[0] // 4} ch {bad[0] % 4}: {got[bad[0]]} vs {want[bad[0]]}")
 
     box_kernel = KERNEL_NAMES.get(r.last_kernel(), "?")
+    comm_ranks = None
+    if native is not None and not native.get("emulated"):
+        comm_ranks = r.dist_info()[0]   # what RCCL itself reports (ncclCommCount)
     dist_legs = None
     if dist is not None and default_cfg and not (args.no_scene_legs or args.profile_run):
         # configs 4 and 5 across the same N GPUs (every rank takes part)
@@ -1338,11 +1532,24 @@ def main():
             legs = [tuple(f if k < 2 else int(f) for k, f in enumerate(e.split()))
                     for e in os.environ["PT_BENCH_DIST_LEGS"].split(";")]
         for key, scene_name, lw, lh, lspp, ldepth, lsteps in legs:
-            if rank == 0:
-                print(f"bench: {key} leg on {world} GPUs ({scene_name} {lw}x{lh} {lspp}spp D{ldepth})",
-                      file=sys.stderr, flush=True)
+            log(f"{key} leg on {world} GPUs ({scene_name} {lw}x{lh} {lspp}spp D{ldepth})")
             dist_legs[key] = dist_scene_leg(dist, backend, device, world, rank, scene_name, lw, lh, lspp, ldepth,
                                             SSS, lsteps)
+
+    # the one-process drop-in (pt_create_multi) over the N devices: rank 0
+    # drives every GPU while the other ranks wait at the barrier
+    group = None
+    gdevs = args.group_devices
+    if gdevs is None and world > 1 and default_cfg and not args.profile_run:
+        gdevs = ",".join(str(k) for k in range(world))
+    if gdevs is not None and gdevs != "none":
+        if dist is not None:
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+        if rank == 0:
+            group = group_leg_child(gdevs, args, rays_per_frame)
+        if dist is not None:
+            dist.barrier()
 
     if rank == 0:
         ms_per_step = dt / args.steps * 1e3
@@ -1432,6 +1639,10 @@ def main():
                                        f"{oracle_img[bad[0]]}")
         if dist_legs is not None:
             out_line["configs"] = dist_legs
+        if group is not None:
+            out_line["group_leg"] = group
+        if comm_ranks is not None:
+            out_line["config"]["rccl_comm_ranks"] = comm_ranks
         if world == 1 and emu == 1 and default_cfg and not (args.no_scene_legs or args.profile_run or args.packed):
             torch.cuda.synchronize(dev)
             del r
@@ -1442,7 +1653,7 @@ def main():
                 bs.close()
             out_line["configs"] = {}
             for key, scene_name, lw, lh, lspp, ldepth, steps, workload, nctx in SCENE_LEGS:
-                print(f"bench: {key} leg ({scene_name} {lw}x{lh} {lspp}spp D{ldepth})", file=sys.stderr, flush=True)
+                log(f"{key} leg ({scene_name} {lw}x{lh} {lspp}spp D{ldepth})")
                 out_line["configs"][key] = scene_leg(scene_name, lw, lh, lspp, ldepth, SSS, steps, device, workload,
                                                      exhaustive_too=key == "config5", contexts=nctx)
         out_line["bench_wall_s"] = round(time.perf_counter() - T_START, 1)

@@ -291,6 +291,7 @@ constexpr int kDistSets = 2 * kDistStreams;     // frame k uses buffer set k % (
 struct DistState {
   ncclComm_t comm = nullptr;
   int nranks = 0, rank = 0;
+  int comm_count = -1;   // ncclCommCount of the communicator (-1: not reported by the library)
   hipStream_t comm_stream = nullptr;
   hipStream_t streams[kDistStreams] = {};
   hipStream_t own[kDistStreams + 1] = {};   // created here: render streams, then the gather stream
@@ -855,7 +856,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     // With frames alternating between two streams (bench.py N > 1), the
     // 1/2 and 1/4 shares favour 4 lanes (0.187 vs 0.210, 0.101 vs 0.110 ms
     // per step) and the 1/8 share 8 (0.062 vs 0.069).  Round 3's kernels,
-    // the emulated root step on the native loop (tools/r03_share_opts.sh,
+    // the emulated root step on the native loop (DESIGN Appendix A, round-3 share options;
     // two runs each): 1/2 share spl 2/4 = 0.1175/0.1225 ms, 1/4 share 4/8 =
     // 0.069/0.082, 1/8 share 4/8 = 0.046/0.042.
     const bool small = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
@@ -1096,6 +1097,17 @@ int pt_group_info(pt_context* c, int* n_devices, int* devices, int max_devices, 
     return PT_OK;
   }
   return ptg::members(c->group, n_devices, devices, max_devices, peer_stores);
+}
+
+int pt_group_check(pt_context* c, int* state, float* ms_peer, float* ms_staged) {
+  if (!c) return fail(PT_ERR_INVALID, "null context");
+  if (!c->group) {
+    if (state) *state = -1;
+    if (ms_peer) *ms_peer = 0.0f;
+    if (ms_staged) *ms_staged = 0.0f;
+    return PT_OK;
+  }
+  return ptg::check_info(c->group, state, ms_peer, ms_staged);
 }
 
 int pt_destroy(pt_context* c) {
@@ -1611,6 +1623,9 @@ int pt_set_option(pt_context* c, int key, int value) {
       if (value < 0 || value > 2) return fail(PT_ERR_INVALID, "PT_OPT_SCENE_IN_LDS takes 0, 1 or 2");
       c->opt_scene_lds = value;
       return PT_OK;
+    case PT_OPT_GROUP_EXCHANGE:
+    case PT_OPT_GROUP_CHECK:
+      return fail(PT_ERR_UNSUPPORTED, "option " + std::to_string(key) + ": multi-device contexts only (pt_create_multi)");
     default:
       return fail(PT_ERR_INVALID, "unknown option " + std::to_string(key));
   }
@@ -2248,6 +2263,7 @@ struct RcclApi {
   void* h = nullptr;
   ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*CommCount)(ncclComm_t, int*) = nullptr;   // optional (the tests' stand-in may lack it)
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
@@ -2278,6 +2294,7 @@ const RcclApi* rccl_api() {
     if (h) {
       api.GetUniqueId = (decltype(api.GetUniqueId))dlsym(h, "ncclGetUniqueId");
       api.CommInitRank = (decltype(api.CommInitRank))dlsym(h, "ncclCommInitRank");
+      api.CommCount = (decltype(api.CommCount))dlsym(h, "ncclCommCount");
       api.CommDestroy = (decltype(api.CommDestroy))dlsym(h, "ncclCommDestroy");
       api.CommAbort = (decltype(api.CommAbort))dlsym(h, "ncclCommAbort");
       api.GroupStart = (decltype(api.GroupStart))dlsym(h, "ncclGroupStart");
@@ -2388,7 +2405,20 @@ int pt_dist_init(pt_context* c, const void* id, int nranks, int rank) {
   ncclUniqueId u;
   memcpy(&u, id, sizeof u);
   PT_NCCL(R->CommInitRank(&d->comm, nranks, u, rank));
+  if (R->CommCount) {
+    int cnt = -1;
+    if (R->CommCount(d->comm, &cnt) == ncclSuccess) d->comm_count = cnt;
+  }
   d->ready = true;
+  return PT_OK;
+}
+
+int pt_dist_info(pt_context* c, int* comm_ranks, int* nranks, int* rank) {
+  if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_dist_info: not on a multi-device context (pt_create_multi)");
+  if (!c || !c->dist) return fail(PT_ERR_INVALID, "pt_dist_info: no communicator (pt_dist_init)");
+  if (comm_ranks) *comm_ranks = c->dist->comm_count;
+  if (nranks) *nranks = c->dist->nranks;
+  if (rank) *rank = c->dist->rank;
   return PT_OK;
 }
 

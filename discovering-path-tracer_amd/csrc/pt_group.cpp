@@ -37,6 +37,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <mutex>
@@ -58,6 +59,7 @@ namespace {
   } while (0)
 
 constexpr int kOptGroupExchange = 18;   // PT_OPT_GROUP_EXCHANGE (pathtracer.h)
+constexpr int kOptGroupCheck = 19;      // PT_OPT_GROUP_CHECK (pathtracer.h)
 
 }  // namespace
 
@@ -69,9 +71,18 @@ struct pt_group {
   std::vector<hipStream_t> s;        // the streams the members run on (s[0] may be the caller's)
   std::vector<hipEvent_t> done;      // member r's last launch (r > 0)
   hipEvent_t start = nullptr;        // the group stream's work before a render
-  bool peer_ok = true;               // every member can map the first device's memory
+  bool peer_ok = true;               // peer stores usable: mapped, and not refused by the exchange check
+  bool peer_map_ok = true;           // every member can map the first device's memory
   int exchange = 0;                  // PT_OPT_GROUP_EXCHANGE: 0 auto, 1 staged copies
   bool staged = false;               // the exchange the current frame buffer was set up for
+  // PT_OPT_GROUP_CHECK: before peer stores carry a frame whose members span
+  // devices, one probe frame through peer stores and one through the staged
+  // exchange are compared bit for bit (check_exchange)
+  int check = 1;                     // 0 never, 1 once per group (distinct devices), 2 every binding, 3 as 2, mismatch forced (tests)
+  bool check_pending = false;        // armed by setup_frame, run by the next render
+  bool check_passed = false;
+  int check_state = -1;              // -1 not run, 0 peer stores matched, 1 mismatch: staged copies in force
+  float check_ms[2] = {0.0f, 0.0f};  // the probe frames' wall time: peer stores, staged copies
   float* frame = nullptr;            // W x H float4 on dev[0]
   bool own_frame = false;
   int W = 0, H = 0;
@@ -207,10 +218,20 @@ int quiesce_all(pt_group* g) {
   return PT_OK;
 }
 
+bool distinct_devices(const pt_group* g) {
+  for (int r = 1; r < g->n; ++r)
+    if (g->dev[(size_t)r] != g->dev[0]) return true;
+  return false;
+}
+
 // (Re)binds the frame of W x H on dev[0] to the members for the exchange in
 // force: peer stores (every member renders into the frame) or staged copies
-// (members r > 0 render into their own buffers and ship packed tiles).
-int setup_frame(pt_group* g) {
+// (members r > 0 render into their own buffers and ship packed tiles).  A
+// staged member's buffer starts as a copy of the frame, so a render that
+// continues the accumulation (first batch > 0) reads the frame's history
+// whichever exchange was in force before.  arm: a new binding,
+// which the exchange check (PT_OPT_GROUP_CHECK) covers before it is used.
+int setup_frame(pt_group* g, bool arm = true) {
   G_RC(quiesce_all(g));
   free_exchange(g);
   g->staged = g->n > 1 && (g->exchange == 1 || !g->peer_ok);
@@ -221,16 +242,143 @@ int setup_frame(pt_group* g) {
       continue;
     }
     G_RC(pt_resize_and_clear(c, g->W, g->H));   // +0 on its tiles, -0 elsewhere
+    const size_t frame_bytes = (size_t)g->W * g->H * 16;
+    G_HIP(hipSetDevice(g->dev[(size_t)r]));
+    // after the clear, on the member's stream: its tiles start from the frame's content
+    G_HIP(hipMemcpyPeerAsync(pt_accum_device_ptr(c), g->dev[(size_t)r], g->frame, g->dev[0], frame_bytes,
+                             g->s[(size_t)r]));
     int tiles = 0;
     G_RC(pt_tiles_owned(c, &tiles));
     const size_t bytes = (size_t)std::max(tiles, 1) * 256 * 16;
-    G_HIP(hipSetDevice(g->dev[(size_t)r]));
     G_HIP(hipMalloc((void**)&g->pack_local[(size_t)r], bytes));
     G_HIP(hipSetDevice(g->dev[0]));
     G_HIP(hipMalloc((void**)&g->pack_root[(size_t)r], bytes));
     g->pack_bytes[(size_t)r] = bytes;
   }
+  if (arm)
+    g->check_pending = !g->staged && g->n > 1 &&
+                       (g->check >= 2 || (g->check == 1 && !g->check_passed && distinct_devices(g)));
   return PT_OK;
+}
+
+// One frame of every member on the group's stream ordering (render's
+// events): start after s[0]'s work, s[0] waits for every member.  staged:
+// members r > 0 pack their tiles, copy them to dev[0] and member 0 unpacks
+// them into `frame`.
+int run_members(pt_group* g, uint32_t first_batch, uint32_t n_batches, bool staged, void* frame,
+                const std::vector<float*>& loc, const std::vector<float*>& root, const std::vector<size_t>& bytes,
+                bool threads) {
+  G_HIP(hipSetDevice(g->dev[0]));
+  G_HIP(hipEventRecord(g->start, g->s[0]));
+  auto one = [&](int r) -> int {
+    if (r == 0) return pt_render(g->m[0], first_batch, n_batches);
+    G_HIP(hipSetDevice(g->dev[(size_t)r]));
+    G_HIP(hipStreamWaitEvent(g->s[(size_t)r], g->start, 0));
+    G_RC(pt_render(g->m[(size_t)r], first_batch, n_batches));
+    if (staged) {
+      G_RC(pt_tiles_pack(g->m[(size_t)r], loc[(size_t)r]));
+      G_HIP(hipSetDevice(g->dev[(size_t)r]));
+      G_HIP(hipMemcpyPeerAsync(root[(size_t)r], g->dev[0], loc[(size_t)r], g->dev[(size_t)r], bytes[(size_t)r],
+                               g->s[(size_t)r]));
+    }
+    G_HIP(hipSetDevice(g->dev[(size_t)r]));
+    G_HIP(hipEventRecord(g->done[(size_t)r], g->s[(size_t)r]));
+    return PT_OK;
+  };
+  G_RC(threads ? each_member(g, one) : each(g, one));
+  G_HIP(hipSetDevice(g->dev[0]));
+  for (int r = 1; r < g->n; ++r) {
+    G_HIP(hipStreamWaitEvent(g->s[0], g->done[(size_t)r], 0));
+    if (staged) G_RC(pt_tiles_unpack(g->m[0], root[(size_t)r], r, frame));
+  }
+  return PT_OK;
+}
+
+// PT_OPT_GROUP_CHECK.  Peer stores assume that a member kernel's stores into
+// the first device's memory are visible there once the group's stream has
+// waited for the member's completion event -- as the reference's dispatch
+// result is visible when its fence returns (VulkanCommandBuffer.cpp:140).
+// Before the first frame relies on that, a probe frame of 16n x 32 pixels
+// (two tiles per member) at 1 spp is rendered both ways -- peer stores into
+// one buffer on the first device, and the staged exchange (pack, peer copy,
+// unpack) into another -- and the two are compared bit for bit on the host.
+// On any difference the group falls back to the staged exchange for good.
+// check == 3 (tests) flips one bit of the peer-store probe before comparing.
+int check_exchange(pt_group* g) {
+  g->check_pending = false;
+  const int n = g->n, PW = 16 * n, PH = 32;
+  const size_t fbytes = (size_t)PW * PH * 16;
+  float* probe[2] = {nullptr, nullptr};   // peer stores, staged copies
+  std::vector<float*> loc((size_t)n, nullptr), root((size_t)n, nullptr);
+  std::vector<size_t> bytes((size_t)n, 0);
+  std::vector<float> host[2];
+  auto release = [&]() {
+    (void)quiesce_all(g);
+    for (int r = 0; r < n; ++r) {
+      gfree(g->dev[(size_t)r], loc[(size_t)r]);
+      gfree(g->dev[0], root[(size_t)r]);
+    }
+    gfree(g->dev[0], probe[0]);
+    gfree(g->dev[0], probe[1]);
+  };
+  auto body = [&]() -> int {
+    G_RC(quiesce_all(g));
+    G_HIP(hipSetDevice(g->dev[0]));
+    for (float*& p : probe) {
+      G_HIP(hipMalloc((void**)&p, fbytes));
+      G_HIP(hipMemset(p, 0, fbytes));
+    }
+    // peer stores: every member renders its tiles straight into probe[0]
+    for (int r = 0; r < n; ++r) G_RC(pt_bind_accum(g->m[(size_t)r], probe[0], PW, PH));
+    auto t0 = std::chrono::steady_clock::now();
+    G_RC(run_members(g, 0, 1, false, probe[0], loc, root, bytes, false));
+    G_RC(quiesce_all(g));
+    auto t1 = std::chrono::steady_clock::now();
+    // staged copies into probe[1]
+    G_RC(pt_bind_accum(g->m[0], probe[1], PW, PH));
+    for (int r = 1; r < n; ++r) {
+      pt_context* c = g->m[(size_t)r];
+      G_RC(pt_resize_and_clear(c, PW, PH));
+      int tiles = 0;
+      G_RC(pt_tiles_owned(c, &tiles));
+      bytes[(size_t)r] = (size_t)std::max(tiles, 1) * 256 * 16;
+      G_HIP(hipSetDevice(g->dev[(size_t)r]));
+      G_HIP(hipMalloc((void**)&loc[(size_t)r], bytes[(size_t)r]));
+      G_HIP(hipSetDevice(g->dev[0]));
+      G_HIP(hipMalloc((void**)&root[(size_t)r], bytes[(size_t)r]));
+    }
+    G_RC(quiesce_all(g));
+    auto t2 = std::chrono::steady_clock::now();
+    G_RC(run_members(g, 0, 1, true, probe[1], loc, root, bytes, false));
+    G_RC(quiesce_all(g));
+    auto t3 = std::chrono::steady_clock::now();
+    g->check_ms[0] = std::chrono::duration<float, std::milli>(t1 - t0).count();
+    g->check_ms[1] = std::chrono::duration<float, std::milli>(t3 - t2).count();
+    G_HIP(hipSetDevice(g->dev[0]));
+    for (int k = 0; k < 2; ++k) {
+      host[k].resize(fbytes / 4);
+      G_HIP(hipMemcpy(host[k].data(), probe[k], fbytes, hipMemcpyDeviceToHost));
+    }
+    return PT_OK;
+  };
+  const int rc = body();
+  release();
+  if (rc) {
+    const std::string msg = pt_last_error();
+    (void)setup_frame(g, false);
+    return pt_fail_internal(rc, "pt_create_multi exchange check: " + msg);
+  }
+  if (g->check == 3) {
+    uint32_t w;
+    memcpy(&w, &host[0][0], 4);
+    w ^= 1u;
+    memcpy(&host[0][0], &w, 4);
+  }
+  const bool same = memcmp(host[0].data(), host[1].data(), fbytes) == 0;
+  g->check_state = same ? 0 : 1;
+  g->check_passed = same;
+  if (!same) g->peer_ok = false;   // staged copies from now on
+  return setup_frame(g, false);
 }
 
 }  // namespace
@@ -280,7 +428,7 @@ int make(const int* ordinals, int n, pt_group** out) {
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) ok = 0;
         (void)hipGetLastError();
       }
-      if (!ok) g->peer_ok = false;
+      if (!ok) g->peer_ok = g->peer_map_ok = false;
     }
   }
   if (hipSetDevice(g->dev[0]) != hipSuccess ||
@@ -396,30 +544,10 @@ int read_accum(pt_group* g, float* rgba, size_t n) { return pt_read_accum(g->m[0
 
 int render(pt_group* g, uint32_t first_batch, uint32_t n_batches) {
   if (!g->frame) return pt_fail_internal(PT_ERR_INVALID, "no accumulation buffer");
+  if (g->check_pending) G_RC(check_exchange(g));
   // the members start after the group stream's earlier work (clear, readback)
-  G_HIP(hipSetDevice(g->dev[0]));
-  G_HIP(hipEventRecord(g->start, g->s[0]));
-  G_RC(each_member(g, [&](int r) -> int {
-    if (r == 0) return pt_render(g->m[0], first_batch, n_batches);
-    G_HIP(hipSetDevice(g->dev[(size_t)r]));
-    G_HIP(hipStreamWaitEvent(g->s[(size_t)r], g->start, 0));
-    G_RC(pt_render(g->m[(size_t)r], first_batch, n_batches));
-    if (g->staged) {
-      G_RC(pt_tiles_pack(g->m[(size_t)r], g->pack_local[(size_t)r]));
-      G_HIP(hipSetDevice(g->dev[(size_t)r]));
-      G_HIP(hipMemcpyPeerAsync(g->pack_root[(size_t)r], g->dev[0], g->pack_local[(size_t)r], g->dev[(size_t)r],
-                               g->pack_bytes[(size_t)r], g->s[(size_t)r]));
-    }
-    G_HIP(hipSetDevice(g->dev[(size_t)r]));
-    G_HIP(hipEventRecord(g->done[(size_t)r], g->s[(size_t)r]));
-    return PT_OK;
-  }));
-  G_HIP(hipSetDevice(g->dev[0]));
-  for (int r = 1; r < g->n; ++r) {
-    G_HIP(hipStreamWaitEvent(g->s[0], g->done[(size_t)r], 0));
-    if (g->staged) G_RC(pt_tiles_unpack(g->m[0], g->pack_root[(size_t)r], r, g->frame));
-  }
-  return PT_OK;
+  return run_members(g, first_batch, n_batches, g->staged, g->frame, g->pack_local, g->pack_root, g->pack_bytes,
+                     true);
 }
 
 int progressive_camera(pt_group* g, const float ubo[16], int* reset) {
@@ -458,6 +586,17 @@ int set_option(pt_group* g, int key, int value) {
     if (value == g->exchange) return PT_OK;
     g->exchange = value;
     return g->frame ? setup_frame(g) : PT_OK;
+  }
+  if (key == kOptGroupCheck) {
+    if (value < 0 || value > 3) return pt_fail_internal(PT_ERR_INVALID, "PT_OPT_GROUP_CHECK takes 0 to 3");
+    g->check = value;
+    if (value >= 2) {   // a fresh check on the next render (peer stores are tried again)
+      g->peer_ok = g->peer_map_ok;
+      g->check_passed = false;
+      return g->frame ? setup_frame(g) : PT_OK;
+    }
+    if (value == 0) g->check_pending = false;
+    return PT_OK;
   }
   return each(g, [&](int r) { return pt_set_option(g->m[(size_t)r], key, value); });
 }
@@ -516,6 +655,13 @@ int members(pt_group* g, int* n, int* devices, int max_devices, int* peer) {
   if (devices)
     for (int r = 0; r < g->n && r < max_devices; ++r) devices[r] = g->dev[(size_t)r];
   if (peer) *peer = g->n > 1 && !(g->exchange == 1 || !g->peer_ok) ? 1 : 0;
+  return PT_OK;
+}
+
+int check_info(pt_group* g, int* state, float* ms_peer, float* ms_staged) {
+  if (state) *state = g->check_pending ? -2 : g->check_state;
+  if (ms_peer) *ms_peer = g->check_ms[0];
+  if (ms_staged) *ms_staged = g->check_ms[1];
   return PT_OK;
 }
 

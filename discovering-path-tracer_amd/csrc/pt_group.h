@@ -51,4 +51,5 @@ int launch_times_ms(pt_group* g, float* out, size_t max_n, size_t* n_out);
 int launch_span_ms(pt_group* g, float* ms, size_t* n_out);
 int reset_launch_times(pt_group* g);
 int members(pt_group* g, int* n, int* devices, int max_devices, int* peer);
+int check_info(pt_group* g, int* state, float* ms_peer, float* ms_staged);
 }  // namespace ptg

@@ -35,6 +35,7 @@ PT_OPT_WF_FUSE = 15
 PT_OPT_WIDE_NODE = 16
 PT_OPT_WF_TAIL = 17
 PT_OPT_GROUP_EXCHANGE = 18
+PT_OPT_GROUP_CHECK = 19
 KERNEL_AUTO, KERNEL_RECURSIVE, KERNEL_WAVEFRONT = 0, 1, 3   # 2 (lane state machine) was removed
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).
@@ -52,6 +53,7 @@ EXPORTS = [
     "pt_set_partition_slots", "pt_get_traced", "pt_wide_info", "pt_partition_items",
     "pt_dist_unique_id", "pt_dist_init", "pt_dist_run", "pt_dist_slot_floats", "pt_dist_finalize",
     "pt_dist_set_streams", "pt_dist_wait", "pt_dist_abort", "pt_create_multi", "pt_group_info",
+    "pt_group_check", "pt_dist_info",
 ]
 
 
@@ -90,6 +92,9 @@ def lib():
             "pt_create": ([i32, ctypes.POINTER(vp)], i32), "pt_destroy": ([vp], i32),
             "pt_create_multi": ([vp, i32, ctypes.POINTER(vp)], i32),
             "pt_group_info": ([vp, ctypes.POINTER(i32), vp, i32, ctypes.POINTER(i32)], i32),
+            "pt_group_check": ([vp, ctypes.POINTER(i32), ctypes.POINTER(ctypes.c_float),
+                                ctypes.POINTER(ctypes.c_float)], i32),
+            "pt_dist_info": ([vp, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
             "pt_set_stream": ([vp, vp], i32), "pt_synchronize": ([vp], i32),
             "pt_upload_scene": ([vp, vp, sz, vp, sz, vp, sz, vp, sz, vp, sz, u32], i32),
             "pt_upload_lights": ([vp, vp, sz], i32), "pt_set_camera": ([vp, vp], i32),
@@ -354,6 +359,14 @@ class Renderer:
                "pt_group_info")
         return [int(x) for x in devs[:n.value]], bool(peer.value)
 
+    def group_check(self):
+        """The peer-store check (PT_OPT_GROUP_CHECK): (state, ms_peer,
+        ms_staged); state -2 armed, -1 not run, 0 matched, 1 mismatch (staged
+        copies in force)."""
+        st, a, b = ctypes.c_int(0), ctypes.c_float(0), ctypes.c_float(0)
+        _check(lib().pt_group_check(self._c, ctypes.byref(st), ctypes.byref(a), ctypes.byref(b)), "pt_group_check")
+        return st.value, a.value, b.value
+
     def upload_scene(self, vertices, indices, nodes, uvs=None, mat=None, int_bits=False):
         v = np.ascontiguousarray(vertices, np.float32).reshape(-1)
         i = np.ascontiguousarray(indices, np.uint32).reshape(-1)
@@ -504,6 +517,13 @@ class Renderer:
     def dist_init(self, uid, nranks, rank):
         b = (ctypes.c_char * 128).from_buffer_copy(uid)
         _check(lib().pt_dist_init(self._c, b, nranks, rank), "pt_dist_init")
+
+    def dist_info(self):
+        """(ranks the RCCL communicator reports via ncclCommCount, or -1;
+        nranks and rank given to pt_dist_init)."""
+        c, n, r = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+        _check(lib().pt_dist_info(self._c, ctypes.byref(c), ctypes.byref(n), ctypes.byref(r)), "pt_dist_info")
+        return c.value, n.value, r.value
 
     def dist_run(self, n_batches, n_frames, frames_ptr=None, n_frame_bufs=1, n_streams=2):
         _check(lib().pt_dist_run(self._c, n_batches, n_frames, n_streams, frames_ptr, n_frame_bufs), "pt_dist_run")

@@ -30,7 +30,11 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 1
+/* ABI history.  2 (round 5): pt_group_check, pt_dist_info and
+ * PT_OPT_GROUP_CHECK added; option values removed since 1 now return
+ * PT_ERR_UNSUPPORTED: PT_OPT_KERNEL 2, PT_OPT_SM_BATCH, PT_OPT_PAIRS 1,
+ * PT_OPT_WIDE_NODE 80 (kernels measured slower on every scene). */
+#define PT_ABI_VERSION 2
 
 enum {
   PT_OK = 0,
@@ -109,7 +113,12 @@ int pt_create(int device_ordinal, pt_context** out);
  * a single-GPU render.  Members store their tiles into that frame directly
  * over xGMI (peer access), or -- when a member cannot map it, or with
  * PT_OPT_GROUP_EXCHANGE 1 -- ship them as packed tiles copied to the first
- * device.  An ordinal may repeat (several members on one device: tests).
+ * device.  Before peer stores carry a frame on members of distinct devices,
+ * a probe frame checks them bit for bit against the packed copies and falls
+ * back to the copies on any difference (PT_OPT_GROUP_CHECK, pt_group_check).
+ * UNVERIFIED on hardware: members on distinct devices have not run in this
+ * build's tests (one-GPU boxes); every group test so far put its members on
+ * one device, where the bit identity is tested.  An ordinal may repeat (several members on one device: tests).
  * With three or more members, members 1..n-1 enqueue their launches from
  * threads of their own (environment PT_GROUP_THREADS=0: all on the calling
  * thread), so a render costs the caller about one member's host time.
@@ -122,6 +131,15 @@ int pt_create_multi(const int* device_ordinals, int n, pt_context** out);
  * whether its members store their tiles straight into the frame (1) or ship
  * packed tiles (0). */
 int pt_group_info(pt_context* ctx, int* n_devices, int* devices, int max_devices, int* peer_stores);
+/* The peer-store check of a multi-device context (PT_OPT_GROUP_CHECK):
+ * *state -2 armed (runs on the next render), -1 not run (members on one
+ * device, staged exchange in force, or a pt_create context), 0 the probe
+ * frames matched bit for bit (peer stores in force), 1 they differed (the
+ * staged exchange is in force from then on); the probe frames' wall times.
+ * Cross-device bit identity of peer stores is verified by this check at run
+ * time; it has not been observed on a multi-GPU node by this build (every
+ * test so far ran its members on one device). */
+int pt_group_check(pt_context* ctx, int* state, float* ms_peer, float* ms_staged);
 int pt_destroy(pt_context* ctx);
 /* Launch on a caller-owned hipStream_t (e.g. a torch.cuda.Stream's handle);
  * NULL returns to the context's own stream — so the legacy default stream
@@ -289,6 +307,9 @@ int pt_dist_slot_floats(pt_context* ctx, size_t* slot_floats);
  * timeout.  pt_dist_abort: ncclCommAbort + free, after such a timeout. */
 int pt_dist_wait(pt_context* ctx, int timeout_ms);
 int pt_dist_abort(pt_context* ctx);
+/* The communicator's rank count as RCCL reports it (ncclCommCount; -1 if
+ * the loaded library lacks it), and the rank count / rank pt_dist_init took. */
+int pt_dist_info(pt_context* ctx, int* comm_ranks, int* nranks, int* rank);
 int pt_dist_finalize(pt_context* ctx);
 
 /* ---- kernel options ---------------------------------------------------- */
@@ -394,6 +415,15 @@ int pt_dist_finalize(pt_context* ctx);
  * always packed copies (pt_tiles_pack, hipMemcpyPeerAsync, pt_tiles_unpack).
  * Output is identical. */
 #define PT_OPT_GROUP_EXCHANGE 18
+/* PT_OPT_GROUP_CHECK (pt_create_multi contexts only): before peer stores
+ * carry a frame, a probe frame (16n x 32 pixels, 1 spp) is rendered once
+ * through peer stores and once through the staged exchange, and the two are
+ * compared bit for bit; on any difference the context falls back to the
+ * staged exchange for good (pt_group_check reports it).  1 (default) = once
+ * per context, when its members span distinct devices; 2 = on the first
+ * render after every pt_resize_and_clear / pt_bind_accum, any devices; 3 =
+ * as 2 with a mismatch forced (tests of the fallback); 0 = never. */
+#define PT_OPT_GROUP_CHECK 19
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */

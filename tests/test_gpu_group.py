@@ -132,3 +132,93 @@ def test_group_rejects_share_calls():
         g.tiles_owned()
     with pytest.raises(ptamd.PTError):
         ptamd.Renderer(devices=[0, 99])
+
+
+def test_group_check_matches_on_one_device():
+    """PT_OPT_GROUP_CHECK 2 runs the peer-store probe on the first render even
+    with every member on device 0: the peer-store and staged probe frames
+    agree bit for bit, peer stores stay in force, and the frame is the
+    single-GPU frame."""
+    v, i, n = _box()
+    g = _setup(ptamd.Renderer(devices=[0, 0, 0]), v, i, n)
+    assert g.group_check()[0] == -1   # one device: not armed by default
+    g.set_option(ptamd.PT_OPT_GROUP_CHECK, 2)
+    g.resize_and_clear(96, 64)
+    assert g.group_check()[0] == -2   # armed: runs on the next render
+    g.render(0, 3)
+    state, ms_peer, ms_staged = g.group_check()
+    assert state == 0 and ms_peer > 0 and ms_staged > 0
+    assert g.group_info()[1] is True
+    ref, _ = O.render(v, i, n.reshape(-1), scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, 96, 64, n_batches=3)
+    _same(g.read_accum(), ref, "after the check")
+
+
+def test_group_check_mismatch_falls_back_to_staged_copies():
+    """PT_OPT_GROUP_CHECK 3 forces the probe comparison to fail (one flipped
+    bit, a test-only option): the context must fall back to the staged
+    exchange for good and still produce the single-GPU frame -- including
+    the history accumulated before the switch."""
+    v, i, n = _box()
+    W, H = 128, 80
+    g = _setup(ptamd.Renderer(devices=[0, 0]), v, i, n)
+    g.resize_and_clear(W, H)
+    g.render(0, 2)                        # peer stores, no check yet
+    assert g.group_info()[1] is True
+    g.set_option(ptamd.PT_OPT_GROUP_CHECK, 3)
+    g.dispatch(2)                         # the check runs first, fails, staged from here on
+    state, _, _ = g.group_check()
+    assert state == 1
+    assert g.group_info()[1] is False
+    g.dispatch(3)
+    ref, _ = O.render(v, i, n.reshape(-1), scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, W, H, n_batches=4)
+    _same(g.read_accum(), ref, "batches 0-1 by peer stores, 2-3 by staged copies")
+
+
+def test_group_exchange_switch_keeps_the_accumulation():
+    """switching to the staged exchange between progressive
+    advances must continue the frame's accumulation (each member's buffer
+    starts from the frame), and switching back too."""
+    v, i, n = _box()
+    W, H = 96, 64
+    g = _setup(ptamd.Renderer(devices=[0, 0, 0]), v, i, n)
+    g.resize_and_clear(W, H)
+    assert g.progressive_camera(scenes.DEFAULT_CAMERA)
+    assert g.progressive_advance(2) == (0, 2)
+    g.set_option(ptamd.PT_OPT_GROUP_EXCHANGE, 1)
+    assert g.progressive_advance(2) == (2, 2)
+    g.set_option(ptamd.PT_OPT_GROUP_EXCHANGE, 0)
+    assert g.progressive_advance(1) == (4, 1)
+    ref, _ = O.render(v, i, n.reshape(-1), scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, W, H, n_batches=5)
+    _same(g.read_accum(), ref, "exchange 0 -> 1 -> 0 across advances")
+
+
+def _devices():
+    import torch
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif("_devices() < 2")
+@pytest.mark.parametrize("exchange", [0, 1])
+def test_group_on_distinct_devices(exchange):
+    """members on distinct GPUs -- peer stores into the
+    first device's frame over xGMI (after the context's own probe check) or
+    staged copies -- bitwise the single-GPU frame, through the progressive
+    loop and a readback.  Skipped on a one-GPU box (every box this build
+    had); the driver's multi-GPU node runs it."""
+    nd = min(_devices(), 4)
+    v, i, n = _box()
+    W, H = 160, 100
+    g = _setup(ptamd.Renderer(devices=list(range(nd))), v, i, n)
+    g.set_option(ptamd.PT_OPT_GROUP_EXCHANGE, exchange)
+    g.resize_and_clear(W, H)
+    assert g.progressive_camera(scenes.DEFAULT_CAMERA)
+    assert g.progressive_advance(3) == (0, 3)
+    t = g.readback_begin()
+    assert g.progressive_advance(2) == (3, 2)
+    snap = g.readback_end(t)
+    if exchange == 0:
+        assert g.group_check()[0] in (0, 1)   # the probe ran; 1 would mean staged copies took over
+    ref3, _ = O.render(v, i, n.reshape(-1), scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, W, H, n_batches=3)
+    _same(snap, ref3, f"{nd} devices, exchange {exchange}: snapshot after 3 batches")
+    ref5, _ = O.render(v, i, n.reshape(-1), scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, W, H, n_batches=5)
+    _same(g.read_accum(), ref5, f"{nd} devices, exchange {exchange}: 5 batches")

@@ -24,7 +24,9 @@ def _run(cmd, env, timeout=180):
     """subprocess.run with the children's stacks on a hang: bench.py dumps
     every thread's stack to stderr after PT_BENCH_TRACEBACK_AFTER_S, and a
     timeout reports the tail of what the children wrote."""
-    env = dict(env, PT_BENCH_TRACEBACK_AFTER_S=str(timeout - 30))
+    # a collective one rank never reaches fails after 90 s with the others'
+    # stacks (bench.py's process-group timeout), inside the test's own limit
+    env = dict(env, PT_BENCH_TRACEBACK_AFTER_S=str(timeout - 30), PT_BENCH_PG_TIMEOUT_S="90")
     try:
         return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     except subprocess.TimeoutExpired as e:
@@ -181,3 +183,22 @@ def test_native_loop_back_to_back_calls(streams):
         got = frames[f].cpu().numpy().reshape(-1).view(np.uint32)
         assert np.array_equal(got, want), f"frame buffer {f}"
     r.dist_finalize()
+
+
+def test_bench_group_leg_members_on_one_device():
+    """bench.py's pt_create_multi leg with two members
+    on device 0: both exchanges timed and each last frame bitwise the
+    one-GPU frame; the peer-store probe check is not armed on one device."""
+    env = dict(os.environ)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1", "--no-scene-legs",
+           "--no-cpu-baseline", "--group-devices", "0,0"]
+    res = _run(cmd, env)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
+    out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
+    g = out["group_leg"]
+    assert g["devices"] == [0, 0]
+    for k in ("exchange0", "exchange1"):
+        assert g[k]["verified_bitwise_vs_single_gpu"] is True, g
+        assert g[k]["ms_per_step"] > 0
+    assert g["exchange0"]["exchange"].startswith("peer stores")
+    assert g["exchange1"]["exchange"].startswith("staged")

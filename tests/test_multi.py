@@ -13,6 +13,7 @@ be the single-rank frame bit for bit.  A second test covers the reduce
 alternative: each rank's -0/+0 cleared share (partition_owned), SUM-reduced.
 This is the exchange bench.py runs over RCCL for N > 1."""
 import os
+import sys
 import socket
 
 import numpy as np
@@ -24,6 +25,8 @@ import torch.multiprocessing as mp
 import oracle_lib as O
 import ptamd
 import scenes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 W, H, SPP, SPL = 72, 40, 2, 4
 CAM = scenes.camera((3.0, 2.0, 4.0))   # the box off-centre: live and culled items on every rank
@@ -197,3 +200,37 @@ def test_rccl_standin_exports_the_entry_points_pt_dist_resolves():
     assert 'getenv("PT_RCCL_LIB")' in api
     uid = ctypes.create_string_buffer(128)
     assert lib.ncclGetUniqueId(uid) == 0 and uid.value.startswith(b"/ptshim-")
+
+
+def test_bench_spawns_ranks_without_a_launcher():
+    """`python bench.py --gpus 2` with no WORLD_SIZE starts
+    its two ranks itself (torch.distributed.run as a child process, never an
+    exec) and reaches the two-rank path; --dry-run stops before any GPU call."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"], cwd=ROOT,
+                         env=env, capture_output=True, text=True, timeout=180)
+    assert res.returncode == 0, res.stderr[-3000:]
+    out = json.loads([x for x in res.stdout.splitlines() if x.startswith("{")][-1])
+    assert out == {"dry_run": True, "n_gpus": 2, "ranks_seen": [0, 1], "launcher": "spawned",
+                   "backend_requested": "nccl"}
+
+
+def test_bench_stuck_rank_fails_fast():
+    """a rank that never reaches a collective (the shape
+    of the round-4 two-rank hang, killed after 180 s with nothing said) must
+    end the run with an error within the process-group timeout
+    (PT_BENCH_PG_TIMEOUT_S), naming where each rank was; it must not hold the
+    other ranks for gloo's / RCCL's default 30 minutes."""
+    import subprocess
+    import time as _t
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(PT_BENCH_DRY_STALL_RANK="1", PT_BENCH_PG_TIMEOUT_S="5")
+    t0 = _t.perf_counter()
+    res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"], cwd=ROOT,
+                         env=env, capture_output=True, text=True, timeout=120)
+    dt = _t.perf_counter() - t0
+    assert res.returncode != 0, res.stdout[-2000:]
+    assert dt < 90, dt
+    assert "imed out" in res.stderr or "Timeout" in res.stderr or "timeout" in res.stderr, res.stderr[-3000:]
