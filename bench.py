@@ -277,32 +277,75 @@ SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 12, "sphere_1080p8", 3),
               ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5, "synthetic10M_1080p8", 1))
 
 
-# Which measured gather ceiling bounds each leg's trace kernel
-# (tools/gather_roof.hip, dependent 64-B chains at 6 workgroups per CU,
-# profiles/r04/gather_roof.jsonl): the 2.6-MB wide tree of the displaced
-# sphere (configs 3, 4) is L2-resident; the 10M cloud's 313-MB 64-B tree is
-# not (its leg keeps the HBM roofline primary; the chase ceiling is beside
-# it).
+# Which measured gather ceiling bounds each leg's trace kernel: the 2.6-MB
+# wide tree of the displaced sphere (configs 3, 4) is L2-resident; the 10M
+# cloud's 313-MB tree is not (its leg keeps the fabric-bytes roofline primary,
+# the gather ceiling beside it).  The ceiling is the best rate of 64-B record
+# fetches (four 16-B loads per record per lane, the trace kernel's own access)
+# over every memory-level parallelism measured at the trace kernel's
+# occupancy -- 1, 2 or 4 dependent chains per lane, 2, 4 or 8 independent
+# records in flight per lane (tools/gather_roof.hip mlp) -- so no kernel
+# fetching such records at that occupancy can beat it (VERDICT r04 item 4:
+# the one-chain figure alone was beaten).
 GATHER_CASES = {"sphere_1080p8": ("l2_gather", "l2_4MB"), "sphere_4k16_d8": ("l2_gather", "l2_4MB"),
                 "synthetic10M_1080p8": ("hbm_gather", "hbm1GB")}
+GATHER_FILE = os.path.join("profiles", "r05", "gather_roof_mlp.jsonl")
 
 
-def gather_roofline(workload):
-    if workload not in GATHER_CASES:
-        return None
-    bound, case = GATHER_CASES[workload]
-    path = os.path.join(ROOT, "profiles", "r04", "gather_roof.jsonl")
+def gather_rows(case):
+    """The measured 64-B record gather rates of one table case, or []."""
     try:
-        rows = [json.loads(x) for x in open(path) if x.strip()]
+        rows = [json.loads(x) for x in open(os.path.join(ROOT, GATHER_FILE)) if x.strip().startswith("{")]
     except (OSError, ValueError):
+        return []
+    return [d for d in rows if d.get("case") == case and d.get("record_B") == 64]
+
+
+def _pattern(d):
+    return (f"chains{d['chains_per_lane']}" if d["pattern"] == "dependent_chains"
+            else f"independent{d['records_in_flight_per_lane']}")
+
+
+def gather_roofline(workload, prof=None):
+    """The fetch-rate ceiling of the wide walk's node fetches for a leg.
+    l2_gather (configs 3/4, a 2.6-MB tree): the best rate any measured
+    pattern reaches from an L2-resident table.  hbm_gather (config 5, a
+    313-MB tree whose upper levels stay in L2): with h the trace kernel's L2
+    hit fraction (TCC_HIT / (TCC_HIT + TCC_MISS), committed profile), a frame
+    of N fetches needs at least h N / R_L2 of L2 service and (1 - h) N /
+    R_miss of miss service, so its rate is at most min(R_L2 / h, R_miss /
+    (1 - h)) -- a ceiling even if both overlap perfectly (without h: R_L2)."""
+    base = workload[:-len("_refcam")] if workload.endswith("_refcam") else workload
+    if base not in GATHER_CASES:
         return None
-    for d in rows:
-        if d.get("pattern") == "dependent_chain" and d.get("case") == case and d.get("record_B") == 64:
-            return {"bound": bound, "Grec_per_s": d["Grec_per_s"],
-                    "basis": f"tools/gather_roof.hip: dependent chains of 64-B records over a {d['table_MB']}-MB "
-                             f"table, {d['blocks']} workgroups of 256 (6 per CU, the trace kernel's occupancy), one "
-                             f"load in flight per lane ({os.path.relpath(path, ROOT)})"}
-    return None
+    bound, case = GATHER_CASES[base]
+    l2 = gather_rows("l2_4MB")
+    if not l2:
+        return None
+    best_l2 = max(l2, key=lambda d: d["Grec_per_s"])
+    pats = {"l2_4MB": {_pattern(d): d["Grec_per_s"] for d in l2}}
+    if bound == "l2_gather":
+        return {"bound": bound, "Grec_per_s": best_l2["Grec_per_s"], "patterns": pats,
+                "basis": f"tools/gather_roof.hip mlp: the best of {len(l2)} access patterns of 64-B records (four "
+                         f"16-B loads each) from a {best_l2['table_MB']}-MB table at 6 workgroups of 256 per CU "
+                         f"({_pattern(best_l2)}; {GATHER_FILE})"}
+    miss = gather_rows(case)
+    if not miss:
+        return None
+    best_miss = max(miss, key=lambda d: d["Grec_per_s"])
+    pats[case] = {_pattern(d): d["Grec_per_s"] for d in miss}
+    h = None if prof is None else prof[1].get("trace_kernel_l2", {}).get("hit_fraction")
+    r_l2, r_miss = best_l2["Grec_per_s"], best_miss["Grec_per_s"]
+    if h is None:
+        ceil, how = r_l2, "no L2 hit fraction in the committed profile: the L2-resident ceiling"
+    else:
+        ceil = min(r_l2 / h if h > 0 else float("inf"), r_miss / (1.0 - h) if h < 1 else float("inf"))
+        how = (f"min(R_L2 / h, R_miss / (1 - h)) with h = {h:.3f} (the trace kernel's L2 hit fraction, "
+               f"{prof[0]}), R_L2 = {r_l2} ({_pattern(best_l2)}, 4-MB table), R_miss = {r_miss} "
+               f"({_pattern(best_miss)}, {best_miss['table_MB']}-MB table)")
+    return {"bound": bound, "Grec_per_s": round(ceil, 2), "patterns": pats, "l2_hit_fraction": h,
+            "basis": f"tools/gather_roof.hip mlp, 64-B records at 6 workgroups of 256 per CU: {how} "
+                     f"({GATHER_FILE})"}
 
 
 def trace_share(prof):
@@ -407,7 +450,7 @@ def price_leg(out, workload, traced, kernel_ms, alg, ref_rays):
     fetches against the measured gather ceiling (configs 3/4 primary, config
     5 beside HBM) and VALU issue."""
     prof = profiled_traffic(workload)
-    gather = gather_roofline(workload)
+    gather = gather_roofline(workload, prof)
     if gather is not None:
         # the wide walk's node fetches against the measured ceiling of
         # dependent 64-B gathers from a table of the tree's size at the trace
@@ -417,6 +460,7 @@ def price_leg(out, workload, traced, kernel_ms, alg, ref_rays):
         roof = {"bound": gather["bound"], "achieved": round(ach, 3), "peak": gather["Grec_per_s"],
                 "unit": "G wide-node fetches/s", "frac": round(ach / gather["Grec_per_s"], 4),
                 "node_visits_per_frame": int(visits), "peak_basis": gather["basis"],
+                "peak_patterns_Grec_per_s": gather.get("patterns"),
                 "time_basis": out["roofline"]["time_basis"] + "; every kernel of the frame"}
         share = trace_share(prof)
         if share is not None:
@@ -481,6 +525,9 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
         if ctxs:
             x.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
             x.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 0)
+        for kv in filter(None, os.environ.get("PT_BENCH_LEG_OPTS", "").split(",")):   # A/B of leg options
+            k, _, val = kv.partition("=")
+            x.set_option(int(k), int(val))
         x.resize_and_clear(W, H)
         ctxs.append(x)
     r = ctxs[0]
@@ -1007,7 +1054,7 @@ def main():
                     help="the process-group plumbing only (no GPU): every rank joins, rank 0 prints a line")
     ap.add_argument("--profile-run", action="store_true",
                     help="only the warmup and timed frames (no stats/counting passes, legs or CPU baseline): "
-                         "the command tools/gpu_*profile.sh runs under rocprofv3")
+                         "the command tools/profile_workload.sh runs under rocprofv3")
     args = ap.parse_args()
     W, H, SPP = args.width, args.height, args.spp
     if args.streams is None:

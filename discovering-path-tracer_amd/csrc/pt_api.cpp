@@ -331,6 +331,7 @@ struct pt_context {
   int opt_wide = 1;           // PT_OPT_WIDE
   int opt_wf_fuse = 1;        // PT_OPT_WF_FUSE
   int opt_wf_tail = -1;       // PT_OPT_WF_TAIL (-1 auto)
+  int opt_wf_grid = 100;      // PT_OPT_WF_GRID (percent of a full-occupancy traversal grid)
   int opt_wide_node = 64;     // PT_OPT_WIDE_NODE
   int n_nodes_full = 0;
   float4* d_tris = nullptr;
@@ -793,6 +794,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.wide_handback = 0;
   p.wf_fuse = 0;
   p.wf_tail = 0;
+  p.wf_grid = c->opt_wf_grid;
   p.wide_qn = 0;
   p.wide_leafbox = nullptr;
   p.nodes = c->stats_mode ? c->d_nodes_full : c->d_nodes;
@@ -1575,6 +1577,10 @@ int pt_set_option(pt_context* c, int key, int value) {
     case PT_OPT_WF_TAIL:
       if (value < -1) return fail(PT_ERR_INVALID, "PT_OPT_WF_TAIL takes -1 (auto) or a ray count >= 0");
       c->opt_wf_tail = value;
+      return PT_OK;
+    case PT_OPT_WF_GRID:
+      if (value < 1 || value > 100) return fail(PT_ERR_INVALID, "PT_OPT_WF_GRID takes 1 to 100 (percent)");
+      c->opt_wf_grid = value;
       return PT_OK;
     case PT_OPT_WF_STREAMS:
       if (value != 1 && value != 2) return fail(PT_ERR_INVALID, "PT_OPT_WF_STREAMS takes 1 or 2");

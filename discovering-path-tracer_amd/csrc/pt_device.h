@@ -90,6 +90,7 @@ struct RenderParams {
   int wide_handback;        // test: hand every odd list slot to the exact walk (PT_OPT_WIDE 2)
   int wf_fuse;              // PT_OPT_WF_FUSE: the wide trace kernel also walks a closest hit's first-light shadow ray
   int wf_tail;              // PT_OPT_WF_TAIL: a list of fewer rays than this is finished by wf_tail_kernel (0: never)
+  int wf_grid;              // PT_OPT_WF_GRID: the persistent traversal grid in percent of a full-occupancy grid (1-100)
   const float4* nodes;
   const float4* tris;
   const LightDev* lights;

@@ -86,6 +86,25 @@ struct Hit {
 static_assert(PT_WF_WAVEFLUSH || !PT_WF_SHADOW_QUEUE, "PT_WF_SHADOW_QUEUE needs PT_WF_WAVEFLUSH");
 constexpr int kCand = PT_KCAND;
 
+// The running mean's step (:467-469): (acc * b + c) / (b + 1).  PT_FOLD_FAST:
+// where b + 1 is a power of two the quotient is a product with its exact
+// reciprocal (bitwise the IEEE quotient: both round the same exact value),
+// and a running value of 1 folding a colour of 1 stays 1 ((b + 1) / (b + 1),
+// b + 1 < 2^24 exact) -- the alpha channel of every live pixel.
+#ifndef PT_FOLD_FAST
+#define PT_FOLD_FAST 1
+#endif
+// PT_FOLD_DIRECT: with one lane per pixel each lane folds its own sample
+// (no colour hand-off through LDS).  PT_SKIP_DEAD: the last SSS step's next
+// direction and the last bounce's direction, never traced, are not computed
+// (their draws still advance the stream).
+#ifndef PT_FOLD_DIRECT
+#define PT_FOLD_DIRECT 1   // box 1080p8, driver command: with PT_SKIP_DEAD and PT_FOLD_FAST 0.2131 -> 0.2114 ms (profiles/r05b/ab_box.log)
+#endif
+#ifndef PT_SKIP_DEAD
+#define PT_SKIP_DEAD 1
+#endif
+
 // PF (prefetch): load node k+1 while node k is being tested — it is the next
 // visit whenever k is a hit internal node or a leaf (the node arrays carry one
 // node of padding so k+1 is always readable).  It was worth 12 % on a
@@ -527,10 +546,19 @@ __device__ v3 path_trace(const RenderParams& P, v3 ro, v3 rd, uint32_t seed, Ctr
       }
       rad = add(rad, muls(mul(mul(thr, sss_thr), sl), 1.0f + sss_radius * 0.5f));
       sss_thr = mul(sss_thr, muls(sss_albedo, exp_(-travel / (sss_radius * 1.5f))));
-      so = sub(cp, muls(sn, OFFSET));
-      sd = sample_sphere(&rng);
+      // the last step's next direction (:406-407) is never traced: its two
+      // draws only advance the stream (the same state as sample_sphere's)
+      if (STATS || !PT_SKIP_DEAD || k + 1 < P.sss_bounces) {
+        so = sub(cp, muls(sn, OFFSET));
+        sd = sample_sphere(&rng);
+      } else {
+        rng_skip(&rng, 2);
+      }
     }
 
+    // the last bounce's direction (:411-414) is never traced and the stream
+    // is not read again: the path ends here
+    if (PT_SKIP_DEAD && !STATS && depth + 1 >= P.max_depth) break;
     const v3 bd = sample_hemisphere(hn, &rng);          // :411-414
     thr = mul(thr, muls(albedo, dot(hn, bd)));
     ro = add(hp, muls(hn, OFFSET));
@@ -794,6 +822,15 @@ __device__ __forceinline__ void unpack_block(const RenderParams& P, int block) {
   }
 }
 
+// One step of the running mean (:467-469); PT_FOLD_FAST above.
+__device__ __forceinline__ float fold_one(float a, float c, uint32_t batch) {
+  const float fb = (float)batch, fb1 = (float)(batch + 1u);
+  if (PT_FOLD_FAST && a == 1.0f && c == 1.0f && batch < (1u << 24)) return 1.0f;
+  const float x = a * fb + c;
+  if (PT_FOLD_FAST && ((batch + 1u) & batch) == 0u && batch + 1u != 0u) return x * (1.0f / fb1);
+  return x / fb1;
+}
+
 // LDS=true stages the whole scene (threaded nodes + triangle records) in LDS
 // once per workgroup; chosen by the host for scenes of at most a few tens of
 // KB (box.obj is 1.3 KB), where every lane re-reads the same few nodes.
@@ -953,6 +990,16 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
         col = path_trace_fused<PT_REC_PF != 0, CNT>(P, origin, dir, seed, cand, c);
       col4 = make_float4(col.x, col.y, col.z, 1.0f);                      // vec4(color, 1.0)
      }
+     if (PT_FOLD_DIRECT && spl == 1) {   // uniform: each lane folds its own sample, no hand-off (:467-469)
+      if (active && live) {
+        const uint32_t batch = P.first_batch + base;   // wave-uniform
+        acc[0] = fold_one(acc[0], col4.x, batch);
+        acc[1] = fold_one(acc[1], col4.y, batch);
+        acc[2] = fold_one(acc[2], col4.z, batch);
+        acc[3] = fold_one(acc[3], col4.w, batch);
+      }
+      continue;
+     }
      // hand the chunk's colours to the folding lanes of the same pixel
      colw[lane] = col4.x;
      colw[64 + lane] = col4.y;
@@ -965,12 +1012,11 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
       const uint32_t m = min((uint32_t)spl, P.n_batches - base);
       const int first_lane = lane - j;
       for (uint32_t t = 0; t < m; ++t) {
-        const uint32_t batch = P.first_batch + base + t;
-        const float fb = (float)batch, fb1 = (float)(batch + 1u);          // :468
+        const uint32_t batch = P.first_batch + base + t;                    // :468
         const float* cc = colw + first_lane + (int)t;
 #pragma unroll
         for (int ch = 0; ch < 4; ++ch)
-          if (ch % spl == j) acc[ch] = (acc[ch] * fb + cc[ch * 64]) / fb1;
+          if (ch % spl == j) acc[ch] = fold_one(acc[ch], cc[ch * 64], batch);
       }
      }
      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2752,6 +2798,10 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
   if (e != hipSuccess) return e;
   unsigned grid_t = (unsigned)(cus * (per_cu_t > 0 ? per_cu_t : 1));
   unsigned grid_x = (unsigned)(cus * (per_cu_x > 0 ? per_cu_x : 1));
+  // PT_OPT_WF_GRID: a smaller persistent grid gives each lane more rays per
+  // round (a shorter drain relative to the round) when other frames' launches
+  // fill the rest of the GPU
+  if (p0.wf_grid > 0 && p0.wf_grid < 100) grid_t = std::max(1u, (unsigned)((unsigned long long)grid_t * p0.wf_grid / 100));
   if (wide) {   // every lane needs its overflow stack area
     if (p0.wide_ovf_lanes < 256) return hipErrorInvalidValue;
     grid_t = std::min<unsigned>(grid_t, (unsigned)(p0.wide_ovf_lanes / 256));

@@ -263,6 +263,11 @@ PT_FN float radians_(float deg) { return deg * 0x1.1df46ap-6f; }
 // ----------------------------------------------------------------- RNG ------
 // raytrace_comp.comp:209-216 (PCG-style LCG + RXS-M-XS output).  The divisor
 // literal 4294967295.0 is a GLSL *float* literal, i.e. 2^32 exactly.
+// The state update of rng_next alone: n draws whose values are never used
+// (a direction the shader samples and never traces) still advance the stream.
+PT_FN void rng_skip(uint32_t* s, int n) {
+  for (int i = 0; i < n; ++i) *s = *s * 747796405u + 2891336453u;
+}
 PT_FN float rng_next(uint32_t* s) {
   *s = *s * 747796405u + 2891336453u;
   uint32_t result = ((*s >> ((*s >> 28u) + 4u)) ^ *s) * 277803737u;

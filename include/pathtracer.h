@@ -424,6 +424,11 @@ int pt_dist_finalize(pt_context* ctx);
  * render after every pt_resize_and_clear / pt_bind_accum, any devices; 3 =
  * as 2 with a mismatch forced (tests of the fallback); 0 = never. */
 #define PT_OPT_GROUP_CHECK 19
+/* PT_OPT_WF_GRID: wavefront traversal launches use this percentage (1-100,
+ * default 100) of a full-occupancy persistent grid; with frames in flight on
+ * several contexts a smaller grid gives each lane more rays per round.
+ * Output is identical. */
+#define PT_OPT_WF_GRID 20
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */

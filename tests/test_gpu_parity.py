@@ -1025,3 +1025,49 @@ def test_wide_walk_fused_shadow_rays(case, fuse):
     r.render(0, 1)
     r.render(1, 3)
     _assert_same(r.read_accum(), ref, f"fuse {fuse} {case}")
+
+
+@pytest.mark.parametrize("first,nb", [(0, 16), (3, 6), (7, 9), (1000, 3)])
+def test_one_lane_fold_over_stale_accumulator(first, nb):
+    """The one-lane-per-pixel fold (PT_OPT_SAMPLE_LANES 1: each lane folds its
+    own samples, no hand-off; batch + 1 a power of two divides by multiplying,
+    a running alpha of 1 stays 1) against the oracle's running mean (:467-469)
+    over an accumulator holding arbitrary values, alpha included, from batch
+    `first` on."""
+    v, i, n = _box()
+    W, H = 80, 56
+    rng = np.random.default_rng(first + nb)
+    stale = rng.uniform(-3.0, 3.0, W * H * 4).astype(np.float32)
+    stale[3::4][::3] = 1.0    # some pixels with alpha exactly 1
+    r = _setup(v, i, n)
+    r.set_option(ptamd.PT_OPT_SAMPLE_LANES, 1)
+    r.set_option(ptamd.PT_OPT_PRIMARY_CULL, 0)
+    import torch
+    buf = torch.from_numpy(stale.copy()).to("cuda:0")
+    r.bind_accum(buf.data_ptr(), W, H)
+    r.render(first, nb)
+    ref, _ = O.render(v, i, n.reshape(-1), scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, W, H, first_batch=first,
+                      n_batches=nb, accum=stale.copy())
+    _assert_same(r.read_accum(), ref, f"one-lane fold from batch {first}, {nb} batches")
+
+
+def test_wavefront_grid_fraction_is_output_invariant():
+    """PT_OPT_WF_GRID (a smaller persistent traversal grid) changes which lane
+    walks which ray, never a bit of the frame."""
+    sv, si = scenes.displaced_sphere(3)
+    s = ptamd.Scene.from_arrays(sv, si).build_bvh()
+    v, i, n, _, _ = s.arrays()
+    cam = scenes.camera((0.0, 0.5, 3.0))
+    frames = []
+    for g in (100, 37, 5):
+        r = _setup(v, i, n, cam=cam, lds=0)
+        r.set_option(ptamd.PT_OPT_KERNEL, ptamd.KERNEL_WAVEFRONT)
+        r.set_option(ptamd.PT_OPT_WF_GRID, g)
+        r.resize_and_clear(160, 96)
+        r.render(0, 3)
+        assert r.last_kernel() == ptamd.KERNEL_WAVEFRONT
+        frames.append(r.read_accum())
+    _assert_same(frames[1], frames[0], "grid 37 %")
+    _assert_same(frames[2], frames[0], "grid 5 %")
+    with pytest.raises(ptamd.PTError):
+        r.set_option(ptamd.PT_OPT_WF_GRID, 0)

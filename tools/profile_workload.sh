@@ -4,7 +4,7 @@
 # own (they cannot share one on gfx950), plus VALU/SALU instruction counts,
 # then tools/summarize_profile.py -> profiles/<TAG>/<WORKLOAD>_summary.json,
 # which bench.py prices its roofline from (matched by kernel SHA and workload).
-#   TAG=r02b WORKLOAD=box|sphere_1080p8|sphere_4k16_d8|synthetic10M_1080p8[_exhaustive] tools/profile_workload.sh
+#   TAG=r02b WORKLOAD=box|sphere_1080p8[_refcam]|sphere_4k16_d8[_refcam]|synthetic10M_1080p8[_exhaustive|_refcam] tools/profile_workload.sh
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -16,6 +16,10 @@ case $WORKLOAD in
   synthetic10M_1080p8) ARGS="--scene synthetic:10000000 --steps 1 --warmup 1"; STEPS=1; WARM=1 ;;
   synthetic10M_1080p8_exhaustive) ARGS="--scene synthetic:10000000 --steps 1 --warmup 1 --opt 12=0"; STEPS=1; WARM=1 ;;
   sphere_4k16_d8) ARGS="--scene sphere --width 3840 --height 2160 --spp 16 --depth 8 --steps 1 --warmup 1"; STEPS=1; WARM=1 ;;
+  # the legs' primary numbers: BASELINE's camera (0,0,5) (bench.py scene_leg)
+  sphere_1080p8_refcam) ARGS="--scene sphere --camera reference --steps 2 --warmup 1"; STEPS=2; WARM=1 ;;
+  sphere_4k16_d8_refcam) ARGS="--scene sphere --camera reference --width 3840 --height 2160 --spp 16 --depth 8 --steps 1 --warmup 1"; STEPS=1; WARM=1 ;;
+  synthetic10M_1080p8_refcam) ARGS="--scene synthetic:10000000 --camera reference --steps 1 --warmup 1"; STEPS=1; WARM=1 ;;
   *) echo "unknown WORKLOAD $WORKLOAD"; exit 2 ;;
 esac
 OUT=gpurun_out/prof_${TAG}_${WORKLOAD}
@@ -24,7 +28,7 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/t
   python3 bench.py $ARGS --profile-run > $OUT/bench_trace.log 2>&1 \
   || { echo "trace rc=$?"; tail -20 $OUT/bench_trace.log; exit 1; }
 grep '^{' $OUT/bench_trace.log | tail -1 | cut -c1-300
-for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES"; do
+for c in FETCH_SIZE WRITE_SIZE "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES" "TCC_HIT_sum TCC_MISS_sum"; do
   n=${c%% *}
   timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$n -o run -- \
     python3 bench.py $ARGS --profile-run > $OUT/bench_$n.log 2>&1 \

@@ -93,6 +93,22 @@ def main(tag, workload, frames):
         out["fetch_calibration"]["source"] = "profiles/r02/fetch_calibration.json (x2 holds for 128-B line requests)"
     if sq:
         out["sq_per_launch"] = sq
+    # L2 hits and misses of the traversal kernel alone (its node fetches, ray
+    # and triangle loads): the hit fraction the gather ceiling of a partly
+    # L2-resident tree is priced with (bench.py gather_roofline)
+    tpath = os.path.join(src, "pmc_TCC_HIT_sum", "run_counter_collection.csv")
+    if os.path.exists(tpath):
+        tcc = {}
+        for r in csv.DictReader(open(tpath)):
+            k = r["Kernel_Name"]
+            fam = "trace" if ("wf_trace_wide_kernel" in k or (box and BOX_KERNEL in k)) else None
+            if fam and r["Counter_Name"] in ("TCC_HIT_sum", "TCC_MISS_sum"):
+                tcc[r["Counter_Name"]] = tcc.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"]) / frames
+        if tcc.get("TCC_HIT_sum", 0.0) + tcc.get("TCC_MISS_sum", 0.0) > 0:
+            tot = tcc.get("TCC_HIT_sum", 0.0) + tcc.get("TCC_MISS_sum", 0.0)
+            out["trace_kernel_l2"] = {"hits_per_frame": tcc.get("TCC_HIT_sum", 0.0),
+                                      "misses_per_frame": tcc.get("TCC_MISS_sum", 0.0),
+                                      "hit_fraction": tcc.get("TCC_HIT_sum", 0.0) / tot}
     p = os.path.join(src, "bench_trace.log")
     if os.path.exists(p):
         lines = [l for l in open(p) if l.startswith("{")]
