@@ -265,16 +265,23 @@ def roofline_block(prof, time_ms, alg_bytes, kernel, kernel_ms, interval_ms, n_t
     return out
 
 
-# the BASELINE configs the default run reports beside the headline, one GPU
-# each: (key, scene, W, H, spp, MAX_DEPTH, timed frames, profile workload)
-# (key, scene, W, H, spp, MAX_DEPTH, timed frames, profile workload,
-# contexts): config 3's frames alternate between three contexts (a frame's
-# ray rounds run beside the others' drains: 43.7 -> 39.4 (two) -> 38.2 ms
-# per frame, tools/scene_streams.py); configs 4 and 5 gain nothing from it
-# (10M cloud: 117.2 / 116.6 / 119.1)
-SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 12, "sphere_1080p8", 3),
-              ("config4", "sphere", 3840, 2160, 16, 8, 3, "sphere_4k16_d8", 1),
-              ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5, "synthetic10M_1080p8", 1))
+# The BASELINE configs the default run reports beside the headline, one GPU
+# each: (key, scene, W, H, spp, MAX_DEPTH, timed frames, profile workload,
+# (contexts, grid %) at BASELINE's camera, (contexts, grid %) at the
+# frame-filling camera).  Frames alternate over that many contexts (own
+# stream, accumulation and wavefront buffers each), each context's
+# traversal launches on `grid` % of a full persistent grid (PT_OPT_WF_GRID):
+# with C contexts at 100/C % every frame's rounds run side by side with more
+# rays per lane, instead of each launch taking the whole GPU and leaving its
+# drain to the others.  Measured one variant per process (profiles/r05c,
+# profiles/r05d): config 3 at (0,0,5) 3 contexts 15.7 ms -> 4 at 25 % 13.4;
+# config 4 at (0,0,5) 1 context 141.5 -> 3 at 33 % 134.9 (2 at 100 % 136.5,
+# 2 at 50 % 152.7); config 5 at (0,0,5) 1 context 23.3 -> 3 at 33 % 17.9; at
+# the frame-filling cameras config 3 36.1 -> 35.2, config 5 keeps one context
+# (110.9; 2 at 50 %: 113) and so does config 4 (round 4: contexts +-0.2 %).
+SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 12, "sphere_1080p8", (4, 25), (4, 25)),
+              ("config4", "sphere", 3840, 2160, 16, 8, 3, "sphere_4k16_d8", (3, 33), (1, 100)),
+              ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5, "synthetic10M_1080p8", (3, 33), (1, 100)))
 
 
 # Which measured gather ceiling bounds each leg's trace kernel: the 2.6-MB
@@ -486,7 +493,8 @@ def price_leg(out, workload, traced, kernel_ms, alg, ref_rays):
                                 "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 f32 instruction"}
 
 
-def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaustive_too=False, contexts=1):
+def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaustive_too=False, contexts=1,
+              setup_ref=None, setup_ff=None):
     """One BASELINE config on one GPU (N = 1 only), at two cameras: BASELINE's
     (0,0,5) (Camera.cpp:7-9, Camera.h:34-36) leads -- its
     numbers are the leg's `value` and `roofline`, priced from the committed
@@ -497,14 +505,18 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
     exhaustive_too: one more frame at the frame-filling camera with
     PT_OPT_WIDE 0 -- the threaded exhaustive walk, the reference's own
     traversal shape -- reported as `exhaustive_walk` (workload +
-    "_exhaustive").  contexts > 1: the timed frames alternate between that
-    many contexts (own stream, accumulation and wavefront buffers each),
-    frames in flight; ms per frame is then the wall time of a run over its
-    frames, and the contexts' frames are checked bitwise equal."""
+    "_exhaustive").  setup_ref / setup_ff: (contexts, grid %) at each camera
+    (default (contexts, 100)); with more than one context the timed frames
+    alternate between them (own stream, accumulation and wavefront buffers
+    each), frames in flight; ms per frame is then the wall time of a run over
+    its frames, and the contexts' frames are checked bitwise equal."""
     import ptamd
     import scenes
     import torch
     t_setup = time.perf_counter()
+    setup_ref = setup_ref or (contexts, 100)
+    setup_ff = setup_ff or (contexts, 100)
+    contexts = max(setup_ref[0], setup_ff[0])
     scene, cam, int_bits, desc = load_scene(scene_name)
     v, i, n, _, _ = scene.arrays()
     del scene
@@ -516,9 +528,6 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
         x.upload_lights(scenes.REFERENCE_LIGHT)
         x.set_params(depth, sss)
         if contexts > 1:
-            # the other frames fill a frame's last ray rounds: the tail kernel
-            # (PT_OPT_WF_TAIL, for a frame alone) then costs more than it saves
-            x.set_option(ptamd.PT_OPT_WF_TAIL, 0)
             hs = HipStream(device)
             hip_streams.append(hs)
             x.set_stream(hs.handle)
@@ -536,22 +545,29 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
     setup_s = time.perf_counter() - t_setup
     base = desc.split(", camera")[0]
 
-    def measure(camera, cam_desc, wl):
-        for x in ctxs:
+    def measure(camera, cam_desc, wl, setup):
+        nctx, grid = setup
+        use = ctxs[:nctx]
+        for x in use:
             x.set_camera(camera)
+            x.set_option(ptamd.PT_OPT_WF_GRID, grid)
+            # with frames in flight the other frames fill a frame's last ray
+            # rounds: the tail kernel (PT_OPT_WF_TAIL, for a frame alone) then
+            # costs more than it saves
+            x.set_option(ptamd.PT_OPT_WF_TAIL, 0 if nctx > 1 else -1)
         t0 = time.perf_counter()
         r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 0)
         ref, traced = reference_and_traced_counts(r, spp)
         counts_s = time.perf_counter() - t0
         r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
-        for x in ctxs:
+        for x in use:
             x.render(0, spp)
         torch.cuda.synchronize()
-        if contexts > 1:
-            walls = time_frames_pipelined(ctxs, spp, steps)
+        if nctx > 1:
+            walls = time_frames_pipelined(use, spp, steps)
             kt = walls
             want = r.read_accum().view(np.uint32)
-            for x in ctxs[1:]:
+            for x in use[1:]:
                 if not np.array_equal(x.read_accum().view(np.uint32), want):
                     raise SystemExit(f"bench: {scene_name} leg: the pipelined contexts' frames differ")
         else:
@@ -570,16 +586,17 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
                "roofline": roofline_block(profiled_traffic(wl), kernel_ms, alg, kname, kernel_ms, kernel_ms,
                                           int(kt.size),
                                           f"median wall ms per frame of runs of {steps} frames alternating over "
-                                          f"{contexts} contexts (frames overlap)" if contexts > 1 else
+                                          f"{nctx} contexts (frames overlap)" if nctx > 1 else
                                           "median kernel_ms (HIP events around each frame's launches on the render "
                                           "stream)"),
-               "contexts": contexts, "counting_passes_s": round(counts_s, 2)}
+               "contexts": nctx, "wf_grid_percent": grid, "counting_passes_s": round(counts_s, 2)}
         price_leg(out, wl, traced, kernel_ms, alg, ref[0])
         return out, ref, alg
 
-    out, _, _ = measure(scenes.DEFAULT_CAMERA, "camera (0,0,5) fov 60 (BASELINE.md §3)", workload + "_refcam")
+    out, _, _ = measure(scenes.DEFAULT_CAMERA, "camera (0,0,5) fov 60 (BASELINE.md §3)", workload + "_refcam",
+                        setup_ref)
     out["setup_s"] = round(setup_s, 2)
-    ff, ref_ff, alg_ff = measure(cam, "camera" + desc.split(", camera")[1], workload)
+    ff, ref_ff, alg_ff = measure(cam, "camera" + desc.split(", camera")[1], workload, setup_ff)
     ff["note"] = "the scene's frame-filling camera (more pixels on geometry than BASELINE's (0,0,5))"
     if exhaustive_too:
         r.set_option(ptamd.PT_OPT_WIDE, 0)
@@ -615,7 +632,8 @@ DIST_SCENE_LEGS = (("config4", "sphere", 3840, 2160, 16, 8, 9),
                    ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 12))
 
 
-def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, depth, sss, steps, contexts=3):
+def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, depth, sss, steps, contexts=3,
+                   grid=33):
     """One multi-GPU BASELINE config at N = world: every rank renders its
     screen tiles (pt_set_partition) of the frame with the kernel the library
     picks for its share, then one RCCL SUM reduce of the accumulation buffer
@@ -663,6 +681,10 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
                 # kernel (1/8 sphere share, three contexts: 8.89 -> 7.37 ms per
                 # frame without it; 10M cloud 17.81 -> 17.62)
                 r.set_option(ptamd.PT_OPT_WF_TAIL, 0)
+            # each context's traversal on 1/C of the GPU (PT_OPT_WF_GRID):
+            # emulated 1/8 shares at (0,0,5), three contexts, 100 -> 33 %:
+            # config 4 23.7 -> 20.7 ms, config 5 5.07 -> 4.22 (profiles/r05d)
+            r.set_option(ptamd.PT_OPT_WF_GRID, grid)
             if ctxs:
                 r.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 0)
             frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
@@ -748,7 +770,7 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
         cfg = {"workload": f"{desc} {W}x{H} {spp}spp {depth} bounces {sss} sss", "triangles": int(ntri),
                "int_bits_nodes": bool(int_bits), "rays_per_frame": int(ref[0]),
                "parallelism": f"tiles{world}-reduce (RCCL SUM of the accumulation buffer to rank 0); "
-                              f"{len(ctxs)} frames in flight per rank"}
+                              f"{len(ctxs)} frames in flight per rank, traversal grid {grid} %"}
         add_traced(cfg, traced, dt)
         out = {"metric": "Mrays/s (reference-equivalent traceRay calls)", "value": round(ref[0] / dt / 1e6, 3),
                "unit": "Mrays/s", "n_gpus": world, "ms_per_step": round(dt * 1e3, 2), "steps": steps,
@@ -1699,10 +1721,11 @@ def main():
             for bs in box_streams:
                 bs.close()
             out_line["configs"] = {}
-            for key, scene_name, lw, lh, lspp, ldepth, steps, workload, nctx in SCENE_LEGS:
+            for key, scene_name, lw, lh, lspp, ldepth, steps, workload, s_ref, s_ff in SCENE_LEGS:
                 log(f"{key} leg ({scene_name} {lw}x{lh} {lspp}spp D{ldepth})")
                 out_line["configs"][key] = scene_leg(scene_name, lw, lh, lspp, ldepth, SSS, steps, device, workload,
-                                                     exhaustive_too=key == "config5", contexts=nctx)
+                                                     exhaustive_too=key == "config5", setup_ref=s_ref,
+                                                     setup_ff=s_ff)
         out_line["bench_wall_s"] = round(time.perf_counter() - T_START, 1)
         print(json.dumps(out_line), flush=True)
         if oracle_mismatch is not None:

@@ -276,3 +276,26 @@ def test_create_multi_argument_errors_without_a_gpu():
     rc = L.pt_create_multi(devs.ctypes.data, 2, ctypes.byref(out))
     assert rc < 0 and not out.value
     assert L.pt_last_error()
+
+
+def test_gather_ceilings_are_the_best_measured_patterns():
+    """the node-fetch rooflines price against the best
+    rate any measured access pattern reached (tools/gather_roof.hip mlp,
+    profiles/r05), and config 5's composed ceiling min(R_L2 / h, R_miss /
+    (1 - h)) is at least each resource's own rate."""
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    rows = [json.loads(x) for x in open(os.path.join(ROOT, bench.GATHER_FILE)) if x.startswith("{")]
+    l2 = max(d["Grec_per_s"] for d in rows if d["case"] == "l2_4MB")
+    hbm = max(d["Grec_per_s"] for d in rows if d["case"] == "hbm1GB")
+    for wl in ("sphere_1080p8", "sphere_4k16_d8_refcam"):
+        g = bench.gather_roofline(wl)
+        assert g["bound"] == "l2_gather" and g["Grec_per_s"] == l2
+    g = bench.gather_roofline("synthetic10M_1080p8_refcam")   # no profile: the loosest true ceiling
+    assert g["bound"] == "hbm_gather" and g["Grec_per_s"] == l2
+    for h in (0.1, 0.5, 0.9):
+        g = bench.gather_roofline("synthetic10M_1080p8", ("p", {"trace_kernel_l2": {"hit_fraction": h}}))
+        assert g["Grec_per_s"] >= hbm - 1e-6 and g["Grec_per_s"] >= min(l2, hbm / (1 - h)) - 1e-2
+        assert abs(g["Grec_per_s"] - min(l2 / h, hbm / (1 - h))) < 0.01

@@ -21,7 +21,10 @@ Both legs use the same context count, so the ratio full/share is the
 emulated N-GPU speed-up with the collective's local cost in.  Wall ms per
 frame over K frames, median of 3 runs.  Prints one JSON line per config.
 
-usage: r04_scene_emu.py {config3|config4|config5} [N=8] [C=3] [K]"""
+usage: r04_scene_emu.py {config3|config4|config5} [N=8] [C=3] [K]
+environment: CAM=reference (BASELINE's (0,0,5), the legs' camera since round 5)
+or scene (the frame-filling camera); GRID=percent (PT_OPT_WF_GRID of every
+context, default 100)."""
 import json
 import os
 import sys
@@ -52,6 +55,10 @@ def main():
         K = int(sys.argv[4])
     dev = torch.device("cuda", 0)
     scene, cam, int_bits, desc = bench.load_scene(scene_name)
+    if os.environ.get("CAM", "scene") == "reference":
+        cam = scenes.DEFAULT_CAMERA
+        desc = desc.split(", camera")[0] + ", camera (0,0,5) fov 60"
+    grid = int(os.environ.get("GRID", "100"))
     v, i, n, _, _ = scene.arrays()
     del scene
     comm = torch.cuda.Stream(dev, priority=-1)
@@ -65,6 +72,7 @@ def main():
         r.set_params(depth, 3)
         if C > 1:
             r.set_option(ptamd.PT_OPT_WF_TAIL, 0)   # as dist_scene_leg with frames in flight
+        r.set_option(ptamd.PT_OPT_WF_GRID, grid)
         hs = bench.HipStream(0)
         streams.append(hs)
         r.set_stream(hs.handle)
@@ -107,7 +115,7 @@ def main():
         ok = ok and np.array_equal(r.read_accum().view(np.uint32), ctxs[0][0].read_accum().view(np.uint32))
     f, s = float(np.median(full)), float(np.median(share))
     print(json.dumps({"config": key, "workload": f"{desc} {W}x{H} {spp}spp D{depth}", "emulated_ranks": N,
-                      "contexts": C, "frames_per_run": K, "reduce_standin_bytes": W * H * 16,
+                      "contexts": C, "wf_grid_percent": grid, "frames_per_run": K, "reduce_standin_bytes": W * H * 16,
                       "full_frame_ms": [round(x, 3) for x in full], "share_ms": [round(x, 3) for x in share],
                       "full_frame_ms_median": round(f, 3), "share_ms_median": round(s, 3),
                       "emulated_speedup": round(f / s, 3), "shares_bitwise_equal": ok,
