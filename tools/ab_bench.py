@@ -44,6 +44,8 @@ def main():
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     scene, cam = load_scene(a.scene)
+    if os.environ.get("CAM") == "reference":   # BASELINE's camera (0,0,5), the legs' primary
+        cam = scenes.DEFAULT_CAMERA
     rs = []
     for spec in a.variants:
         name, _, kv = spec.partition(":")
