@@ -332,6 +332,7 @@ struct pt_context {
   int opt_wf_fuse = 1;        // PT_OPT_WF_FUSE
   int opt_wf_tail = -1;       // PT_OPT_WF_TAIL (-1 auto)
   int opt_wf_grid = 100;      // PT_OPT_WF_GRID (percent of a full-occupancy traversal grid)
+  int opt_wf_refill = 0;      // PT_OPT_WF_REFILL (0 auto)
   int opt_wide_node = 64;     // PT_OPT_WIDE_NODE
   int n_nodes_full = 0;
   float4* d_tris = nullptr;
@@ -795,6 +796,10 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.wf_fuse = 0;
   p.wf_tail = 0;
   p.wf_grid = c->opt_wf_grid;
+  // PT_OPT_WF_REFILL auto: 16 idle lanes on a full grid, 8 on a split one
+  // (more rays per lane per round; the refill's cost is shared by fewer
+  // concurrent waves: profiles/r05i)
+  p.wide_refill = c->opt_wf_refill > 0 ? c->opt_wf_refill : (c->opt_wf_grid < 100 ? 8 : 16);
   p.wide_qn = 0;
   p.wide_leafbox = nullptr;
   p.nodes = c->stats_mode ? c->d_nodes_full : c->d_nodes;
@@ -1577,6 +1582,10 @@ int pt_set_option(pt_context* c, int key, int value) {
     case PT_OPT_WF_TAIL:
       if (value < -1) return fail(PT_ERR_INVALID, "PT_OPT_WF_TAIL takes -1 (auto) or a ray count >= 0");
       c->opt_wf_tail = value;
+      return PT_OK;
+    case PT_OPT_WF_REFILL:
+      if (value < 0 || value > 64) return fail(PT_ERR_INVALID, "PT_OPT_WF_REFILL takes 0 (auto) to 64 idle lanes");
+      c->opt_wf_refill = value;
       return PT_OK;
     case PT_OPT_WF_GRID:
       if (value < 1 || value > 100) return fail(PT_ERR_INVALID, "PT_OPT_WF_GRID takes 1 to 100 (percent)");

@@ -91,6 +91,7 @@ struct RenderParams {
   int wf_fuse;              // PT_OPT_WF_FUSE: the wide trace kernel also walks a closest hit's first-light shadow ray
   int wf_tail;              // PT_OPT_WF_TAIL: a list of fewer rays than this is finished by wf_tail_kernel (0: never)
   int wf_grid;              // PT_OPT_WF_GRID: the persistent traversal grid in percent of a full-occupancy grid (1-100)
+  int wide_refill;          // PT_OPT_WF_REFILL: idle lanes at which a wave of the wide trace kernel refills
   const float4* nodes;
   const float4* tris;
   const LightDev* lights;

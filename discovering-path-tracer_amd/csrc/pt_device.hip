@@ -1971,7 +1971,8 @@ __global__ __launch_bounds__(256, PT_WF_MIN_BLOCKS) void wf_trace_kernel(RenderP
 // list still held rays -- a lane could refill only once its whole aligned
 // group of four was idle.  G = 1 vs the earlier choice (2 below 500K
 // triangles, 4 above): sphere 78.0 -> 75.1 ms, 10M cloud 237 -> 206 ms;
-// the refill threshold is PT_WIDE_REFILL.
+// the refill threshold is P.wide_refill (PT_OPT_WF_REFILL; PT_WIDE_REFILL for
+// the tail kernel).
 #ifndef PT_WIDE_G
 #define PT_WIDE_G 1
 #endif
@@ -2210,7 +2211,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
     for (int sh = 1; sh < G; sh <<= 1) gm &= gm >> sh;
     gm &= group_lead<G>();
     const int ng = (int)__popcll(gm);
-    if (more && ng * G >= PT_WIDE_REFILL) {
+    if (more && ng * G >= P.wide_refill) {
       const int need = ng * G;
       int base = 0;
       if (lane == 0) base = atomicAdd(&B.counters[2], need);

@@ -37,6 +37,7 @@ PT_OPT_WF_TAIL = 17
 PT_OPT_GROUP_EXCHANGE = 18
 PT_OPT_GROUP_CHECK = 19
 PT_OPT_WF_GRID = 20
+PT_OPT_WF_REFILL = 21
 KERNEL_AUTO, KERNEL_RECURSIVE, KERNEL_WAVEFRONT = 0, 1, 3   # 2 (lane state machine) was removed
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).

@@ -429,6 +429,10 @@ int pt_dist_finalize(pt_context* ctx);
  * several contexts a smaller grid gives each lane more rays per round.
  * Output is identical. */
 #define PT_OPT_WF_GRID 20
+/* PT_OPT_WF_REFILL: idle lanes at which a wave of the wavefront's wide
+ * traversal kernel claims new rays; 0 (default) = auto: 16 with a full grid,
+ * 8 with PT_OPT_WF_GRID below 100.  Output is identical. */
+#define PT_OPT_WF_REFILL 21
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */

@@ -1052,22 +1052,27 @@ def test_one_lane_fold_over_stale_accumulator(first, nb):
 
 
 def test_wavefront_grid_fraction_is_output_invariant():
-    """PT_OPT_WF_GRID (a smaller persistent traversal grid) changes which lane
-    walks which ray, never a bit of the frame."""
+    """PT_OPT_WF_GRID (a smaller persistent traversal grid) and
+    PT_OPT_WF_REFILL (the idle-lane count at which a wave claims new rays)
+    change which lane walks which ray, never a bit of the frame."""
     sv, si = scenes.displaced_sphere(3)
     s = ptamd.Scene.from_arrays(sv, si).build_bvh()
     v, i, n, _, _ = s.arrays()
     cam = scenes.camera((0.0, 0.5, 3.0))
     frames = []
-    for g in (100, 37, 5):
+    cases = ((100, 0), (37, 0), (5, 0), (100, 1), (25, 4), (100, 64))   # (grid %, refill lanes; 0 auto)
+    for g, rf in cases:
         r = _setup(v, i, n, cam=cam, lds=0)
         r.set_option(ptamd.PT_OPT_KERNEL, ptamd.KERNEL_WAVEFRONT)
         r.set_option(ptamd.PT_OPT_WF_GRID, g)
+        r.set_option(ptamd.PT_OPT_WF_REFILL, rf)
         r.resize_and_clear(160, 96)
         r.render(0, 3)
         assert r.last_kernel() == ptamd.KERNEL_WAVEFRONT
         frames.append(r.read_accum())
-    _assert_same(frames[1], frames[0], "grid 37 %")
-    _assert_same(frames[2], frames[0], "grid 5 %")
+    for (g, rf), f in zip(cases[1:], frames[1:]):
+        _assert_same(f, frames[0], f"grid {g} %, refill at {rf} idle lanes")
     with pytest.raises(ptamd.PTError):
         r.set_option(ptamd.PT_OPT_WF_GRID, 0)
+    with pytest.raises(ptamd.PTError):
+        r.set_option(ptamd.PT_OPT_WF_REFILL, 65)
