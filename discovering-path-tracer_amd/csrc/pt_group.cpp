@@ -60,6 +60,7 @@ namespace {
 
 constexpr int kOptGroupExchange = 18;   // PT_OPT_GROUP_EXCHANGE (pathtracer.h)
 constexpr int kOptGroupCheck = 19;      // PT_OPT_GROUP_CHECK (pathtracer.h)
+constexpr int kOptCountTraced = 10;     // PT_OPT_COUNT_TRACED (pathtracer.h)
 
 }  // namespace
 
@@ -83,6 +84,8 @@ struct pt_group {
   bool check_passed = false;
   int check_state = -1;              // -1 not run, 0 peer stores matched, 1 mismatch: staged copies in force
   float check_ms[2] = {0.0f, 0.0f};  // the probe frames' wall time: peer stores, staged copies
+  bool stats_mode = false;           // the members' counters (stats mode, PT_OPT_COUNT_TRACED) are off
+  bool count_traced = false;         // during the probe frames and restored after
   float* frame = nullptr;            // W x H float4 on dev[0]
   bool own_frame = false;
   int W = 0, H = 0;
@@ -321,7 +324,15 @@ int check_exchange(pt_group* g) {
     gfree(g->dev[0], probe[0]);
     gfree(g->dev[0], probe[1]);
   };
+  // the probe frames are not the caller's frames: no stats or traced counts
+  auto counters = [&](bool on) -> int {
+    if (g->stats_mode) G_RC(each(g, [&](int r) { return pt_set_stats_mode(g->m[(size_t)r], on ? 1 : 0); }));
+    if (g->count_traced)
+      G_RC(each(g, [&](int r) { return pt_set_option(g->m[(size_t)r], kOptCountTraced, on ? 1 : 0); }));
+    return PT_OK;
+  };
   auto body = [&]() -> int {
+    G_RC(counters(false));
     G_RC(quiesce_all(g));
     G_HIP(hipSetDevice(g->dev[0]));
     for (float*& p : probe) {
@@ -361,8 +372,10 @@ int check_exchange(pt_group* g) {
     }
     return PT_OK;
   };
-  const int rc = body();
+  int rc = body();
   release();
+  const int rc2 = counters(true);
+  if (!rc) rc = rc2;
   if (rc) {
     const std::string msg = pt_last_error();
     (void)setup_frame(g, false);
@@ -598,13 +611,17 @@ int set_option(pt_group* g, int key, int value) {
     if (value == 0) g->check_pending = false;
     return PT_OK;
   }
-  return each(g, [&](int r) { return pt_set_option(g->m[(size_t)r], key, value); });
+  G_RC(each(g, [&](int r) { return pt_set_option(g->m[(size_t)r], key, value); }));
+  if (key == kOptCountTraced) g->count_traced = value != 0;
+  return PT_OK;
 }
 
 int last_kernel(pt_group* g, int* kernel) { return pt_last_kernel(g->m[0], kernel); }
 
 int set_stats_mode(pt_group* g, int enabled) {
-  return each(g, [&](int r) { return pt_set_stats_mode(g->m[(size_t)r], enabled); });
+  G_RC(each(g, [&](int r) { return pt_set_stats_mode(g->m[(size_t)r], enabled); }));
+  g->stats_mode = enabled != 0;
+  return PT_OK;
 }
 
 int get_stats(pt_group* g, pt_stats* out) {

@@ -222,3 +222,29 @@ def test_group_on_distinct_devices(exchange):
     _same(snap, ref3, f"{nd} devices, exchange {exchange}: snapshot after 3 batches")
     ref5, _ = O.render(v, i, n.reshape(-1), scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, W, H, n_batches=5)
     _same(g.read_accum(), ref5, f"{nd} devices, exchange {exchange}: 5 batches")
+
+
+def test_group_check_probe_frames_are_not_counted():
+    """The peer-store probe frames (PT_OPT_GROUP_CHECK) run with the members'
+    counters off: stats mode and traced counts after the checked render are
+    the single-GPU frame's."""
+    v, i, n = _box()
+    g = _setup(ptamd.Renderer(devices=[0, 0]), v, i, n)
+    one = _setup(ptamd.Renderer(0), v, i, n)
+    g.set_option(ptamd.PT_OPT_GROUP_CHECK, 2)
+    for r in (g, one):
+        r.resize_and_clear(64, 40)
+        r.set_stats_mode(True)
+        r.reset_stats()
+        r.render(0, 2)
+    assert g.group_check()[0] == 0
+    assert g.stats() == one.stats()
+    g.set_stats_mode(False)
+    one.set_stats_mode(False)
+    g.resize_and_clear(64, 40)   # re-arms the check
+    for r in (g, one):
+        r.set_option(ptamd.PT_OPT_COUNT_TRACED, 1)
+        r.reset_stats()
+        r.render(0, 2)
+    assert g.group_check()[0] == 0
+    assert g.traced() == one.traced()
