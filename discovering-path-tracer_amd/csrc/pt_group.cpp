@@ -376,9 +376,10 @@ int check_exchange(pt_group* g) {
   release();
   const int rc2 = counters(true);
   if (!rc) rc = rc2;
-  if (rc) {
+  if (rc) {   // e.g. no scene yet: the render fails, and the check runs again on the next one
     const std::string msg = pt_last_error();
     (void)setup_frame(g, false);
+    g->check_pending = true;
     return pt_fail_internal(rc, "pt_create_multi exchange check: " + msg);
   }
   if (g->check == 3) {
