@@ -248,3 +248,20 @@ def test_group_check_probe_frames_are_not_counted():
         r.render(0, 2)
     assert g.group_check()[0] == 0
     assert g.traced() == one.traced()
+
+
+def test_group_check_rearmed_after_a_failed_render():
+    """A render that fails before the probe can run (no scene yet) leaves the
+    peer-store check armed for the next render."""
+    v, i, n = _box()
+    g = ptamd.Renderer(devices=[0, 0])
+    g.set_option(ptamd.PT_OPT_GROUP_CHECK, 2)
+    g.resize_and_clear(48, 32)
+    with pytest.raises(ptamd.PTError):
+        g.render(0, 1)
+    assert g.group_check()[0] == -2
+    _setup(g, v, i, n)
+    g.render(0, 2)
+    assert g.group_check()[0] == 0
+    ref, _ = O.render(v, i, n.reshape(-1), scenes.DEFAULT_CAMERA, scenes.REFERENCE_LIGHT, 48, 32, n_batches=2)
+    _same(g.read_accum(), ref, "after a failed first render")
