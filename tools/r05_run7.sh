@@ -4,7 +4,7 @@
 # rocprofv3 kernel-trace stats of the driver's box command
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/r05f; mkdir -p $OUT
+OUT=gpurun_out/r05m; mkdir -p $OUT
 for k in 1 2; do
   timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench$k.log 2>&1 || { echo "bench $k rc=$?"; tail -5 $OUT/bench$k.log; exit 1; }
   grep '^{' $OUT/bench$k.log | cut -c1-300
