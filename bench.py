@@ -274,14 +274,17 @@ def roofline_block(prof, time_ms, alg_bytes, kernel, kernel_ms, interval_ms, n_t
 # with C contexts at 100/C % every frame's rounds run side by side with more
 # rays per lane, instead of each launch taking the whole GPU and leaving its
 # drain to the others.  Measured one variant per process (profiles/r05c,
-# profiles/r05d): config 3 at (0,0,5) 3 contexts 15.7 ms -> 4 at 25 % 13.4;
-# config 4 at (0,0,5) 1 context 141.5 -> 3 at 33 % 134.9 (2 at 100 % 136.5,
-# 2 at 50 % 152.7); config 5 at (0,0,5) 1 context 23.3 -> 3 at 33 % 17.9; at
-# the frame-filling cameras config 3 36.1 -> 35.2, config 5 keeps one context
-# (110.9; 2 at 50 %: 113) and so does config 4 (round 4: contexts +-0.2 %).
+# profiles/r05d, r05g, r05l; with the split grid's refill at 8 idle lanes):
+# config 3 at (0,0,5) 3 contexts 15.7 ms -> 4 at 25 % 13.2; config 4 at
+# (0,0,5) 1 context 141.5 -> 2 at 50 % 131.3 (3 at 33 % ~132-135, 4 at 25 %
+# 151); config 5 at (0,0,5) 1 context 23.3 -> 3 at 33 % 17.7.  At the
+# frame-filling cameras config 3 36.1 -> 34.7 (4 at 25 %), config 4 360.4 ->
+# 351.4 (2 at 50 %), config 5 111.1 -> 110.3 (2 at 100 %; 2 at 50 % 112.9).
+# Config 4 times runs of 6 frames: with 3 the runs were mostly the pipeline's
+# fill and drain.
 SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 12, "sphere_1080p8", (4, 25), (4, 25)),
-              ("config4", "sphere", 3840, 2160, 16, 8, 3, "sphere_4k16_d8", (3, 33), (1, 100)),
-              ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5, "synthetic10M_1080p8", (3, 33), (1, 100)))
+              ("config4", "sphere", 3840, 2160, 16, 8, 6, "sphere_4k16_d8", (2, 50), (2, 50)),
+              ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5, "synthetic10M_1080p8", (3, 33), (2, 100)))
 
 
 # Which measured gather ceiling bounds each leg's trace kernel: the 2.6-MB
