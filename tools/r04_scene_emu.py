@@ -24,7 +24,7 @@ frame over K frames, median of 3 runs.  Prints one JSON line per config.
 usage: r04_scene_emu.py {config3|config4|config5} [N=8] [C=3] [K]
 environment: CAM=reference (BASELINE's (0,0,5), the legs' camera since round 5)
 or scene (the frame-filling camera); GRID=percent (PT_OPT_WF_GRID of every
-context, default 100)."""
+context, default 100); TAIL=PT_OPT_WF_TAIL with C > 1 (default 0, -1 auto)."""
 import json
 import os
 import sys
@@ -71,7 +71,7 @@ def main():
         r.set_camera(cam)
         r.set_params(depth, 3)
         if C > 1:
-            r.set_option(ptamd.PT_OPT_WF_TAIL, 0)   # as dist_scene_leg with frames in flight
+            r.set_option(ptamd.PT_OPT_WF_TAIL, int(os.environ.get("TAIL", "0")))   # as dist_scene_leg with frames in flight
         r.set_option(ptamd.PT_OPT_WF_GRID, grid)
         hs = bench.HipStream(0)
         streams.append(hs)
@@ -115,7 +115,7 @@ def main():
         ok = ok and np.array_equal(r.read_accum().view(np.uint32), ctxs[0][0].read_accum().view(np.uint32))
     f, s = float(np.median(full)), float(np.median(share))
     print(json.dumps({"config": key, "workload": f"{desc} {W}x{H} {spp}spp D{depth}", "emulated_ranks": N,
-                      "contexts": C, "wf_grid_percent": grid, "frames_per_run": K, "reduce_standin_bytes": W * H * 16,
+                      "contexts": C, "wf_grid_percent": grid, "wf_tail": int(os.environ.get("TAIL", "0")), "frames_per_run": K, "reduce_standin_bytes": W * H * 16,
                       "full_frame_ms": [round(x, 3) for x in full], "share_ms": [round(x, 3) for x in share],
                       "full_frame_ms_median": round(f, 3), "share_ms_median": round(s, 3),
                       "emulated_speedup": round(f / s, 3), "shares_bitwise_equal": ok,

@@ -1,0 +1,13 @@
+#!/bin/bash
+# round-5 GPU call 13: emulated 1/8 shares at (0,0,5): tail kernel on/off and
+# 2 x 50 % against 3 x 33 %
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/r05o; mkdir -p $OUT
+for cfg in config5 config4; do
+  for v in "3 33 0" "3 33 -1" "2 50 0" "2 50 -1"; do
+    set -- $v
+    CAM=reference GRID=$2 TAIL=$3 timeout -k 10 300 python3 tools/r04_scene_emu.py $cfg 8 $1 > $OUT/emu.log 2>&1 || { echo "emu $cfg $v rc=$?"; tail -5 $OUT/emu.log; exit 1; }
+    grep '^{' $OUT/emu.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['config'], d['contexts'], d['wf_grid_percent'], d['wf_tail'], d['full_frame_ms_median'], d['share_ms_median'], d['emulated_speedup'], d['shares_bitwise_equal'])" | tee -a $OUT/shares.log
+  done
+done
