@@ -11,3 +11,8 @@ for cfg in config5 config4; do
     grep '^{' $OUT/emu.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['config'], d['contexts'], d['wf_grid_percent'], d['wf_tail'], d['full_frame_ms_median'], d['share_ms_median'], d['emulated_speedup'], d['shares_bitwise_equal'])" | tee -a $OUT/shares.log
   done
 done
+# the drop-in leg with members sharing this box's one GPU: both exchanges timed
+for d in 0,0 0,0,0,0,0,0,0,0; do
+  timeout -k 10 300 python3 bench.py --steps 20 --warmup 2 --no-scene-legs --no-cpu-baseline --group-devices $d > $OUT/group_$d.log 2>&1 || { echo "group $d rc=$?"; tail -5 $OUT/group_$d.log; exit 1; }
+  grep '^{' $OUT/group_$d.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], json.dumps(d['group_leg']))" | tee -a $OUT/group.log
+done
