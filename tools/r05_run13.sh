@@ -4,6 +4,8 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/r05o; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_group.py tests/test_gpu_parity.py -m gpu -x -q --timeout 240 --timeout-method thread > $OUT/pytest_group_parity.log 2>&1; rc=$?; tail -3 $OUT/pytest_group_parity.log
+[ $rc -ne 0 ] && [ $rc -ne 1 ] && exit $rc
 for cfg in config5 config4; do
   for v in "3 33 0" "3 33 -1" "2 50 0" "2 50 -1"; do
     set -- $v
