@@ -96,12 +96,14 @@ def load_scene(name):
     raise SystemExit(f"unknown scene {name}")
 
 
-KERNEL_SOURCES = ("pt_device.hip", "pt_device.h", "pt_isect.h", "wide_walk.h", "pt_math.h", "scene/wide_bvh.cpp")
+KERNEL_SOURCES = ("pt_device.hip", "pt_device.h", "pt_isect.h", "wide_walk.h", "pt_math.h", "scene/wide_bvh.cpp",
+                  "../Makefile")   # the Makefile: the device build flags
 
 
 def kernel_sha1():
-    """SHA-1 of the kernel source (pt_device.hip and the headers its kernels
-    are built from), as tools/summarize_profile.py records it."""
+    """SHA-1 of the kernel source (pt_device.hip, the headers its kernels
+    are built from and the Makefile that holds the device build flags), as
+    tools/summarize_profile.py records it."""
     import hashlib
     h = hashlib.sha1()
     for f in KERNEL_SOURCES:

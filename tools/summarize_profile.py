@@ -22,7 +22,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BOX_KERNEL = "render_kernel<false, true, false>"
-KERNEL_SOURCES = ("pt_device.hip", "pt_device.h", "pt_isect.h", "wide_walk.h", "pt_math.h", "scene/wide_bvh.cpp")   # == bench.py
+KERNEL_SOURCES = ("pt_device.hip", "pt_device.h", "pt_isect.h", "wide_walk.h", "pt_math.h", "scene/wide_bvh.cpp",
+                  "../Makefile")   # the Makefile: the device build flags   # == bench.py
 WF_KERNELS = ("wf_gen_kernel", "wf_trace_kernel", "wf_trace_wide_kernel", "wf_trace_pairs_kernel", "wf_tail_kernel", "wf_shade_kernel",
               "wf_fold_kernel", "fill_culled_kernel")
 
@@ -63,7 +64,7 @@ def main(tag, workload, frames):
     pmc.update(per_launch(os.path.join(src, "pmc_WRITE_SIZE", "run_counter_collection.csv"), ("WRITE_SIZE",)))
     sq = per_launch(os.path.join(src, "pmc_SQ_INSTS_VALU", "run_counter_collection.csv"),
                     ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES"))
-    # the kernel source: pt_device.hip and the headers its kernels are built from
+    # the kernel source: pt_device.hip, the headers its kernels are built from and the Makefile (build flags)
     h = hashlib.sha1()
     for name in KERNEL_SOURCES:
         h.update(open(os.path.join(ROOT, "discovering-path-tracer_amd", "csrc", name), "rb").read())
