@@ -283,10 +283,15 @@ def roofline_block(prof, time_ms, alg_bytes, kernel, kernel_ms, interval_ms, n_t
 # frame-filling cameras config 3 36.1 -> 34.7 (4 at 25 %), config 4 360.4 ->
 # 351.4 (2 at 50 %), config 5 111.1 -> 110.3 (2 at 100 %; 2 at 50 % 112.9).
 # Config 4 times runs of 6 frames: with 3 the runs were mostly the pipeline's
-# fill and drain.
+# fill and drain.  A run's frame count is a multiple of the contexts at both
+# cameras, so its last frames do not run on part of the grid alone: config 5
+# at (0,0,5) (3 x 33 %) measured 18.4 ms per frame in runs of 5 frames, 18.9
+# in runs of 10 and 17.4 in runs of 20 (profiles/r05w/frames.log); configs 3
+# and 4, whose runs already were such multiples, within 0.4 % at 2-4 times
+# the frames.
 SCENE_LEGS = (("config3", "sphere", 1920, 1080, 8, 4, 12, "sphere_1080p8", (4, 25), (4, 25)),
               ("config4", "sphere", 3840, 2160, 16, 8, 6, "sphere_4k16_d8", (2, 50), (2, 50)),
-              ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 5, "synthetic10M_1080p8", (3, 33), (2, 100)))
+              ("config5", "synthetic:10000000", 1920, 1080, 8, 4, 12, "synthetic10M_1080p8", (3, 33), (2, 100)))
 
 
 # Which measured gather ceiling bounds each leg's trace kernel: the 2.6-MB
