@@ -865,9 +865,12 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     // per step) and the 1/8 share 8 (0.062 vs 0.069).  Round 3's kernels,
     // the emulated root step on the native loop (DESIGN Appendix A, round-3 share options;
     // two runs each): 1/2 share spl 2/4 = 0.1175/0.1225 ms, 1/4 share 4/8 =
-    // 0.069/0.082, 1/8 share 4/8 = 0.046/0.042.
+    // 0.069/0.082, 1/8 share 4/8 = 0.046/0.042.  Round 5's kernels (the
+    // build without the SLP vectorizer, profiles/r05zc/spl.log, 200 frames):
+    // 1/2 share spl 1/2/4/8 = 0.1066/0.1067/0.118/0.1411 ms, 1/4 share
+    // 0.0811/0.0594/0.0603/0.0692, 1/8 share 0.0725/0.0465/0.0348/0.0374.
     const bool small = ptd::scene_lds_bytes(p) <= ptd::kMaxSceneLds;
-    int want = (c->nranks >= 8 || !small) ? 8 : (c->nranks == 2 || c->nranks == 3) ? 2 : 4;
+    int want = !small ? 8 : c->nranks >= 8 ? 4 : c->nranks >= 2 ? 2 : 4;
     while (want > 1 && (uint32_t)want > n_batches) want >>= 1;
     p.spl = want;
   }

@@ -318,8 +318,9 @@ int pt_dist_finalize(pt_context* ctx);
  * Output is identical either way. */
 #define PT_OPT_SCENE_IN_LDS 1
 /* PT_OPT_SAMPLE_LANES: lanes that trace one pixel's samples side by side in
- * pt_render — 0 auto (min(n_batches, 8) rounded down to 1/2/4/8), or 1, 2, 4, 8.
- * Output is identical for every value. */
+ * pt_render — 0 auto (scenes in device memory 8; LDS-resident scenes 4 on a
+ * whole frame or a partition of 8 or more ranks, 2 on 2-7 ranks; never more
+ * lanes than samples), or 1, 2, 4, 8.  Output is identical for every value. */
 #define PT_OPT_SAMPLE_LANES 2
 /* PT_OPT_FRESH_BATCH0: 1 = a launch whose first batch is 0 starts from a
  * cleared (+0) accumulator without reading it — bitwise what
