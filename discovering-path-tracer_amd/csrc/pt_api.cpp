@@ -376,6 +376,7 @@ struct pt_context {
   int* d_items = nullptr;
   size_t items_cap = 0;
   int n_live_items = 0, n_culled_items = 0;
+  size_t culled_org_off = 0;   // h_items / d_items: where the culled items' first pixels start
   std::vector<int> h_items;
   std::vector<float> items_key;
   ptd::RenderParams last{};     // configuration of the last pt_render
@@ -385,7 +386,7 @@ struct pt_context {
   size_t pack_cap = 0;
   int n_pack_items = 0;
   std::vector<float> pack_key;
-  int* d_unpack = nullptr;      // per entry: rank, item, slot (-1 = culled)
+  int* d_unpack = nullptr;      // per entry: rank, x0, y0, slot (-1 = culled)
   size_t unpack_cap = 0;
   int n_unpack = 0;
   std::vector<float> unpack_key;
@@ -634,8 +635,19 @@ static int compact_items(pt_context* c, ptd::RenderParams* p) {
     std::vector<int> live, culled;
     item_lists(*p, pt, &live, &culled);
     { const int rc_ = quiesce(c); if (rc_) return rc_; }   // the previous list may still be in use
+    // live items, culled items, then (8-B aligned) each culled item's first
+    // pixel {x, y} for the fill (fill_culled: no tile arithmetic per pixel)
     c->h_items = live;
     c->h_items.insert(c->h_items.end(), culled.begin(), culled.end());
+    if (c->h_items.size() & 1) c->h_items.push_back(0);
+    c->culled_org_off = c->h_items.size();
+    const int rows = 16 / p->spl;
+    for (int it : culled) {
+      int bx, by;
+      ptd::tile_block(ptd::part_tile(pt, it / p->spl), p->blocks_x, &bx, &by);
+      c->h_items.push_back(bx * 16);
+      c->h_items.push_back(by * 16 + (it % p->spl) * rows);
+    }
     if (c->h_items.size() > c->items_cap) {
       dev_free(c->d_items);
       c->items_cap = 0;
@@ -650,7 +662,7 @@ static int compact_items(pt_context* c, ptd::RenderParams* p) {
   }
   p->items = c->d_items;
   p->n_items = c->n_live_items;
-  p->culled_items = c->d_items + c->n_live_items;
+  p->culled_org = (const int2*)(c->d_items + c->culled_org_off);
   p->n_culled_items = c->n_culled_items;
   return PT_OK;
 }
@@ -684,22 +696,27 @@ constexpr long long kWfMaxPaths = 1ll << 27;
 constexpr int kWfAutoTris = 32768;
 constexpr int kWfWideAutoTris = 16384;   // ... with the culled wide walk (render_impl)
 // The root's assembly table for frames rendered with params p: per rank its
-// live items {rank, tile*8 + part, slot} and its culled items {rank, tile*8 + part, -1}.
+// live items {rank, x0, y0, slot} and its culled items {rank, x0, y0, -1},
+// (x0, y0) the item's first pixel.
 int unpack_table(pt_context* c, const ptd::RenderParams& p, const std::vector<float>& key) {
   if (key == c->unpack_key) return PT_OK;
   std::vector<int> table, live, culled;
   for (int r = 0; r < p.nranks; ++r) {
     const ptd::Part pt = part_of(c, r);
     item_lists(p, pt, &live, &culled);
-    // {rank, tile*8 + part, slot}: tile and part of the item (unpack_pixel)
-    auto tp = [&](int item) { return ptd::part_tile(pt, item / p.spl) * 8 + item % p.spl; };
-    for (size_t i = 0; i < live.size(); ++i) table.insert(table.end(), {r, tp(live[i]), (int)i});
-    for (int it : culled) table.insert(table.end(), {r, tp(it), -1});
+    // {rank, x0, y0, slot} (unpack_pixel)
+    auto add = [&](int item, int slot) {
+      int bx, by;
+      ptd::tile_block(ptd::part_tile(pt, item / p.spl), p.blocks_x, &bx, &by);
+      table.insert(table.end(), {r, bx * 16, by * 16 + (item % p.spl) * (16 / p.spl), slot});
+    };
+    for (size_t i = 0; i < live.size(); ++i) add(live[i], (int)i);
+    for (int it : culled) add(it, -1);
   }
   { const int rc_ = quiesce(c); if (rc_) return rc_; }
   const int rc = upload_ints(table, &c->d_unpack, &c->unpack_cap);
   if (rc) return rc;
-  c->n_unpack = (int)(table.size() / 3);
+  c->n_unpack = (int)(table.size() / 4);
   c->unpack_key = key;
   return PT_OK;
 }
@@ -904,7 +921,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   const bool cnt = c->opt_count != 0 && !c->stats_mode;
   p.n_cull = -1;
   p.items = nullptr;
-  p.culled_items = nullptr;
+  p.culled_org = nullptr;
   p.n_items = p.n_culled_items = 0;
   if (c->opt_cull && !c->stats_mode)
     p.n_cull = cull_rects(c->cam, c->width, c->height, c->root_lo, c->root_hi, c->lights_host.data(),

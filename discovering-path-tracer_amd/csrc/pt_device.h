@@ -124,7 +124,7 @@ struct RenderParams {
   // spl + part) that may hold a live pixel, and those that cannot
   const int* items;             // null = every item, blockIdx.x = item
   int n_items;
-  const int* culled_items;
+  const int2* culled_org;       // per culled item: its first pixel {x, y} (host-computed)
   int n_culled_items;
   int n_cull;
   float cull[8][4];
@@ -133,7 +133,8 @@ struct RenderParams {
   // culled-item fill runs; null = normal rendering
   float4* pack_out;
   // ... and, optionally, trailing workgroups that assemble a gathered frame
-  // (the pt_items_unpack_all work: table entries {rank, item, slot} over
+  // (the pt_items_unpack_all work: int4 table entries {rank, x0, y0, slot}
+  // -- the item's first pixel, its slot or -1 for a culled item -- over
   // per-rank slots of unpack_slot_f4 float4s) in the same launch
   const float4* unpack_src;
   float4* unpack_frame;

@@ -758,24 +758,27 @@ __device__ __forceinline__ void emit_lane(const RenderParams& P, bool active, si
     store_lane(P.accum + pix, acc, spl, j);
 }
 
-// Items (tile parts) whose every pixel is culled, listed by the host: each
-// thread folds the constant colour (0,0,0,1) into one pixel's running mean,
-// closed form where exact (fold_constant) — kPixPerFill pixels per thread.
-// Runs as the trailing workgroups of the render launch, so it overlaps the
-// render tail instead of costing a launch of its own.
+// Items (tile parts) whose every pixel is culled, listed by the host with
+// their first pixel: each thread folds the constant colour (0,0,0,1) into one
+// pixel's running mean, closed form where exact (fold_constant) — kPixPerFill
+// pixels per thread.  Runs as the trailing workgroups of the render launch,
+// so it overlaps the render tail instead of costing a launch of its own.
+// An item is 256 / spl pixels (a power of two), so a pixel's item and place
+// in it are a shift and a mask: the per-pixel tile arithmetic (a 64-bit
+// division, the partition's and the rotated tile order's) cost more than the
+// fill itself -- box 1080p8, 70 % of the pixels culled: see DESIGN A.4.
 constexpr int kPixPerFill = 8;
-__device__ __forceinline__ void fill_culled(const RenderParams& P, const int* __restrict__ items, int n, int block) {
-  const int spl = P.spl, per_item = 256 / spl;
-  const long long total = (long long)n * per_item;
+__device__ __forceinline__ int item_shift(int spl) { return 8 - __builtin_ctz((unsigned)spl); }   // log2(256 / spl)
+__device__ __forceinline__ void fill_culled(const RenderParams& P, const int2* __restrict__ org, int n, int block) {
+  const int lg = item_shift(P.spl);
+  const long long total = (long long)n << lg;
   for (int k = 0; k < kPixPerFill; ++k) {
     const long long g = ((long long)block * kPixPerFill + k) * 256 + threadIdx.x;
     if (g >= total) return;
-    const int item = items[g / per_item], q = (int)(g % per_item);
-    const int tile = rank_tile(P, item / spl), part = item % spl;
-    int bx, by;
-    tile_block(tile, P.blocks_x, &bx, &by);
-    const int px = bx * 16 + q % 16;
-    const int py = by * 16 + part * (16 / spl) + q / 16;
+    const int2 o = org[g >> lg];
+    const int q = (int)g & ((1 << lg) - 1);
+    const int px = o.x + (q & 15);
+    const int py = o.y + (q >> 4);
     if (px >= P.width || py >= P.height) continue;
     float4* dst = P.accum + (size_t)py * (size_t)P.width + (size_t)px;
     float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -801,16 +804,19 @@ __device__ __forceinline__ bool tile_pixel(const RenderParams& P, int tile, int 
 
 // One pixel-slot g of the gathered-frame assembly (items_unpack_kernel, and
 // the trailing workgroups of a pt_render_packed launch): a live item's pixel
-// from its rank's slot, a culled item's pixel as (0,0,0,1).
+// from its rank's slot, a culled item's pixel as (0,0,0,1).  Table entries
+// are {rank, x0, y0, slot}: the item's first pixel comes from the host, so
+// a pixel costs a shift and a mask (fill_culled).
 __device__ __forceinline__ void unpack_pixel(const RenderParams& P, float4* __restrict__ frame,
                                              const float4* __restrict__ src, size_t slot_f4,
                                              const int* __restrict__ table, long long g) {
-  const int per = 256 / P.spl;
-  const int* e = table + 3 * (g / per);
-  const int q = (int)(g % per);
-  size_t pix;
-  if (!tile_pixel(P, e[1] >> 3, e[1] & 7, q, &pix)) return;   // e = {rank, tile*8 + part, slot}
-  frame[pix] = e[2] >= 0 ? src[(size_t)e[0] * slot_f4 + (size_t)e[2] * per + q] : make_float4(0.0f, 0.0f, 0.0f, 1.0f);
+  const int lg = item_shift(P.spl);
+  const int4 e = ((const int4*)table)[g >> lg];
+  const int q = (int)g & ((1 << lg) - 1);
+  const int px = e.y + (q & 15), py = e.z + (q >> 4);
+  if (px >= P.width || py >= P.height) return;
+  frame[(size_t)py * (size_t)P.width + (size_t)px] =
+      e.w >= 0 ? src[(size_t)e.x * slot_f4 + ((size_t)e.w << lg) + q] : make_float4(0.0f, 0.0f, 0.0f, 1.0f);
 }
 
 __device__ __forceinline__ void unpack_block(const RenderParams& P, int block) {
@@ -856,7 +862,7 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
     if (P.pack_out)
       unpack_block(P, (int)blockIdx.x - P.n_items);   // assemble the previous gathered frame
     else
-      fill_culled(P, P.culled_items, P.n_culled_items, (int)blockIdx.x - P.n_items);
+      fill_culled(P, P.culled_org, P.n_culled_items, (int)blockIdx.x - P.n_items);
     return;
   }
   const int spl = P.spl;
@@ -2637,7 +2643,7 @@ __global__ __launch_bounds__(256) void wf_fold_kernel(RenderParams P, WfBuffers 
 }
 
 __global__ __launch_bounds__(256) void fill_culled_kernel(RenderParams P) {
-  fill_culled(P, P.culled_items, P.n_culled_items, (int)blockIdx.x);
+  fill_culled(P, P.culled_org, P.n_culled_items, (int)blockIdx.x);
 }
 
 }  // namespace
