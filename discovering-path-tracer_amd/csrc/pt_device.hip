@@ -767,7 +767,10 @@ __device__ __forceinline__ void emit_lane(const RenderParams& P, bool active, si
 // in it are a shift and a mask: the per-pixel tile arithmetic (a 64-bit
 // division, the partition's and the rotated tile order's) cost more than the
 // fill itself -- box 1080p8, 70 % of the pixels culled: see DESIGN A.4.
-constexpr int kPixPerFill = 8;
+#ifndef PT_PIX_PER_FILL
+#define PT_PIX_PER_FILL 8
+#endif
+constexpr int kPixPerFill = PT_PIX_PER_FILL;
 __device__ __forceinline__ int item_shift(int spl) { return 8 - __builtin_ctz((unsigned)spl); }   // log2(256 / spl)
 __device__ __forceinline__ void fill_culled(const RenderParams& P, const int2* __restrict__ org, int n, int block) {
   const int lg = item_shift(P.spl);
