@@ -377,6 +377,7 @@ struct pt_context {
   size_t items_cap = 0;
   int n_live_items = 0, n_culled_items = 0;
   size_t culled_org_off = 0;   // h_items / d_items: where the culled items' first pixels start
+  size_t live_org_off = 0;     // ... and the live items' ones
   std::vector<int> h_items;
   std::vector<float> items_key;
   ptd::RenderParams last{};     // configuration of the last pt_render
@@ -640,14 +641,19 @@ static int compact_items(pt_context* c, ptd::RenderParams* p) {
     c->h_items = live;
     c->h_items.insert(c->h_items.end(), culled.begin(), culled.end());
     if (c->h_items.size() & 1) c->h_items.push_back(0);
-    c->culled_org_off = c->h_items.size();
     const int rows = 16 / p->spl;
-    for (int it : culled) {
-      int bx, by;
-      ptd::tile_block(ptd::part_tile(pt, it / p->spl), p->blocks_x, &bx, &by);
-      c->h_items.push_back(bx * 16);
-      c->h_items.push_back(by * 16 + (it % p->spl) * rows);
-    }
+    auto origins = [&](const std::vector<int>& list) {
+      for (int it : list) {
+        int bx, by;
+        ptd::tile_block(ptd::part_tile(pt, it / p->spl), p->blocks_x, &bx, &by);
+        c->h_items.push_back(bx * 16);
+        c->h_items.push_back(by * 16 + (it % p->spl) * rows);
+      }
+    };
+    c->culled_org_off = c->h_items.size();
+    origins(culled);
+    c->live_org_off = c->h_items.size();
+    origins(live);
     if (c->h_items.size() > c->items_cap) {
       dev_free(c->d_items);
       c->items_cap = 0;
@@ -663,6 +669,7 @@ static int compact_items(pt_context* c, ptd::RenderParams* p) {
   p->items = c->d_items;
   p->n_items = c->n_live_items;
   p->culled_org = (const int2*)(c->d_items + c->culled_org_off);
+  p->items_org = (const int2*)(c->d_items + c->live_org_off);
   p->n_culled_items = c->n_culled_items;
   return PT_OK;
 }
@@ -922,6 +929,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.n_cull = -1;
   p.items = nullptr;
   p.culled_org = nullptr;
+  p.items_org = nullptr;
   p.n_items = p.n_culled_items = 0;
   if (c->opt_cull && !c->stats_mode)
     p.n_cull = cull_rects(c->cam, c->width, c->height, c->root_lo, c->root_hi, c->lights_host.data(),

@@ -123,6 +123,7 @@ struct RenderParams {
   // compact launch (host-built when culling applies): items (owned tile *
   // spl + part) that may hold a live pixel, and those that cannot
   const int* items;             // null = every item, blockIdx.x = item
+  const int2* items_org;        // with items: per live item its first pixel {x, y} (host-computed)
   int n_items;
   const int2* culled_org;       // per culled item: its first pixel {x, y} (host-computed)
   int n_culled_items;

@@ -871,9 +871,6 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
   const int spl = P.spl;
   // item = (owned tile, part); with culling the host launches only items that
   // can hold a live pixel, listed in P.items
-  const int item = P.items ? P.items[blockIdx.x] : (int)blockIdx.x;
-  const int tile = rank_tile(P, item / spl);
-  const int part = item % spl;
   const int wave = tid >> 6, lane = tid & 63;
   // per wave: the leaf-candidate queue, then a [slot][lane] area that holds
   // the path state parked during walks (kPark floats) and, between samples,
@@ -883,11 +880,26 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
   float* colw = (float*)&cand_buf[wave][kCand][0];   // colour hand-off, [channel][lane]
   const int q = wave * (64 / spl) + lane / spl;       // pixel within the workgroup
   const int j = lane % spl;                           // sample slot
-  int bx, by;
-  tile_block(tile, P.blocks_x, &bx, &by);
-  const int px = bx * 16 + q % 16;
-  const int py = by * 16 + part * (16 / spl) + q / 16;
-  const bool active = tile < P.blocks_total && px < P.width && py < P.height;   // :425-428
+  // the item's first pixel: host-computed with the item list (items_org),
+  // else from the tile order (every owned item, blockIdx.x = item)
+  int gx0, gy0;
+  bool tile_ok = true;
+  if (P.items_org) {
+    const int2 o = P.items_org[blockIdx.x];
+    gx0 = o.x;
+    gy0 = o.y;
+  } else {
+    const int item = (int)blockIdx.x;
+    const int tile = rank_tile(P, item / spl);
+    int bx, by;
+    tile_block(tile, P.blocks_x, &bx, &by);
+    gx0 = bx * 16;
+    gy0 = by * 16 + (item % spl) * (16 / spl);
+    tile_ok = tile < P.blocks_total;
+  }
+  const int px = gx0 + q % 16;
+  const int py = gy0 + q / 16;
+  const bool active = tile_ok && px < P.width && py < P.height;   // :425-428
   Ctr c = {0u, 0u, 0u, 0u, 0u};
   const int W = P.width, H = P.height;
   // Per-pixel constants of main() (:430-432, :446-447, :457), hoisted out of
@@ -901,7 +913,6 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
   bool live = true;
   bool wg_live = true;
   if (P.n_cull >= 0) {
-    const int gx0 = bx * 16, gy0 = by * 16 + part * (16 / spl);
     const float wx0 = (2.0f * (float)gx0 / (float)W) - 1.0f, wx1 = (2.0f * (float)(gx0 + 15) / (float)W) - 1.0f;
     const float wy0 = (2.0f * (float)gy0 / (float)H) - 1.0f;
     const float wy1 = (2.0f * (float)(gy0 + 16 / spl - 1) / (float)H) - 1.0f;
