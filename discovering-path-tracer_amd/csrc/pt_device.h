@@ -156,8 +156,8 @@ hipError_t launch_tiles(bool pack, float4* frame, float4* packed, int width, int
                         hipStream_t stream);
 hipError_t launch_clear(float4* accum, int width, int height, const Part& part, const int* d_pos, hipStream_t stream);
 // live-item exchange: pack this rank's listed items (256/spl pixels each) of
-// frame densely; unpack entries {rank, item, slot} from per-rank slots of
-// slot_f4 float4s into frame, slot -1 = culled item -> (0,0,0,1)
+// frame densely; unpack int4 entries {rank, x0, y0, slot} from per-rank slots
+// of slot_f4 float4s into frame, slot -1 = culled item -> (0,0,0,1)
 hipError_t launch_items_pack(const RenderParams& p, const float4* frame, float4* packed, const int* items, int n,
                              hipStream_t stream);
 hipError_t launch_items_unpack(const RenderParams& p, float4* frame, const float4* src, size_t slot_f4,
