@@ -579,12 +579,30 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
         if nctx > 1:
             walls = time_frames_pipelined(use, spp, steps)
             kt = walls
-            want = r.read_accum().view(np.uint32)
+            want = r.read_accum().view(np.uint32).copy()
             for x in use[1:]:
                 if not np.array_equal(x.read_accum().view(np.uint32), want):
                     raise SystemExit(f"bench: {scene_name} leg: the pipelined contexts' frames differ")
         else:
             walls, kt = time_frames(r, spp, steps)
+            want = r.read_accum().view(np.uint32).copy()
+        # The timed frame against the same frame through the exhaustive
+        # threaded walk (PT_OPT_WIDE 0: every box a ray passes, in the
+        # reference's visit order, raytrace_comp.comp:159-204), bit for bit;
+        # the GPU tests pin that walk to the oracle's rows (test_gpu_configs).
+        for x in use[1:]:
+            x.synchronize()
+        r.set_option(ptamd.PT_OPT_WIDE, 0)
+        r.reset_launch_times()
+        t_ex = time.perf_counter()
+        r.render(0, spp)
+        r.synchronize()
+        ex_s = time.perf_counter() - t_ex
+        ex_kt = r.launch_times_ms()
+        r.set_option(ptamd.PT_OPT_WIDE, 1)
+        ex_bad = int(np.count_nonzero(r.read_accum().view(np.uint32) != want))
+        exhaustive = {"ms": ex_s * 1e3, "kernel_ms": float(np.sum(ex_kt)) if ex_kt.size else float("nan"),
+                      "launches": int(ex_kt.size), "mismatched_floats": ex_bad}
         dt = float(np.median(walls)) * 1e-3   # the median frame (min/max beside it)
         kernel_ms = float(np.median(kt)) if kt.size else float("nan")
         alg = algorithmic_bytes({"nodes": ref[1], "leaf_tests": ref[2], "samples": ref[3]})
@@ -602,32 +620,36 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
                                           f"{nctx} contexts (frames overlap)" if nctx > 1 else
                                           "median kernel_ms (HIP events around each frame's launches on the render "
                                           "stream)"),
-               "contexts": nctx, "wf_grid_percent": grid, "counting_passes_s": round(counts_s, 2)}
+               "contexts": nctx, "wf_grid_percent": grid, "counting_passes_s": round(counts_s, 2),
+               "verified_vs_exhaustive": ex_bad == 0,
+               "verified_vs_exhaustive_basis": f"the last timed frame (context 0) bitwise against the same frame "
+                                               f"through the exhaustive walk (PT_OPT_WIDE 0): {ex_bad} floats differ"}
         price_leg(out, wl, traced, kernel_ms, alg, ref[0])
-        return out, ref, alg
+        prof = profiled_traffic(wl)
+        if prof is not None and prof[1].get("bench_line"):
+            # the committed counters' run against the timed one: same
+            # contexts and grid
+            bl = prof[1]["bench_line"]
+            out["profile_parallelism"] = {"contexts": bl.get("contexts"), "grid": bl.get("wf_grid_percent")}
+            out["profile_parallelism_matches"] = (bl.get("contexts") == nctx and bl.get("wf_grid_percent") == grid)
+        return out, ref, alg, exhaustive
 
-    out, _, _ = measure(scenes.DEFAULT_CAMERA, "camera (0,0,5) fov 60 (BASELINE.md §3)", workload + "_refcam",
-                        setup_ref)
+    out, _, _, _ = measure(scenes.DEFAULT_CAMERA, "camera (0,0,5) fov 60 (BASELINE.md §3)", workload + "_refcam",
+                           setup_ref)
     out["setup_s"] = round(setup_s, 2)
-    ff, ref_ff, alg_ff = measure(cam, "camera" + desc.split(", camera")[1], workload, setup_ff)
+    ff, ref_ff, alg_ff, ex = measure(cam, "camera" + desc.split(", camera")[1], workload, setup_ff)
     ff["note"] = "the scene's frame-filling camera (more pixels on geometry than BASELINE's (0,0,5))"
     if exhaustive_too:
-        r.set_option(ptamd.PT_OPT_WIDE, 0)
-        r.reset_launch_times()
-        t0 = time.perf_counter()
-        r.render(0, spp)
-        r.synchronize()
-        dt0 = time.perf_counter() - t0
-        kt0 = r.launch_times_ms()
-        k0 = float(np.mean(kt0)) if kt0.size else float("nan")
+        # the exhaustive frame measure() just checked against the timed frame
+        dt0 = ex["ms"] * 1e-3
+        k0 = ex["kernel_ms"]
         name0 = "wavefront pipeline, threaded exhaustive walk (PT_OPT_WIDE 0), per frame"
         ff["exhaustive_walk"] = {
             "value": round(ref_ff[0] / dt0 / 1e6, 3), "unit": "Mrays/s", "ms_per_step": round(dt0 * 1e3, 2),
             "steps": 1, "note": "the reference's traversal shape (every box a ray passes, visit order kept); "
-                                "same frame bit for bit",
+                                "compared bitwise with the timed frame (verified_vs_exhaustive)",
             "roofline": roofline_block(profiled_traffic(workload + "_exhaustive"), k0, alg_ff, name0, k0, k0,
-                                       int(kt0.size), "kernel_ms (HIP events around the frame's launches)")}
-        r.set_option(ptamd.PT_OPT_WIDE, 1)
+                                       ex["launches"], "kernel_ms (HIP events around the frame's launches)")}
     out["frame_filling_camera"] = ff
     del r, ctxs
     torch.cuda.synchronize()
@@ -779,26 +801,54 @@ def dist_scene_leg(dist, backend, device, world, rank, scene_name, W, H, spp, de
         r0.synchronize()
         want = r0.read_accum().view(np.uint32)
         same = all(bool(np.array_equal(g.view(np.uint32), want)) for g in got)
-        dt = float(np.median(wmax)) * 1e-3
-        cfg = {"workload": f"{desc} {W}x{H} {spp}spp {depth} bounces {sss} sss", "triangles": int(ntri),
-               "int_bits_nodes": bool(int_bits), "rays_per_frame": int(ref[0]),
-               "parallelism": f"tiles{world}-reduce (RCCL SUM of the accumulation buffer to rank 0); "
-                              f"{len(ctxs)} frames in flight per rank, traversal grid {grid} %"}
-        add_traced(cfg, traced, dt)
-        out = {"metric": "Mrays/s (reference-equivalent traceRay calls)", "value": round(ref[0] / dt / 1e6, 3),
-               "unit": "Mrays/s", "n_gpus": world, "ms_per_step": round(dt * 1e3, 2), "steps": steps,
-               "warmup": len(ctxs), "ms_per_frame": spread(wmax),
-               "rank_ms_per_frame": {"slowest": spread(wmax), "fastest": spread(wmin),
-                                     "note": "per run of frames, the slowest and the fastest rank"},
-               "kernel": KERNEL_NAMES.get(r0.last_kernel(), "?"), "config": cfg, "contexts": len(ctxs),
-               "verified_bitwise_vs_single_gpu": same,
-               "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
+        out = dist_leg_record(f"{desc} {W}x{H} {spp}spp {depth} bounces {sss} sss", ntri, int_bits, ref, traced,
+                              world, len(ctxs), grid, steps, np.asarray(wmax), np.asarray(wmin), same,
+                              KERNEL_NAMES.get(r0.last_kernel(), "?"), setup_s, counts_s)
     del r0, ctxs
     torch.cuda.synchronize(dev)
     for hs in hip_streams:
         hs.close()
     dist.barrier()
     return out
+
+
+def dist_leg_record(workload, ntri, int_bits, ref, traced, world, nctx, grid, steps, wmax, wmin, same, kernel,
+                    setup_s, counts_s):
+    """The full record of one N > 1 scene leg (rank 0): ms per frame = the
+    slowest rank's run wall time over its frames, median over runs."""
+    dt = float(np.median(wmax)) * 1e-3
+    cfg = {"workload": workload, "triangles": int(ntri), "int_bits_nodes": bool(int_bits),
+           "rays_per_frame": int(ref[0]),
+           "parallelism": f"tiles{world}-reduce (RCCL SUM of the accumulation buffer to rank 0); "
+                          f"{nctx} frames in flight per rank, traversal grid {grid} %"}
+    add_traced(cfg, traced, dt)
+    return {"metric": "Mrays/s (reference-equivalent traceRay calls)", "value": round(ref[0] / dt / 1e6, 3),
+            "unit": "Mrays/s", "n_gpus": world, "ms_per_step": round(dt * 1e3, 2), "steps": steps,
+            "warmup": nctx, "ms_per_frame": spread(wmax),
+            "rank_ms_per_frame": {"slowest": spread(wmax), "fastest": spread(wmin),
+                                  "note": "per run of frames, the slowest and the fastest rank"},
+            "kernel": kernel, "config": cfg, "contexts": nctx, "verified_bitwise_vs_single_gpu": bool(same),
+            "setup_s": round(setup_s, 2), "counting_passes_s": round(counts_s, 2)}
+
+
+def group_record(devs, setup_s, state, ms_peer, ms_staged, peer):
+    """The pt_create_multi leg's header: devices, the peer-store probe's
+    outcome (pt_group_check) and the exchange in force (pt_group_info)."""
+    return {"devices": devs, "setup_s": round(setup_s, 2),
+            "peer_store_check": {"state": {-1: "not run", 0: "matched", 1: "mismatch: staged copies in force",
+                                           -2: "armed"}.get(state, state),
+                                 "probe_ms_peer": round(ms_peer, 3), "probe_ms_staged": round(ms_staged, 3)},
+            "peer_stores_in_force": bool(peer),
+            "note": "one process, one thread, pt_create_multi over the devices (the reference's single-thread "
+                    "drop-in); frames whole from batch 0, enqueued back to back, synchronized at the end"}
+
+
+def group_exchange_record(peer, dt, steps, rays_per_frame, same):
+    return {"exchange": "peer stores into the first device's frame" if peer else
+            "staged packed copies (pt_tiles_pack, hipMemcpyPeerAsync, pt_tiles_unpack)",
+            "ms_per_step": round(dt * 1e3, 4), "steps": steps,
+            "value": None if rays_per_frame != rays_per_frame else round(rays_per_frame / dt / 1e6, 3),
+            "unit": "Mrays/s", "verified_bitwise_vs_single_gpu": bool(same)}
 
 
 def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light, cam, depth, sss, coll_dev,
@@ -878,6 +928,162 @@ class _StreamWork:
         torch.cuda.current_stream().wait_event(self.ev)
 
 
+# --- the printed line -------------------------------------------------------
+# The driver parses the LAST stdout line and reads only its tail: round 5's
+# 21.5-KB line could not be parsed (BENCH_r05.parsed null).  The full record
+# (per-leg spreads, gather-pattern tables, calibration, basis prose) goes to a
+# detail file that the line names; the line keeps the measured numbers, one
+# compact entry per leg, and every verification flag, within LINE_MAX_BYTES.
+LINE_MAX_BYTES = 6144
+DETAIL_DEFAULT = os.path.join("gpurun_out", "bench_detail.json")
+
+
+def _r(x, nd):
+    return None if x is None else round(float(x), nd)
+
+
+def compact_roofline(rf):
+    """bound/achieved/peak/unit/frac/traffic/source of a full roofline block,
+    plus the HBM fraction beside a non-HBM primary bound."""
+    if not rf:
+        return None
+    out = {k: rf.get(k) for k in ("bound", "achieved", "peak", "unit", "frac", "traffic")}
+    out["source"] = rf.get("source") or rf.get("traffic_source")
+    if isinstance(rf.get("hbm"), dict):
+        out["hbm_frac"] = rf["hbm"].get("frac")
+    if "frac_raw_counters" in rf:
+        out["frac_raw_counters"] = rf["frac_raw_counters"]
+    return out
+
+
+def _leg_camera(leg):
+    """value / ms / primary frac / verification of one camera of an N=1 leg."""
+    rf = leg.get("roofline") or {}
+    out = {"value": leg.get("value"), "ms_per_step": leg.get("ms_per_step"), "bound": rf.get("bound"),
+           "frac": rf.get("frac"), "contexts": leg.get("contexts"), "grid": leg.get("wf_grid_percent"),
+           "verified": leg.get("verified_vs_exhaustive")}
+    if leg.get("roofline_gather"):
+        out["gather_frac"] = leg["roofline_gather"].get("frac")
+    if leg.get("roofline_valu"):
+        out["valu_frac"] = leg["roofline_valu"].get("frac")
+    if leg.get("profile_parallelism_matches") is not None:
+        out["profile_matches_timed"] = leg["profile_parallelism_matches"]
+    return out
+
+
+def compact_leg(leg):
+    """One compact entry per leg: N=1 legs at BASELINE's camera with the
+    frame-filling camera nested (`ff`); N>1 legs value/ms/verified/error."""
+    if leg is None:
+        return None
+    if "error" in leg and "value" not in leg:
+        return {"error": str(leg["error"])[:300]}
+    if "n_gpus" in leg:   # a distributed leg
+        return {"value": leg.get("value"), "ms_per_step": leg.get("ms_per_step"), "n_gpus": leg.get("n_gpus"),
+                "verified": leg.get("verified_bitwise_vs_single_gpu"), "error": leg.get("error")}
+    out = _leg_camera(leg)
+    ff = leg.get("frame_filling_camera")
+    if ff:
+        out["ff"] = _leg_camera(ff)
+        ex = ff.get("exhaustive_walk")
+        if ex:
+            out["ff"]["exhaustive_ms"] = ex.get("ms_per_step")
+    return out
+
+
+def compact_group(g):
+    """The pt_create_multi leg: devices, the peer-store probe's state, each
+    exchange's time and bitwise check, or a short error."""
+    if g is None:
+        return None
+    out = {"devices": g.get("devices")}
+    if g.get("skipped"):
+        out["skipped"] = str(g["skipped"])[:200]
+    if g.get("error"):
+        out["error"] = str(g["error"])[:300]
+    if isinstance(g.get("peer_store_check"), dict):
+        out["peer_store_check"] = g["peer_store_check"].get("state")
+    if "peer_stores_in_force" in g:
+        out["peer_stores_in_force"] = g["peer_stores_in_force"]
+    for k in ("exchange0", "exchange1"):
+        if isinstance(g.get(k), dict):
+            e = g[k]
+            out[k] = {"ms_per_step": e.get("ms_per_step"), "value": e.get("value"),
+                      "verified": e.get("verified_bitwise_vs_single_gpu"),
+                      "peer": e.get("exchange", "").startswith("peer")}
+    return out
+
+
+def _finite(x):
+    """NaN / inf -> None, recursively: the line is strict JSON."""
+    if isinstance(x, dict):
+        return {k: _finite(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return [_finite(v) for v in x]
+    if isinstance(x, float) and (x != x or x in (float("inf"), float("-inf"))):
+        return None
+    return x
+
+
+def compact_line(full, detail_path=None):
+    """The line bench.py prints: the driver's contract keys, a short config,
+    the headline roofline and CPU baseline, every verification, one compact
+    entry per leg.  Raises if it would exceed LINE_MAX_BYTES."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "verified_vs_oracle", "verified_bitwise_vs_single_gpu",
+            "emulated_ranks", "bench_wall_s", "dry_run", "ranks_seen", "launcher", "backend_requested")
+    out = {k: full[k] for k in keep if k in full}
+    c = full.get("config", {})
+    out["config"] = {k: c[k] for k in ("workload", "parallelism", "kernel_options", "step_loop", "rays_per_frame",
+                                       "rays_traced", "msamples_per_s", "rays_traced_per_s_M", "rccl_comm_ranks",
+                                       "partition_slots") if c.get(k) is not None}
+    out["roofline"] = compact_roofline(full.get("roofline"))
+    cb = full.get("cpu_baseline")
+    if cb:
+        out["cpu_baseline"] = {"value": cb.get("value"), "unit": cb.get("unit"), "cores": cb.get("cores"),
+                               "kind": cb.get("kind"), "sample": str(cb.get("sample", ""))[:160]}
+        if isinstance(cb.get("single_thread"), dict):
+            out["cpu_baseline"]["single_thread_value"] = cb["single_thread"].get("value")
+    sc = full.get("single_context")
+    if sc:
+        out["single_context"] = {k: sc.get(k) for k in ("value", "ms_per_step", "steps", "kernel_ms",
+                                                        "verified_vs_oracle", "error") if sc.get(k) is not None}
+    if full.get("primary_cull_off"):
+        out["primary_cull_off_ms"] = full["primary_cull_off"].get("ms_per_step")
+    if full.get("configs"):
+        out["configs"] = {k: compact_leg(v) for k, v in full["configs"].items()}
+    if "group_leg" in full:
+        out["group_leg"] = compact_group(full["group_leg"])
+    if detail_path:
+        out["detail_file"] = detail_path
+    out = _finite(out)
+    s = json.dumps(out, separators=(",", ":"), allow_nan=False)
+    if len(s) > LINE_MAX_BYTES:
+        raise ValueError(f"bench line is {len(s)} bytes (> {LINE_MAX_BYTES})")
+    return out
+
+
+def emit_line(full, detail_path=None):
+    """Write the full record to `detail_path` (and one stderr line), print the
+    compact line on stdout as the process's last stdout line."""
+    detail_path = detail_path if detail_path is not None else os.environ.get("PT_BENCH_DETAIL", DETAIL_DEFAULT)
+    written = None
+    if detail_path:
+        try:
+            d = os.path.dirname(detail_path)
+            if d:
+                os.makedirs(d, exist_ok=True)
+            with open(detail_path, "w") as f:
+                json.dump(full, f, indent=1)
+            written = detail_path
+        except OSError as e:
+            log(f"detail file {detail_path} not written: {e}")
+    print("bench detail: " + json.dumps(full), file=sys.stderr, flush=True)
+    line = compact_line(full, written)
+    print(json.dumps(line, separators=(",", ":"), allow_nan=False), flush=True)
+    return line
+
+
 def log(msg):
     """A progress line on stderr, tagged with the rank and the seconds since
     start: a run that stops shows where."""
@@ -917,11 +1123,43 @@ def dry_run(world, rank, backend):
     t[rank] = rank + 1
     dist.all_reduce(t)
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": [int(x) - 1 for x in t.tolist()],
-                          "launcher": "spawned" if os.environ.get("PT_BENCH_SPAWNED") == "1" else "external",
-                          "backend_requested": backend}), flush=True)
+        full = dry_run_record(world, [int(x) - 1 for x in t.tolist()],
+                              "spawned" if os.environ.get("PT_BENCH_SPAWNED") == "1" else "external", backend)
+        emit_line(full, os.environ.get("PT_BENCH_DETAIL", ""))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def dry_run_record(world, ranks_seen, launcher, backend):
+    """The full record of an N-rank run with every N > 1 field filled --
+    the distributed legs and the pt_create_multi leg built by the same
+    helpers as a real run, with placeholder numbers, long worst-case error
+    strings on one leg -- so the printed line's size and keys are checked
+    without a GPU (tests/test_multi.py)."""
+    nan = float("nan")
+    traced = {k: 10 ** 9 for k in TRACED_KEYS}
+    ref = np.array([3.06e7, 9.7e7, 1.7e7, 1.6e7])
+    legs = {}
+    for key, scene_name, lw, lh, lspp, ldepth, lsteps in DIST_SCENE_LEGS:
+        legs[key] = dist_leg_record(f"{scene_name} (0,0,5) {lw}x{lh} {lspp}spp {ldepth} bounces 3 sss", 10 ** 7, True,
+                                    ref, traced, world, 3, 33, lsteps, np.array([1.0, 1.1, 1.2]),
+                                    np.array([0.9, 1.0, 1.1]), True, KERNEL_NAMES[3], 1.0, 1.0)
+    legs["config_failed"] = {"error": "rank 7: PTError: " + "x" * 1000}
+    group = group_record(list(range(world)), 1.0, 0, 0.1, 0.2, True)
+    for exch in (0, 1):
+        group[f"exchange{exch}"] = group_exchange_record(exch == 0, 1e-4, 20, 3.06e7, True)
+    line = {"metric": "Mrays/s at 1920x1080x8spp, box.obj BVH", "value": None, "unit": "Mrays/s", "n_gpus": world,
+            "steps": 0, "warmup": 0, "ms_per_step": None, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "DRY RUN (no GPU call): the process-group plumbing and the line's shape",
+            "dry_run": True, "ranks_seen": ranks_seen, "launcher": launcher, "backend_requested": backend,
+            "config": {"workload": "box.obj, camera (0,0,5) fov 60 1920x1080 8spp 4 bounces 3 sss",
+                       "parallelism": f"tiles{world}-sparse-gather", "kernel_options": [],
+                       "step_loop": "native (pt_dist_run, RCCL from C++)", "rays_per_frame": 30586335,
+                       "rccl_comm_ranks": world, "partition_slots": [12] + [16] * (world - 1)},
+            "roofline": roofline_block(None, nan, 0, KERNEL_NAMES[1], nan, nan, 0, "dry run"),
+            "verified_bitwise_vs_single_gpu": None, "configs": legs, "group_leg": group}
+    return line
 
 
 def group_leg(devices, v, i, n, int_bits, light, cam, W, H, spp, depth, sss, steps, rays_per_frame):
@@ -958,13 +1196,7 @@ def group_leg(devices, v, i, n, int_bits, light, cam, W, H, spp, depth, sss, ste
     g.synchronize()
     state, ms_peer, ms_staged = g.group_check()
     devs, peer = g.group_info()
-    out = {"devices": devs, "setup_s": round(setup_s, 2),
-           "peer_store_check": {"state": {-1: "not run", 0: "matched", 1: "mismatch: staged copies in force",
-                                          -2: "armed"}.get(state, state),
-                                "probe_ms_peer": round(ms_peer, 3), "probe_ms_staged": round(ms_staged, 3)},
-           "peer_stores_in_force": bool(peer),
-           "note": "one process, one thread, pt_create_multi over the devices (the reference's single-thread "
-                   "drop-in); frames whole from batch 0, enqueued back to back, synchronized at the end"}
+    out = group_record(devs, setup_s, state, ms_peer, ms_staged, peer)
     for exch in (0, 1):
         g.set_option(ptamd.PT_OPT_GROUP_EXCHANGE, exch)
         for _ in range(3):
@@ -978,12 +1210,7 @@ def group_leg(devices, v, i, n, int_bits, light, cam, W, H, spp, depth, sss, ste
         got = g.read_accum().view(np.uint32)
         same = bool(np.array_equal(got, want))
         _, peer = g.group_info()
-        out[f"exchange{exch}"] = {
-            "exchange": "peer stores into the first device's frame" if peer else "staged packed copies (pt_tiles_pack, "
-                                                                                  "hipMemcpyPeerAsync, pt_tiles_unpack)",
-            "ms_per_step": round(dt * 1e3, 4), "steps": steps,
-            "value": None if rays_per_frame != rays_per_frame else round(rays_per_frame / dt / 1e6, 3),
-            "unit": "Mrays/s", "verified_bitwise_vs_single_gpu": same}
+        out[f"exchange{exch}"] = group_exchange_record(peer, dt, steps, rays_per_frame, same)
     g.close()
     return out
 
@@ -1054,7 +1281,8 @@ def main():
     ap.add_argument("--sss", type=int, default=3, help="SSS_MAX_BOUNCES (reference 3)")
     ap.add_argument("--collective", choices=["gather", "reduce"], default="gather")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify", action="store_true", help="N>1: compare the assembled frame with a 1-GPU render")
+    ap.add_argument("--verify", type=int, choices=[0, 1], default=None,
+                    help="N>1: compare the assembled frame with a 1-GPU render (default on at N > 1)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VAL",
                     help="pt_set_option before timing (A/B of output-invariant kernel options)")
     ap.add_argument("--assemble", type=int, choices=[0, 1, 2], default=2,
@@ -1130,6 +1358,8 @@ def main():
     # the collective replaced by a device copy of its own slot.  A rehearsal of
     # the root's critical path, never a multi-GPU result (the line says so).
     emu = int(os.environ.get("PT_BENCH_EMULATE_RANKS", "1"))
+    if args.verify is None:
+        args.verify = int(world > 1)
     if emu > 1 and world != 1:
         raise SystemExit("PT_BENCH_EMULATE_RANKS needs a 1-process run")
     if emu > 1 and (args.collective != "gather" or args.verify):
@@ -1570,7 +1800,46 @@ def main():
             if not np.array_equal(c.read_accum().view(np.uint32), want):
                 raise SystemExit("bench: the pipelined contexts' frames differ")
 
+    # The drop-in frame: ONE context at the library's
+    # defaults -- no bench-only options, its own stream -- frames one after
+    # another as the reference's mainLoop renders them (VulkanRayTracer.cpp:
+    # 717-865), `steps` frames after a short warmup, the last one checked
+    # against the oracle with the timed frame below.
+    single = None
+    single_frame = None
+    if world == 1 and emu == 1 and not args.packed and args.collective == "gather" and not args.profile_run:
+        try:
+            sc = ptamd.Renderer(device)
+            sc.upload_scene(v, i, n, int_bits=int_bits)
+            sc.upload_lights(light)
+            sc.set_camera(cam)
+            sc.set_params(DEPTH, SSS)
+            sc.resize_and_clear(W, H)
+            sc.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 1)
+            for _ in range(max(3, args.warmup)):
+                sc.render(0, SPP)
+            sc.synchronize()
+            sc.reset_launch_times()
+            t_sc = time.perf_counter()
+            for _ in range(args.steps):
+                sc.render(0, SPP)
+            sc.synchronize()
+            dt_sc = time.perf_counter() - t_sc
+            kt_sc = sc.launch_times_ms()
+            single_frame = sc.read_accum()
+            single = {"ms_per_step": round(dt_sc / args.steps * 1e3, 4), "steps": args.steps,
+                      "value": None if rays_per_frame != rays_per_frame else
+                      round(rays_per_frame * args.steps / dt_sc / 1e6, 3),
+                      "kernel_ms": round(float(np.mean(kt_sc)), 4) if kt_sc.size else None,
+                      "basis": "one context, library defaults (no pt_set_option), its own stream; pt_render(0, spp) "
+                               "per frame back to back, synchronized at the end"}
+            sc.close()
+            log(f"single context: {single['ms_per_step']} ms per frame")
+        except ptamd.PTError as e:
+            single = {"error": str(e)[:300]}
+
     verified = None
+    verify_error = None
     if args.verify and dist is not None and rank == 0:
         # the assembled frame must be bitwise the single-GPU frame
         ref = ptamd.Renderer(device)
@@ -1593,9 +1862,11 @@ def main():
             if not verified:
                 break
         if not verified:
+            # recorded, and the run exits non-zero after the line: the other
+            # ranks still reach every collective that follows
             bad = np.flatnonzero(got.view(np.uint32) != want.view(np.uint32))
-            raise SystemExit(f"bench --verify: assembled frame differs from the single-GPU frame in {bad.size} "
-                             f"floats; first at pixel {bad[0] // 4} ch {bad[0] % 4}: {got[bad[0]]} vs {want[bad[0]]}")
+            verify_error = (f"bench --verify: assembled frame differs from the single-GPU frame in {bad.size} "
+                            f"floats; first at pixel {bad[0] // 4} ch {bad[0] % 4}: {got[bad[0]]} vs {want[bad[0]]}")
 
     box_kernel = KERNEL_NAMES.get(r.last_kernel(), "?")
     comm_ranks = None
@@ -1704,7 +1975,7 @@ def main():
             out_line["primary_cull_off"] = no_cull
         if verified is not None:
             out_line["verified_bitwise_vs_single_gpu"] = verified
-        oracle_mismatch = None
+        oracle_mismatch = verify_error
         if world == 1 and emu == 1 and not args.no_cpu_baseline and not args.profile_run:
             out_line["cpu_baseline"], oracle_img = cpu_baseline(v, i, n, cam, light, W, H, SPP, DEPTH, SSS)
             if oracle_img is not None and timed_frame is not None:
@@ -1719,6 +1990,13 @@ def main():
                     oracle_mismatch = (f"bench: the timed frame differs from the oracle in {bad.size} floats; first at "
                                        f"pixel {bad[0] // 4} ch {bad[0] % 4}: {timed_frame[bad[0]]} vs "
                                        f"{oracle_img[bad[0]]}")
+            if oracle_img is not None and single_frame is not None and single is not None:
+                sbad = int(np.count_nonzero(single_frame.view(np.uint32) != oracle_img.view(np.uint32)))
+                single["verified_vs_oracle"] = sbad == 0
+                if sbad and oracle_mismatch is None:
+                    oracle_mismatch = f"bench: the single-context frame differs from the oracle in {sbad} floats"
+        if single is not None:
+            out_line["single_context"] = single
         if dist_legs is not None:
             out_line["configs"] = dist_legs
         if group is not None:
@@ -1739,14 +2017,21 @@ def main():
                 out_line["configs"][key] = scene_leg(scene_name, lw, lh, lspp, ldepth, SSS, steps, device, workload,
                                                      exhaustive_too=key == "config5", setup_ref=s_ref,
                                                      setup_ff=s_ff)
+            for key, leg in out_line["configs"].items():
+                for cam_leg in (leg, leg.get("frame_filling_camera") or {}):
+                    if cam_leg.get("verified_vs_exhaustive") is False and oracle_mismatch is None:
+                        oracle_mismatch = f"bench: {key}: {cam_leg.get('verified_vs_exhaustive_basis')}"
         out_line["bench_wall_s"] = round(time.perf_counter() - T_START, 1)
-        print(json.dumps(out_line), flush=True)
+        emit_line(out_line)
         if oracle_mismatch is not None:
             print(oracle_mismatch, file=sys.stderr, flush=True)
-            sys.exit(1)
+    else:
+        oracle_mismatch = None
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if oracle_mismatch is not None:
+        sys.exit(1)   # after the last collective: the other ranks are not left waiting
 
 
 if __name__ == "__main__":

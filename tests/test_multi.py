@@ -212,9 +212,9 @@ def test_bench_spawns_ranks_without_a_launcher():
     res = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"], cwd=ROOT,
                          env=env, capture_output=True, text=True, timeout=180)
     assert res.returncode == 0, res.stderr[-3000:]
-    out = json.loads([x for x in res.stdout.splitlines() if x.startswith("{")][-1])
-    assert out == {"dry_run": True, "n_gpus": 2, "ranks_seen": [0, 1], "launcher": "spawned",
-                   "backend_requested": "nccl"}
+    out = json.loads(res.stdout.strip().splitlines()[-1])
+    assert {k: out[k] for k in ("dry_run", "n_gpus", "ranks_seen", "launcher", "backend_requested")} == \
+        {"dry_run": True, "n_gpus": 2, "ranks_seen": [0, 1], "launcher": "spawned", "backend_requested": "nccl"}
 
 
 def test_bench_stuck_rank_fails_fast():
