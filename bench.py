@@ -836,7 +836,7 @@ def group_record(devs, setup_s, state, ms_peer, ms_staged, peer):
     outcome (pt_group_check) and the exchange in force (pt_group_info)."""
     return {"devices": devs, "setup_s": round(setup_s, 2),
             "peer_store_check": {"state": {-1: "not run", 0: "matched", 1: "mismatch: staged copies in force",
-                                           -2: "armed"}.get(state, state),
+                                           2: "probe failed: staged copies in force", -2: "armed"}.get(state, state),
                                  "probe_ms_peer": round(ms_peer, 3), "probe_ms_staged": round(ms_staged, 3)},
             "peer_stores_in_force": bool(peer),
             "note": "one process, one thread, pt_create_multi over the devices (the reference's single-thread "

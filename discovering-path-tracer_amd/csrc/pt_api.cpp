@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <rccl/rccl.h>   // types only: the functions are resolved at run time (rccl_api)
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -360,7 +362,8 @@ struct pt_context {
   int opt_scene_lds = 1;   // PT_OPT_SCENE_IN_LDS: 0 never, 1 auto, 2 always
   int opt_sample_lanes = 0;   // PT_OPT_SAMPLE_LANES: 0 auto, else 1/2/4/8
   int opt_fresh = 0;          // PT_OPT_FRESH_BATCH0
-  int opt_item_order = 1;     // PT_OPT_ITEM_ORDER
+  int opt_item_order = -1;    // PT_OPT_ITEM_ORDER (-1 auto)
+  int opt_mixed = -1;         // PT_OPT_MIXED_LANES: -1 auto, 0 off, k = whole tiles for k % of the resident slots
   int opt_kernel = 0;         // PT_OPT_KERNEL: 0 auto, 1 path-recursive, 3 wavefront
   int opt_cull = 1;           // PT_OPT_PRIMARY_CULL
   int opt_wf_paths = 0;       // PT_OPT_WF_PATHS (0 = 2^27)
@@ -375,7 +378,23 @@ struct pt_context {
   // the frame, partition, sample lanes or cull rectangles change
   int* d_items = nullptr;
   size_t items_cap = 0;
-  int n_live_items = 0, n_culled_items = 0;
+  int n_live_items = 0, n_culled_items = 0;   // launched live items (mixed lanes: whole tiles + parts)
+  bool items_mixed = false;                    // the live origins carry per-item lane counts
+  std::vector<int> block_lanes;                // lanes per 16x16 block in the current item lists (0: not launched)
+  // measured mixed-lane schedule (mix_feedback)
+  unsigned* d_cost = nullptr;                  // per 16x4 part: summed wave durations of a measuring launch
+  unsigned* h_cost = nullptr;                  // pinned copy
+  size_t cost_n = 0;                           // blocks allocated
+  hipEvent_t cost_ev = nullptr;
+  bool cost_pending = false, cost_stale = false, cost_measure = false, cost_ready = false;
+  int cost_stable = 0, cost_frames = 0, cost_gen = 0;
+  std::vector<float> cost_key, cost_scratch;
+  std::vector<int> cost_lanes;                 // block_lanes of the measuring launch
+  std::vector<double> block_cost;              // per 16x4 part, at one lane per pixel (averaged)
+  int scene_serial = 0;                        // bumped by scene and light uploads
+  int last_mix = 0;                            // pt_mixed_info: the last launch's schedule
+  long long render_slots = -1;                 // resident LDS render workgroups (mixed lanes' budget)
+  size_t render_slots_lds = 0;                 // ... at this many bytes of staged scene
   size_t culled_org_off = 0;   // h_items / d_items: where the culled items' first pixels start
   size_t live_org_off = 0;     // ... and the live items' ones
   std::vector<int> h_items;
@@ -623,13 +642,242 @@ static void item_lists(const ptd::RenderParams& p, const ptd::Part& part, std::v
   for (const auto& e : weighted) live->push_back(e.second);
 }
 
-static int compact_items(pt_context* c, ptd::RenderParams* p) {
+// Mixed sample lanes (PT_OPT_MIXED_LANES): the first `budget` live tiles
+// whose every part is live, in list order, become whole-tile items at one lane
+// per pixel; every other live part keeps p.spl lanes and follows them.  The
+// whole tiles are the cheapest per sample (8 samples per lane, no colour
+// hand-off) but the longest workgroups, so they start first and at most one
+// round of them runs; the short parts then fill the launch's drain.
+static void mixed_origins(const ptd::RenderParams& p, const ptd::Part& part, const std::vector<int>& live,
+                          long long budget, std::vector<int>* org) {
+  const int spl = p.spl, rows = 16 / spl;
+  const int tiles = ptd::part_count(part, p.blocks_total);
+  std::vector<int> parts_live(tiles, 0);
+  for (int it : live) parts_live[it / spl]++;
+  std::vector<char> whole(tiles, 0);
+  long long k = 0;
+  const int lg = __builtin_ctz((unsigned)spl);
+  for (int it : live) {
+    const int li = it / spl;
+    if (k >= budget) break;
+    if (whole[li] || parts_live[li] != spl) continue;
+    whole[li] = 1;
+    ++k;
+    int bx, by;
+    ptd::tile_block(ptd::part_tile(part, li), p.blocks_x, &bx, &by);
+    org->push_back(bx * 16);   // log2(1) = 0 in the lane-count bits
+    org->push_back(by * 16);
+  }
+  for (int it : live) {
+    const int li = it / spl;
+    if (whole[li]) continue;
+    int bx, by;
+    ptd::tile_block(ptd::part_tile(part, li), p.blocks_x, &bx, &by);
+    org->push_back((bx * 16) | (lg << ptd::kMixShift));
+    org->push_back(by * 16 + (it % spl) * rows);
+  }
+}
+
+// Per-sample cost of 1, 2, 4 and 8 lanes per pixel relative to one lane:
+// the box 1080p 8-spp frame with frames in flight (no drain), 0.2037 /
+// 0.2121 / 0.2385 / 0.2775 ms per frame (profiles/r06b).
+static const double kLaneInfl[4] = {1.0, 0.2121 / 0.2037, 0.2385 / 0.2037, 0.2775 / 0.2037};
+
+// The measured schedule of mixed lanes.  cost[k], k = y / 4 * blocks_x +
+// x / 16: the live work of the frame's 16x4 part k at one lane per pixel, in
+// wave time (render_kernel's cost feedback: every wave's duration added to
+// its part, divided by the lane factor it ran at).  A wave covers one part
+// at one lane per pixel, half of one at two, and so on, so a workgroup at s
+// lanes runs ~max over the parts it covers of cost * kLaneInfl[s] / s.
+// Whole-live tiles take the fewest lanes that keep their workgroups at most
+// Dmax long; tiles with culled parts keep their live parts at p.spl.  Items
+// go longest first, and the launch is simulated as greedy list scheduling
+// on `slots` resident workgroups for a range of Dmax; the shortest simulated
+// frame wins.  Any item order and lane count gives the same image.
+struct MixItem {
+  int x, y;
+  double dur;
+};
+static void measured_origins(const ptd::RenderParams& p, const ptd::Part& part, const std::vector<int>& live,
+                             const std::vector<double>& cost, long long slots, int max_lanes,
+                             std::vector<int>* org) {
+  const int spl = p.spl, rows = 16 / spl, lg_base = __builtin_ctz((unsigned)spl);
+  const int tiles = ptd::part_count(part, p.blocks_total);
+  std::vector<int> parts_live(tiles, 0);
+  for (int it : live) parts_live[it / spl]++;
+  struct Tile {
+    int x, y, nlive;
+    double c[4];
+    std::vector<int> parts;
+  };
+  std::vector<Tile> tl;
+  std::vector<int> index(tiles, -1);
+  auto part_cost = [&](int x, int y) {   // pixel (x, y)'s 16x4 part
+    const size_t k = (size_t)(y >> 2) * p.blocks_x + (x >> 4);
+    return k < cost.size() ? std::max(1.0, cost[k]) : 1.0;
+  };
+  for (int it : live) {
+    const int li = it / spl;
+    if (index[li] < 0) {
+      int bx, by;
+      ptd::tile_block(ptd::part_tile(part, li), p.blocks_x, &bx, &by);
+      index[li] = (int)tl.size();
+      Tile t{bx * 16, by * 16, parts_live[li], {0, 0, 0, 0}, {}};
+      for (int k = 0; k < 4; ++k) t.c[k] = part_cost(t.x, t.y + 4 * k);
+      tl.push_back(t);
+    }
+    tl[index[li]].parts.push_back(it % spl);
+  }
+  double total = 0;
+  for (const Tile& t : tl)
+    for (double x : t.c) total += x;
+  const double lb = total / (4.0 * (double)std::max(1ll, slots));   // one lane per pixel, perfectly packed
+  std::vector<MixItem> best, items;
+  double best_span = 1e300;
+  std::vector<double> heap;
+  for (double f : {1e9, 2.0, 1.5, 1.2, 1.0, 0.85, 0.75, 0.6, 0.5, 0.35, 0.25, 0.18, 0.12}) {
+    const double dmax = lb * f;
+    items.clear();
+    for (const Tile& t : tl) {
+      if (t.nlive != spl) {   // culled parts: the live parts at p.spl (a part spans 4 / spl of the 16x4 parts)
+        for (int part_i : t.parts) {
+          const int y = t.y + part_i * rows;
+          double c = 0;
+          for (int yy = y; yy < y + rows; yy += 4) c = std::max(c, t.c[(yy - t.y) >> 2]);
+          if (rows < 4) c = t.c[(y - t.y) >> 2];
+          items.push_back({t.x | (lg_base << ptd::kMixShift), y, c * kLaneInfl[lg_base] / spl});
+        }
+        continue;
+      }
+      // the fewest lanes whose longest workgroup fits dmax
+      int lg = 0;
+      for (;; ++lg) {
+        const int s = 1 << lg, wrows = 16 / s;
+        double longest = 0;
+        for (int k = 0; k < 4; ++k) longest = std::max(longest, t.c[k]);
+        if (s >= max_lanes || longest * kLaneInfl[lg] / s <= dmax) {
+          for (int w = 0; w < s; ++w) {   // workgroup w: rows [w * wrows, (w + 1) * wrows)
+            double c = 0;
+            for (int yy = w * wrows; yy < (w + 1) * wrows; yy += 4) c = std::max(c, t.c[yy >> 2]);
+            if (wrows < 4) c = t.c[(w * wrows) >> 2];
+            items.push_back({t.x | (lg << ptd::kMixShift), t.y + w * wrows, c * kLaneInfl[lg] / s});
+          }
+          break;
+        }
+      }
+    }
+    std::stable_sort(items.begin(), items.end(), [](const MixItem& a, const MixItem& b) { return a.dur > b.dur; });
+    // greedy list scheduling: each item on the earliest free slot
+    heap.assign((size_t)std::max(1ll, slots), 0.0);
+    double span = 0;
+    for (const MixItem& m : items) {
+      std::pop_heap(heap.begin(), heap.end(), std::greater<double>());
+      heap.back() += m.dur;
+      span = std::max(span, heap.back());
+      std::push_heap(heap.begin(), heap.end(), std::greater<double>());
+    }
+    if (span < best_span * 0.999) {
+      best_span = span;
+      best = items;
+    }
+  }
+  for (const MixItem& m : best) {
+    org->push_back(m.x);
+    org->push_back(m.y);
+  }
+  if (const char* dump = getenv("PT_MIX_DUMP")) {   // diagnostics: part costs and the chosen schedule
+    if (FILE* f = fopen(dump, "w")) {
+      fprintf(f, "# slots %lld lb %.1f best_span %.1f items %zu\n", slots, lb, best_span, best.size());
+      for (const Tile& t : tl) fprintf(f, "T %d %d %d %.1f %.1f %.1f %.1f\n", t.x, t.y, t.nlive, t.c[0], t.c[1], t.c[2], t.c[3]);
+      for (const MixItem& m : best)
+        fprintf(f, "I %d %d %d %.1f\n", m.x & ((1 << ptd::kMixShift) - 1), m.y, m.x >> ptd::kMixShift, m.dur);
+      fclose(f);
+    }
+  }
+}
+
+// Cost feedback of the measured mixed-lane schedule (PT_OPT_MIXED_LANES -1).
+// The schedule belongs to the frame's inputs (the cost key: size, batches,
+// lanes, camera, params, scene and lights, culling).  Once the key has held
+// for a render, one launch records its blocks' costs (render_kernel adds
+// every wave's duration on the GPU wall clock to its block), copied back
+// asynchronously behind an event; a later render whose event has completed
+// folds them in, divided by the lane factor each block ran at, and after
+// kCostFrames such launches the schedule is built from them
+// (measured_origins).  The host never waits: a render whose copy has not
+// landed keeps the static schedule.
+constexpr int kCostFrames = 2;
+static int mix_feedback(pt_context* c, const ptd::RenderParams& p, uint32_t n_batches) {
+  std::vector<float>& key = c->cost_scratch;
+  key.assign({(float)p.width, (float)p.height, (float)n_batches, (float)(p.first_batch == 0), (float)p.spl,
+              (float)c->params.max_depth, (float)c->params.sss_bounces, (float)c->scene_serial, (float)p.n_cull,
+              (float)c->opt_item_order});
+  key.insert(key.end(), c->cam, c->cam + 16);
+  for (int r = 0; r < p.n_cull; ++r) key.insert(key.end(), p.cull[r], p.cull[r] + 4);
+  const size_t nb = (size_t)p.blocks_total;
+  const size_t np4 = (size_t)p.blocks_x * (size_t)((p.height + 15) / 16) * 4;   // 16x4 parts
+  if (key != c->cost_key) {
+    c->cost_key = key;
+    c->cost_stable = 0;
+    c->cost_frames = 0;
+    c->cost_ready = false;
+    c->cost_measure = false;
+    c->cost_stale = c->cost_pending;   // a copy in flight belongs to the old inputs
+    c->block_cost.assign(np4, 0.0);
+  }
+  if (c->cost_pending && hipEventQuery(c->cost_ev) == hipSuccess) {
+    c->cost_pending = false;
+    if (!c->cost_stale && c->cost_lanes.size() == nb) {
+      for (size_t k = 0; k < np4; ++k) {   // part k lies in block (k / blocks_x / 4, k % blocks_x)
+        const size_t b = (k / (size_t)p.blocks_x / 4) * (size_t)p.blocks_x + k % (size_t)p.blocks_x;
+        const int s = c->cost_lanes[b];
+        if (s > 0) c->block_cost[k] += (double)c->h_cost[k] / kLaneInfl[__builtin_ctz((unsigned)s)];
+      }
+      if (++c->cost_frames >= kCostFrames) {
+        for (double& x : c->block_cost) x /= c->cost_frames;
+        c->cost_ready = true;
+        c->cost_gen++;
+      }
+    }
+    c->cost_stale = false;
+  }
+  c->cost_stable++;
+  c->cost_measure = false;
+  if (!c->cost_ready && !c->cost_pending && c->cost_stable >= 2) {
+    if (c->cost_n < np4) {
+      dev_free(c->d_cost);
+      if (c->h_cost) (void)hipHostFree(c->h_cost);
+      c->h_cost = nullptr;
+      c->cost_n = 0;
+      PT_HIP(hipMalloc((void**)&c->d_cost, np4 * sizeof(unsigned)));
+      PT_HIP(hipHostMalloc((void**)&c->h_cost, np4 * sizeof(unsigned), hipHostMallocDefault));
+      c->cost_n = np4;
+    }
+    if (!c->cost_ev) PT_HIP(hipEventCreateWithFlags(&c->cost_ev, hipEventDisableTiming));
+    c->cost_measure = true;
+  }
+  return PT_OK;
+}
+
+// How a launch mixes lane counts (render_impl): a static budget of whole
+// tiles (mixed_origins) until block costs are measured, then the measured
+// schedule (measured_origins).
+struct MixPlan {
+  long long budget = 0;                       // whole tiles of the static schedule
+  const std::vector<double>* cost = nullptr;  // measured block costs, or null
+  int gen = 0;                                // measured schedule generation (cache key)
+  long long slots = 0;
+  int max_lanes = 8;
+};
+
+static int compact_items(pt_context* c, ptd::RenderParams* p, const MixPlan* mix = nullptr) {
+  const long long mix_budget = mix ? (mix->cost ? -1 - mix->gen : mix->budget) : 0;
   const ptd::Part& pt = part_of(c, p->rank);
   // every slot position of this rank's share: two slot sets with the same
   // period, count and first position still deal different tiles
   std::vector<float>& key = c->items_scratch;
   key.assign({(float)p->width, (float)p->height, (float)pt.m, (float)pt.cnt, (float)p->rank, (float)p->spl,
-              (float)p->n_cull, (float)p->item_order});
+              (float)p->n_cull, (float)p->item_order, (float)mix_budget});
   for (int k = 0; k < pt.cnt; ++k) key.push_back((float)pt.pos[k]);
   for (int r = 0; r < p->n_cull; ++r) key.insert(key.end(), p->cull[r], p->cull[r] + 4);
   if (key.size() != c->items_key.size() || memcmp(key.data(), c->items_key.data(), key.size() * 4) != 0) {
@@ -653,7 +901,18 @@ static int compact_items(pt_context* c, ptd::RenderParams* p) {
     c->culled_org_off = c->h_items.size();
     origins(culled);
     c->live_org_off = c->h_items.size();
-    origins(live);
+    int n_launch = (int)live.size();
+    if (mix && p->spl > 1 && (mix->cost || mix->budget > 0)) {
+      std::vector<int> org;
+      if (mix->cost)
+        measured_origins(*p, pt, live, *mix->cost, mix->slots, mix->max_lanes, &org);
+      else
+        mixed_origins(*p, pt, live, mix->budget, &org);
+      c->h_items.insert(c->h_items.end(), org.begin(), org.end());
+      n_launch = (int)(org.size() / 2);
+    } else {
+      origins(live);
+    }
     if (c->h_items.size() > c->items_cap) {
       dev_free(c->d_items);
       c->items_cap = 0;
@@ -662,12 +921,21 @@ static int compact_items(pt_context* c, ptd::RenderParams* p) {
     }
     if (!c->h_items.empty())
       PT_HIP(hipMemcpy(c->d_items, c->h_items.data(), c->h_items.size() * sizeof(int), hipMemcpyHostToDevice));
-    c->n_live_items = (int)live.size();
+    c->n_live_items = n_launch;
     c->n_culled_items = (int)culled.size();
+    c->items_mixed = mix && p->spl > 1 && (mix->cost || mix->budget > 0);
+    // the lane count each block's workgroups run at (cost feedback)
+    c->block_lanes.assign((size_t)p->blocks_total, 0);
+    for (size_t k = 0; k + 1 < c->h_items.size() - c->live_org_off; k += 2) {
+      const int ox = c->h_items[c->live_org_off + k], oy = c->h_items[c->live_org_off + k + 1];
+      c->block_lanes[(size_t)(oy >> 4) * p->blocks_x + ((ox & ((1 << ptd::kMixShift) - 1)) >> 4)] =
+          c->items_mixed ? 1 << (ox >> ptd::kMixShift) : p->spl;
+    }
     c->items_key = key;
   }
   p->items = c->d_items;
   p->n_items = c->n_live_items;
+  p->mix = c->items_mixed ? 1 : 0;
   p->culled_org = (const int2*)(c->d_items + c->culled_org_off);
   p->items_org = (const int2*)(c->d_items + c->live_org_off);
   p->n_culled_items = c->n_culled_items;
@@ -871,7 +1139,6 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.part_pos = c->d_parts + (size_t)c->rank * ptd::kMaxSlots;
   p.n_tiles = ptd::part_count(hpart, p.blocks_total);
   p.fresh = pack_out ? 1 : c->opt_fresh;
-  p.item_order = c->opt_item_order;
   p.pack_out = nullptr;
   if (c->opt_sample_lanes) {
     p.spl = c->opt_sample_lanes;
@@ -926,7 +1193,13 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   const bool wf = c->opt_kernel == 3 || (c->opt_kernel == 0 && !lds && !c->stats_mode && wf_auto);
   if (wf && c->stats_mode) return fail(PT_ERR_UNSUPPORTED, "stats mode runs the path-recursive kernel only");
   const bool cnt = c->opt_count != 0 && !c->stats_mode;
+  // PT_OPT_ITEM_ORDER auto: scan order for a whole frame on the path-recursive
+  // kernel (box 1080p8 at 4 lanes, one context: 0.2403 against 0.2463 ms
+  // heaviest first, profiles/r06b), heaviest first on a share of the frame
+  // and on the wavefront pipeline
+  p.item_order = c->opt_item_order >= 0 ? c->opt_item_order : (!wf && c->nranks == 1 ? 0 : 1);
   p.n_cull = -1;
+  c->last_mix = 0;
   p.items = nullptr;
   p.culled_org = nullptr;
   p.items_org = nullptr;
@@ -935,8 +1208,42 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     p.n_cull = cull_rects(c->cam, c->width, c->height, c->root_lo, c->root_hi, c->lights_host.data(),
                           c->n_lights, &p.cull[0][0], ptd::kMaxCullRects);
   if (p.n_cull >= 0) {
-    const int rc = compact_items(c, &p);
+    // mixed lanes (PT_OPT_MIXED_LANES): one rank, LDS-staged path-recursive
+    // launches that render into the accumulation buffer
+    MixPlan plan;
+    bool mixed = false;
+    if (c->opt_mixed != 0 && !wf && lds && c->nranks == 1 && !pack_out && p.spl > 1 && !cnt) {
+      mixed = true;
+      const size_t lds_b = ptd::scene_lds_bytes(p);
+      if (c->render_slots < 0 || c->render_slots_lds != lds_b) {
+        c->render_slots = ptd::render_slots(lds_b);
+        c->render_slots_lds = lds_b;
+      }
+      // auto: every item at PT_OPT_SAMPLE_LANES until the block costs are
+      // measured -- the measuring launches then run a uniform schedule, whose
+      // workgroups nearly all run at full occupancy (a mixed one measured its
+      // drain's parts at low occupancy, too short: profiles/r06g)
+      plan.budget = c->opt_mixed > 0 ? std::max(1ll, c->render_slots * c->opt_mixed / 100) : 0;
+      plan.slots = c->render_slots;
+      plan.max_lanes = (int)std::min<uint32_t>(8u, n_batches);
+      if (c->opt_mixed < 0) {
+        const int rm = mix_feedback(c, p, n_batches);
+        if (rm) return rm;
+        if (c->cost_ready) {
+          plan.cost = &c->block_cost;
+          plan.gen = c->cost_gen;
+        }
+      }
+    }
+    const int rc = compact_items(c, &p, mixed ? &plan : nullptr);
     if (rc) return rc;
+    c->last_mix = !mixed || !c->items_mixed ? 0 : plan.cost ? 2 : 1;
+    if (mixed && c->opt_mixed < 0 && c->cost_measure) {
+      // this launch measures its blocks' costs (mix_feedback)
+      PT_HIP(hipMemsetAsync(c->d_cost, 0, (size_t)p.blocks_total * 4 * sizeof(unsigned), c->stream));
+      p.cost_out = c->d_cost;
+      c->cost_lanes = c->block_lanes;
+    }
   }
   c->last = p;   // the item exchange (pt_items_*) follows the last rendered frame
   c->last_kernel = wf ? 3 : 1;
@@ -1042,6 +1349,13 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     PT_HIP(ptd::launch_wavefront(p, b, lds, c->stream, cnt, two ? c->wf_stream2 : nullptr, c->wf_fork, c->wf_join));
   } else {
     PT_HIP(ptd::launch_render(p, c->stats_mode, lds, c->stream, cnt));
+    if (p.cost_out) {
+      PT_HIP(hipMemcpyAsync(c->h_cost, c->d_cost, (size_t)p.blocks_total * 4 * sizeof(unsigned),
+                            hipMemcpyDeviceToHost, c->stream));
+      PT_HIP(hipEventRecord(c->cost_ev, c->stream));
+      c->cost_pending = true;
+      c->cost_measure = false;
+    }
     if (launched && pack_out && !c->stats_mode) {
       launched->p = p;
       launched->lds = lds;
@@ -1173,6 +1487,9 @@ int pt_destroy(pt_context* c) {
   if (c->own_accum) dev_free(c->d_accum);
   dev_free(c->d_stats);
   dev_free(c->d_items);
+  dev_free(c->d_cost);
+  if (c->h_cost) (void)hipHostFree(c->h_cost);
+  if (c->cost_ev) (void)hipEventDestroy(c->cost_ev);
   dev_free(c->d_pack_items);
   dev_free(c->d_unpack);
   dev_free(c->wf_block);
@@ -1311,6 +1628,7 @@ int pt_upload_scene(pt_context* c, const float* vertices, size_t n_vertex_floats
   memcpy(c->root_lo, lo, sizeof lo);
   memcpy(c->root_hi, hi, sizeof hi);
   c->has_scene = true;
+  c->scene_serial++;
   return PT_OK;
 }
 
@@ -1334,6 +1652,7 @@ int pt_upload_lights(pt_context* c, const pt_area_light* lights, size_t n) {
   }
   c->n_lights = (int)n;
   c->lights_host.assign(lights, lights + n);
+  c->scene_serial++;
   return PT_OK;
 }
 
@@ -1649,8 +1968,12 @@ int pt_set_option(pt_context* c, int key, int value) {
       if (value < 0) return fail(PT_ERR_INVALID, "PT_OPT_LAUNCH_TIMING takes 0 (off) or k >= 1 (every k-th launch)");
       c->opt_timing = value;
       return PT_OK;
+    case PT_OPT_MIXED_LANES:
+      if (value < -1 || value > 1000) return fail(PT_ERR_INVALID, "PT_OPT_MIXED_LANES takes -1 (auto), 0 (off) or 1-1000");
+      c->opt_mixed = value;
+      return PT_OK;
     case PT_OPT_ITEM_ORDER:
-      if (value != 0 && value != 1) return fail(PT_ERR_INVALID, "PT_OPT_ITEM_ORDER takes 0 or 1");
+      if (value < -1 || value > 1) return fail(PT_ERR_INVALID, "PT_OPT_ITEM_ORDER takes -1 (auto), 0 or 1");
       c->opt_item_order = value;
       return PT_OK;
     case PT_OPT_FRESH_BATCH0:
@@ -1794,6 +2117,16 @@ int pt_wide_info(pt_context* c, int info[2]) {
   info[0] = c->n_wide;
   info[1] = c->n_wide ? c->wide_stack : 0;
   if (!c->n_wide) g_err = c->wide_reason;
+  return PT_OK;
+}
+
+int pt_mixed_info(pt_context* c, int info[3]) {
+  if (!c || !info) return fail(PT_ERR_INVALID, "null argument");
+  info[0] = info[1] = info[2] = 0;
+  if (c->group) return PT_OK;
+  info[0] = c->last_mix;
+  info[1] = c->last_mix ? c->n_live_items : 0;
+  info[2] = c->cost_frames;
   return PT_OK;
 }
 

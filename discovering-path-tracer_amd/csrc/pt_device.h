@@ -143,7 +143,16 @@ struct RenderParams {
   int n_unpack;
   long long unpack_slot_f4;
   int item_order;   // host only: PT_OPT_ITEM_ORDER for the item lists
+  // mixed sample lanes (PT_OPT_MIXED_LANES, one-rank path-recursive launches
+  // with items): live item i is items_org[i] = {x | log2(spl_i) << 24, y}, a
+  // whole 16x16 tile at one lane per pixel or a part at `spl` lanes; the
+  // culled items keep `spl`
+  int mix = 0;
+  // per 16x4 part of the frame (y / 4 * blocks_x + x / 16): the summed wave
+  // durations of the launch's live workgroups in GPU wall-clock ticks, or null
+  unsigned* cost_out = nullptr;
 };
+constexpr int kMixShift = 24;
 constexpr int kMaxCullRects = 8;
 constexpr int kStatsWords = 9;   // RenderParams::stats
 
@@ -209,6 +218,8 @@ hipError_t launch_wavefront(const RenderParams& p, const WfBuffers& b, bool lds_
                             hipEvent_t ev_join = nullptr);
 // lanes of the wide walk's persistent grid on this device (overflow areas to allocate)
 long long wide_trace_lanes();
+// workgroups of the LDS-staged render kernel resident on this device at once
+long long render_slots(size_t lds_bytes);
 // triangle records by rank: dst[r] = tris[tri_of[r]]
 hipError_t launch_gather_tris(const float4* tris, const int* tri_of, int n, float4* dst, hipStream_t stream);
 hipError_t launch_math(int fn, const float* x, float* y, size_t n, hipStream_t stream);

@@ -840,6 +840,11 @@ __device__ __forceinline__ float fold_one(float a, float c, uint32_t batch) {
   return x / fb1;
 }
 
+#ifdef PT_WG_TRACE   // probe builds only (tools/r06_wg_trace.py): per live workgroup {t0, t1, hw_id << 32 | xcc | spl << 8, x0 << 32 | y0}
+constexpr int kWgTraceCap = 1 << 16;
+__device__ unsigned long long g_wg_trace[kWgTraceCap][4];
+#endif
+
 // LDS=true stages the whole scene (threaded nodes + triangle records) in LDS
 // once per workgroup; chosen by the host for scenes of at most a few tens of
 // KB (box.obj is 1.3 KB), where every lane re-reads the same few nodes.
@@ -868,26 +873,23 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
       fill_culled(P, P.culled_org, P.n_culled_items, (int)blockIdx.x - P.n_items);
     return;
   }
-  const int spl = P.spl;
   // item = (owned tile, part); with culling the host launches only items that
-  // can hold a live pixel, listed in P.items
-  const int wave = tid >> 6, lane = tid & 63;
-  // per wave: the leaf-candidate queue, then a [slot][lane] area that holds
-  // the path state parked during walks (kPark floats) and, between samples,
-  // the colour hand-off (4 floats) -- never both at once
-  __shared__ int cand_buf[4][kCand + (kPark > 4 ? kPark : 4)][64];
-  int* cand = &cand_buf[wave][0][lane];
-  float* colw = (float*)&cand_buf[wave][kCand][0];   // colour hand-off, [channel][lane]
-  const int q = wave * (64 / spl) + lane / spl;       // pixel within the workgroup
-  const int j = lane % spl;                           // sample slot
-  // the item's first pixel: host-computed with the item list (items_org),
-  // else from the tile order (every owned item, blockIdx.x = item)
+  // can hold a live pixel, listed in P.items.  With mixed lanes (P.mix) each
+  // live item carries its own lane count: whole tiles at one lane per pixel
+  // first (the cheapest per sample), parts at P.spl lanes after them (short
+  // workgroups that fill the launch's drain).  Uniform per workgroup.
+  // cost feedback (PT_OPT_MIXED_LANES' measured schedule): each wave adds
+  // its duration on the GPU wall clock to the counter of the 16x4 part of
+  // the frame its pixels lie in
+  const unsigned long long cost_t0 = P.cost_out ? wall_clock64() : 0ull;
   int gx0, gy0;
   bool tile_ok = true;
+  int spl = P.spl;
   if (P.items_org) {
     const int2 o = P.items_org[blockIdx.x];
-    gx0 = o.x;
+    gx0 = o.x & ((1 << kMixShift) - 1);
     gy0 = o.y;
+    if (P.mix) spl = 1 << (o.x >> kMixShift);
   } else {
     const int item = (int)blockIdx.x;
     const int tile = rank_tile(P, item / spl);
@@ -897,6 +899,18 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
     gy0 = by * 16 + (item % spl) * (16 / spl);
     tile_ok = tile < P.blocks_total;
   }
+#ifdef PT_WG_TRACE
+  const unsigned long long wg_t0 = wall_clock64();
+#endif
+  const int wave = tid >> 6, lane = tid & 63;
+  // per wave: the leaf-candidate queue, then a [slot][lane] area that holds
+  // the path state parked during walks (kPark floats) and, between samples,
+  // the colour hand-off (4 floats) -- never both at once
+  __shared__ int cand_buf[4][kCand + (kPark > 4 ? kPark : 4)][64];
+  int* cand = &cand_buf[wave][0][lane];
+  float* colw = (float*)&cand_buf[wave][kCand][0];   // colour hand-off, [channel][lane]
+  const int q = wave * (64 / spl) + lane / spl;       // pixel within the workgroup
+  const int j = lane % spl;                           // sample slot
   const int px = gx0 + q % 16;
   const int py = gy0 + q / 16;
   const bool active = tile_ok && px < P.width && py < P.height;   // :425-428
@@ -1045,6 +1059,25 @@ __global__ __launch_bounds__(256, LDS && !STATS ? PT_RENDER_MIN_BLOCKS_LDS : PT_
     }
   }
   emit_lane(P, active, pix, q, acc, spl, j);
+  if (!STATS && P.cost_out && lane == 0) {
+    // the wave's pixels lie in one 16x4 part: its first pixel row / 4
+    const int part_row = (gy0 + wave * (64 / spl) / 16) >> 2;
+    const unsigned long long dt = wall_clock64() - cost_t0;
+    atomicAdd(&P.cost_out[part_row * P.blocks_x + (gx0 >> 4)], (unsigned)(dt < 0xffffffull ? dt : 0xffffffull));
+  }
+#ifdef PT_WG_TRACE
+  if (!STATS && !CNT) {
+    __syncthreads();
+    if (tid == 0 && blockIdx.x < (unsigned)kWgTraceCap) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID: wave, SIMD, CU, SE
+      const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
+      g_wg_trace[blockIdx.x][0] = wg_t0;
+      g_wg_trace[blockIdx.x][1] = wall_clock64();
+      g_wg_trace[blockIdx.x][2] = (unsigned long long)hw << 32 | (unsigned long long)((xcc & 0xff) | (spl << 8));
+      g_wg_trace[blockIdx.x][3] = (unsigned long long)(unsigned)gx0 << 32 | (unsigned)gy0;
+    }
+  }
+#endif
   if (STATS) {
     const unsigned long long rays = wave_sum(c.rays), nodes = wave_sum(c.nodes), leaves = wave_sum(c.leaves);
     const unsigned long long smp = wave_sum((unsigned long long)nsamp);
@@ -2759,6 +2792,16 @@ hipError_t launch_render(const RenderParams& p, bool stats, bool lds_scene, hipS
   return hipGetLastError();
 }
 
+long long render_slots(size_t lds_bytes) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, render_kernel<false, true>, 256, lds_bytes) !=
+      hipSuccess)
+    return 0;
+  return (long long)cus * per_cu;
+}
+
 long long wide_trace_lanes() {
   int dev = 0, cus = 0, per_cu = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
@@ -2899,4 +2942,17 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
   return hipGetLastError();
 }
 
+#ifdef PT_WG_TRACE
+hipError_t wg_trace_read(unsigned long long* dst, int n) {
+  if (n > kWgTraceCap) n = kWgTraceCap;
+  const hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return e;
+  return hipMemcpyFromSymbol(dst, HIP_SYMBOL(g_wg_trace), (size_t)n * 32, 0, hipMemcpyDeviceToHost);
+}
+#endif
+
 }  // namespace ptd
+
+#ifdef PT_WG_TRACE
+extern "C" int pt_probe_wg_trace(unsigned long long* dst, int n) { return (int)ptd::wg_trace_read(dst, n); }
+#endif

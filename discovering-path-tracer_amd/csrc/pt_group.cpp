@@ -61,6 +61,7 @@ namespace {
 constexpr int kOptGroupExchange = 18;   // PT_OPT_GROUP_EXCHANGE (pathtracer.h)
 constexpr int kOptGroupCheck = 19;      // PT_OPT_GROUP_CHECK (pathtracer.h)
 constexpr int kOptCountTraced = 10;     // PT_OPT_COUNT_TRACED (pathtracer.h)
+constexpr int kOptLaunchTiming = 9;     // PT_OPT_LAUNCH_TIMING (pathtracer.h)
 
 }  // namespace
 
@@ -82,10 +83,13 @@ struct pt_group {
   int check = 1;                     // 0 never, 1 once per group (distinct devices), 2 every binding, 3 as 2, mismatch forced (tests)
   bool check_pending = false;        // armed by setup_frame, run by the next render
   bool check_passed = false;
-  int check_state = -1;              // -1 not run, 0 peer stores matched, 1 mismatch: staged copies in force
+  int check_state = -1;              // -1 not run, 0 peer stores matched, 1 mismatch: staged copies in force,
+                                     // 2 the peer-store probe failed: staged copies in force
   float check_ms[2] = {0.0f, 0.0f};  // the probe frames' wall time: peer stores, staged copies
   bool stats_mode = false;           // the members' counters (stats mode, PT_OPT_COUNT_TRACED) are off
   bool count_traced = false;         // during the probe frames and restored after
+  int timing = 1;                    // PT_OPT_LAUNCH_TIMING of the members (member 0's ring is the group's):
+                                     // off during the probe frames and restored after
   float* frame = nullptr;            // W x H float4 on dev[0]
   bool own_frame = false;
   int W = 0, H = 0;
@@ -234,10 +238,16 @@ bool distinct_devices(const pt_group* g) {
 // continues the accumulation (first batch > 0) reads the frame's history
 // whichever exchange was in force before.  arm: a new binding,
 // which the exchange check (PT_OPT_GROUP_CHECK) covers before it is used.
-int setup_frame(pt_group* g, bool arm = true) {
+// history: the frame holds an accumulation to continue (false right after
+// an allocation that a clear follows: no copy).
+int setup_frame(pt_group* g, bool arm = true, bool history = true) {
   G_RC(quiesce_all(g));
   free_exchange(g);
   g->staged = g->n > 1 && (g->exchange == 1 || !g->peer_ok);
+  if (g->staged && history) {   // the copies below follow the frame's last writer on s[0]
+    G_HIP(hipSetDevice(g->dev[0]));
+    G_HIP(hipEventRecord(g->start, g->s[0]));
+  }
   for (int r = 0; r < g->n; ++r) {
     pt_context* c = g->m[(size_t)r];
     if (r == 0 || !g->staged) {
@@ -247,9 +257,12 @@ int setup_frame(pt_group* g, bool arm = true) {
     G_RC(pt_resize_and_clear(c, g->W, g->H));   // +0 on its tiles, -0 elsewhere
     const size_t frame_bytes = (size_t)g->W * g->H * 16;
     G_HIP(hipSetDevice(g->dev[(size_t)r]));
-    // after the clear, on the member's stream: its tiles start from the frame's content
-    G_HIP(hipMemcpyPeerAsync(pt_accum_device_ptr(c), g->dev[(size_t)r], g->frame, g->dev[0], frame_bytes,
-                             g->s[(size_t)r]));
+    if (history) {
+      // after the clear, on the member's stream: its tiles start from the frame's content
+      G_HIP(hipStreamWaitEvent(g->s[(size_t)r], g->start, 0));
+      G_HIP(hipMemcpyPeerAsync(pt_accum_device_ptr(c), g->dev[(size_t)r], g->frame, g->dev[0], frame_bytes,
+                               g->s[(size_t)r]));
+    }
     int tiles = 0;
     G_RC(pt_tiles_owned(c, &tiles));
     const size_t bytes = (size_t)std::max(tiles, 1) * 256 * 16;
@@ -325,10 +338,12 @@ int check_exchange(pt_group* g) {
     gfree(g->dev[0], probe[1]);
   };
   // the probe frames are not the caller's frames: no stats or traced counts
+  // nor launch times in member 0's ring
   auto counters = [&](bool on) -> int {
     if (g->stats_mode) G_RC(each(g, [&](int r) { return pt_set_stats_mode(g->m[(size_t)r], on ? 1 : 0); }));
     if (g->count_traced)
       G_RC(each(g, [&](int r) { return pt_set_option(g->m[(size_t)r], kOptCountTraced, on ? 1 : 0); }));
+    G_RC(pt_set_option(g->m[0], kOptLaunchTiming, on ? g->timing : 0));
     return PT_OK;
   };
   auto body = [&]() -> int {
@@ -341,10 +356,18 @@ int check_exchange(pt_group* g) {
     }
     // peer stores: every member renders its tiles straight into probe[0]
     for (int r = 0; r < n; ++r) G_RC(pt_bind_accum(g->m[(size_t)r], probe[0], PW, PH));
+    // Production ordering: a frame's consumers see the members'
+    // stores only through s[0], which run_members makes wait for every
+    // member's completion event -- so the probe is read back on s[0] behind
+    // that wait, with no host-side synchronisation of the members first.
+    for (int k = 0; k < 2; ++k) host[k].resize(fbytes / 4);
     auto t0 = std::chrono::steady_clock::now();
     G_RC(run_members(g, 0, 1, false, probe[0], loc, root, bytes, false));
-    G_RC(quiesce_all(g));
+    G_HIP(hipSetDevice(g->dev[0]));
+    G_HIP(hipMemcpyAsync(host[0].data(), probe[0], fbytes, hipMemcpyDeviceToHost, g->s[0]));
+    G_HIP(hipStreamSynchronize(g->s[0]));
     auto t1 = std::chrono::steady_clock::now();
+    G_RC(quiesce_all(g));
     // staged copies into probe[1]
     G_RC(pt_bind_accum(g->m[0], probe[1], PW, PH));
     for (int r = 1; r < n; ++r) {
@@ -361,26 +384,31 @@ int check_exchange(pt_group* g) {
     G_RC(quiesce_all(g));
     auto t2 = std::chrono::steady_clock::now();
     G_RC(run_members(g, 0, 1, true, probe[1], loc, root, bytes, false));
-    G_RC(quiesce_all(g));
+    G_HIP(hipSetDevice(g->dev[0]));
+    G_HIP(hipMemcpyAsync(host[1].data(), probe[1], fbytes, hipMemcpyDeviceToHost, g->s[0]));
+    G_HIP(hipStreamSynchronize(g->s[0]));
     auto t3 = std::chrono::steady_clock::now();
+    G_RC(quiesce_all(g));
     g->check_ms[0] = std::chrono::duration<float, std::milli>(t1 - t0).count();
     g->check_ms[1] = std::chrono::duration<float, std::milli>(t3 - t2).count();
-    G_HIP(hipSetDevice(g->dev[0]));
-    for (int k = 0; k < 2; ++k) {
-      host[k].resize(fbytes / 4);
-      G_HIP(hipMemcpy(host[k].data(), probe[k], fbytes, hipMemcpyDeviceToHost));
-    }
     return PT_OK;
   };
   int rc = body();
   release();
   const int rc2 = counters(true);
   if (!rc) rc = rc2;
-  if (rc) {   // e.g. no scene yet: the render fails, and the check runs again on the next one
+  if (rc == PT_ERR_INVALID) {   // a precondition (no scene, camera or params yet): the render fails, and
+                                // the check runs again on the next one
     const std::string msg = pt_last_error();
     (void)setup_frame(g, false);
     g->check_pending = true;
     return pt_fail_internal(rc, "pt_create_multi exchange check: " + msg);
+  }
+  if (rc) {   // the probe itself failed: staged copies for good, and the render goes on
+    g->check_state = 2;
+    g->check_passed = false;
+    g->peer_ok = false;
+    return setup_frame(g, false);
   }
   if (g->check == 3) {
     uint32_t w;
@@ -534,7 +562,7 @@ int resize_and_clear(pt_group* g, int w, int h) {
     g->own_frame = true;
     g->W = w;
     g->H = h;
-    G_RC(setup_frame(g));
+    G_RC(setup_frame(g, true, false));   // uninitialised until the clear below: no history to copy
   }
   return clear_accum(g);
 }
@@ -614,6 +642,7 @@ int set_option(pt_group* g, int key, int value) {
   }
   G_RC(each(g, [&](int r) { return pt_set_option(g->m[(size_t)r], key, value); }));
   if (key == kOptCountTraced) g->count_traced = value != 0;
+  if (key == kOptLaunchTiming) g->timing = value;
   return PT_OK;
 }
 

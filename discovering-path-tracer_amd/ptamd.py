@@ -38,6 +38,7 @@ PT_OPT_GROUP_EXCHANGE = 18
 PT_OPT_GROUP_CHECK = 19
 PT_OPT_WF_GRID = 20
 PT_OPT_WF_REFILL = 21
+PT_OPT_MIXED_LANES = 22
 KERNEL_AUTO, KERNEL_RECURSIVE, KERNEL_WAVEFRONT = 0, 1, 3   # 2 (lane state machine) was removed
 
 # Every symbol include/pathtracer.h declares (tests check the .so exports them).
@@ -55,7 +56,7 @@ EXPORTS = [
     "pt_set_partition_slots", "pt_get_traced", "pt_wide_info", "pt_partition_items",
     "pt_dist_unique_id", "pt_dist_init", "pt_dist_run", "pt_dist_slot_floats", "pt_dist_finalize",
     "pt_dist_set_streams", "pt_dist_wait", "pt_dist_abort", "pt_create_multi", "pt_group_info",
-    "pt_group_check", "pt_dist_info",
+    "pt_group_check", "pt_dist_info", "pt_mixed_info",
 ]
 
 
@@ -111,6 +112,7 @@ def lib():
             "pt_tiles_unpack": ([vp, vp, i32, vp], i32), "pt_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
             "pt_reset_stats": ([vp], i32), "pt_get_traced": ([vp, ctypes.POINTER(Traced)], i32),
             "pt_wide_info": ([vp, ctypes.POINTER(ctypes.c_int)], i32),
+            "pt_mixed_info": ([vp, ctypes.POINTER(ctypes.c_int)], i32),
             "pt_partition_items": ([i32, i32, i32, i32, i32, vp, vp, i32, i32, vp, psz, vp, psz, vp], i32),
             "pt_dist_unique_id": ([vp, sz], i32), "pt_dist_init": ([vp, vp, i32, i32], i32),
             "pt_dist_run": ([vp, u32, i32, i32, vp, i32], i32), "pt_dist_slot_floats": ([vp, psz], i32),
@@ -561,6 +563,13 @@ class Renderer:
         if info[0] == 0:
             return 0, 0, lib().pt_last_error().decode()
         return info[0], info[1]
+
+    def mixed_info(self):
+        """(schedule, live workgroups, measured launches) of the last launch:
+        schedule 0 none, 1 static, 2 measured (PT_OPT_MIXED_LANES)."""
+        info = (ctypes.c_int * 3)()
+        _check(lib().pt_mixed_info(self._c, info), "pt_mixed_info")
+        return info[0], info[1], info[2]
 
     def last_launch_ms(self):
         ms = ctypes.c_float()

@@ -135,10 +135,15 @@ int pt_group_info(pt_context* ctx, int* n_devices, int* devices, int max_devices
  * *state -2 armed (runs on the next render), -1 not run (members on one
  * device, staged exchange in force, or a pt_create context), 0 the probe
  * frames matched bit for bit (peer stores in force), 1 they differed (the
- * staged exchange is in force from then on); the probe frames' wall times.
- * Cross-device bit identity of peer stores is verified by this check at run
- * time; it has not been observed on a multi-GPU node by this build (every
- * test so far ran its members on one device). */
+ * staged exchange is in force from then on), 2 the peer-store probe failed
+ * (a HIP error; staged exchange from then on, the render goes on); the probe
+ * frames' wall times.  The probe is read back the way a frame is consumed:
+ * on the first device's stream, behind its wait for every member's
+ * completion event, with no host synchronisation of the members before it.
+ * The check is meant to catch a cross-device visibility failure of peer
+ * stores at run time; it has not yet run on members of distinct devices
+ * (every test so far ran its members on one device), so whether it does is
+ * unverified. */
 int pt_group_check(pt_context* ctx, int* state, float* ms_peer, float* ms_staged);
 int pt_destroy(pt_context* ctx);
 /* Launch on a caller-owned hipStream_t (e.g. a torch.cuda.Stream's handle);
@@ -434,6 +439,23 @@ int pt_dist_finalize(pt_context* ctx);
  * traversal kernel claims new rays; 0 (default) = auto: 16 with a full grid,
  * 8 with PT_OPT_WF_GRID below 100.  Output is identical. */
 #define PT_OPT_WF_REFILL 21
+/* PT_OPT_MIXED_LANES: one-rank path-recursive launches of LDS-resident scenes
+ * (box.obj) with primary culling mix lane counts per workgroup: whole 16x16
+ * tiles at one lane per pixel (all samples of a pixel in one lane: the least
+ * work per sample, the longest workgroups) and tile parts at more lanes
+ * (short workgroups that fill the launch's drain).  -1 (default) = measured:
+ * until the frame's inputs have been measured, the first live tiles up to
+ * half of the workgroups the device holds at once run whole and the rest at
+ * PT_OPT_SAMPLE_LANES; render_kernel meanwhile times its blocks (two
+ * launches once the inputs are unchanged for a render, copied back without
+ * a host wait), and from then on every tile gets the fewest lanes that keep
+ * its workgroups short enough, longest first, the lane cut chosen by a
+ * simulation of the launch (pt_mixed_info reports the schedule).  A change of
+ * size, batches, camera, params, scene or lights starts over.  k = 1-1000:
+ * the static schedule with whole tiles for k % of the resident workgroups,
+ * never measured.  0 = off (every item at PT_OPT_SAMPLE_LANES).  Output is
+ * identical for every value. */
+#define PT_OPT_MIXED_LANES 22
 int pt_set_option(pt_context* ctx, int key, int value);
 /* The kernel the last pt_render / pt_dispatch ran (PT_OPT_KERNEL values 1-3,
  * after auto selection); 0 before the first render. */
@@ -463,6 +485,11 @@ int pt_get_traced(pt_context* ctx, pt_traced* out);
  * nodes (0 = not built; pt_last_error() then says why), info[1] = the most
  * stack entries one walk can hold. */
 int pt_wide_info(pt_context* ctx, int info[2]);
+/* Mixed sample lanes of the last path-recursive launch (PT_OPT_MIXED_LANES):
+ * info[0] = 0 uniform lanes, 1 the static mixed schedule, 2 the measured one;
+ * info[1] = live workgroups it launched; info[2] = measuring launches folded
+ * into the current inputs' block costs.  Multi-device contexts: zeros. */
+int pt_mixed_info(pt_context* ctx, int info[3]);
 /* Device time of the last pt_render/pt_dispatch launch, from HIP events
  * recorded on the launch stream. */
 int pt_last_launch_ms(pt_context* ctx, float* ms);

@@ -182,6 +182,56 @@ def test_box_1080p_8spp_bench_options_two_contexts():
         r.close()
 
 
+def test_mixed_lanes_static_and_measured_schedules():
+    """PT_OPT_MIXED_LANES (the one-context drop-in frame): live tiles at one
+    lane per pixel and tile parts at more lanes -- uniform lanes first, then
+    the schedule built from the measured block costs
+    (the cost feedback of two launches) -- each frame bitwise the oracle's
+    (raytrace_comp.comp:420-470); a camera change drops the measured costs.
+    pt_mixed_info: 0 uniform lanes (while measuring), 2 the measured
+    schedule."""
+    v, i, n = _box()
+    r = _setup(v, i, n)
+    r.resize_and_clear(1920, 1080)
+    ref, _ = _oracle(v, i, n, 1920, 1080, nb=8)
+    seen = set()
+    for k in range(12):
+        r.render(0, 8)
+        r.synchronize()
+        seen.add(r.mixed_info()[0])
+        if k in (0, 11):
+            _assert_same(r.read_accum(), ref, f"mixed lanes, frame {k}, schedule {r.mixed_info()}")
+    sched, items, measured = r.mixed_info()
+    assert sched == 2 and measured >= 2 and items > 0, r.mixed_info()
+    assert 0 in seen   # uniform lanes while the costs are measured
+    # another camera: back to the uniform schedule, same parity
+    cam2 = scenes.camera((0.4, 0.3, 4.0))
+    r.set_camera(cam2)
+    r.render(0, 8)
+    assert r.mixed_info()[0] == 0
+    ref2, _ = _oracle(v, i, n, 1920, 1080, nb=8, cam=cam2)
+    _assert_same(r.read_accum(), ref2, "mixed lanes after a camera change")
+
+
+@pytest.mark.parametrize("budget,spl,nb,first", [(50, 4, 8, 0), (1000, 4, 3, 2), (100, 8, 13, 0), (7, 2, 5, 1)])
+def test_mixed_lanes_static_budgets(budget, spl, nb, first):
+    """Static mixed schedules with every whole-tile budget, lane count and
+    sample count (fewer samples than lanes, progressive continuation over a
+    stale accumulator), ragged edge tiles."""
+    v, i, n = _box()
+    r = _setup(v, i, n)
+    r.set_option(ptamd.PT_OPT_MIXED_LANES, budget)
+    r.set_option(ptamd.PT_OPT_SAMPLE_LANES, spl)
+    W, H = 333, 250
+    r.resize_and_clear(W, H)
+    if first:
+        r.render(0, first)
+    r.render(first, nb)
+    assert r.mixed_info()[0] == 1
+    ref, _ = _oracle(v, i, n, W, H, first=0, nb=first + nb)
+    _assert_same(r.read_accum(), ref, f"mixed budget {budget} spl {spl} nb {nb} first {first}")
+
+
 def test_partition_sum_is_bit_exact():
     v, i, n = _box()
     W, H, nb = 200, 120, 2
