@@ -111,6 +111,13 @@ def kernel_sha1():
     return h.hexdigest()
 
 
+def leg_traffic(workload):
+    """The committed profile of a leg's workload taken in the configuration
+    the leg times (`<workload>_leg`, bench.py --leg), else the one-context
+    profile of the same workload."""
+    return profiled_traffic(workload + "_leg") or profiled_traffic(workload)
+
+
 def profiled_traffic(workload=None):
     """HBM bytes per launch (per frame for the wavefront pipeline) of the
     current kernel source from the newest committed rocprofv3 PMC summary
@@ -469,7 +476,7 @@ def price_leg(out, workload, traced, kernel_ms, alg, ref_rays):
     kernel source and camera): HBM (roofline_block), the wide walk's node
     fetches against the measured gather ceiling (configs 3/4 primary, config
     5 beside HBM) and VALU issue."""
-    prof = profiled_traffic(workload)
+    prof = leg_traffic(workload)
     gather = gather_roofline(workload, prof)
     if gather is not None:
         # the wide walk's node fetches against the measured ceiling of
@@ -506,6 +513,72 @@ def price_leg(out, workload, traced, kernel_ms, alg, ref_rays):
                                 "peak_basis": "1024 SIMDs x 2.4 GHz / 2 cycles per wave64 f32 instruction"}
 
 
+def leg_contexts(scene_name, W, H, depth, sss, device, contexts):
+    """A scene leg's contexts on one GPU: each with the scene, the reference
+    light and params, its own least-priority stream when there are several
+    (HipStream), launch timing on the first only.  Returns (contexts, their
+    HipStreams, the scene's frame-filling camera, int_bits, description,
+    triangles)."""
+    import ptamd
+    import scenes
+    scene, cam, int_bits, desc = load_scene(scene_name)
+    v, i, n, _, _ = scene.arrays()
+    del scene
+    ctxs = []
+    hip_streams = []
+    for _ in range(contexts):
+        x = ptamd.Renderer(device)
+        x.upload_scene(v, i, n, int_bits=int_bits)
+        x.upload_lights(scenes.REFERENCE_LIGHT)
+        x.set_params(depth, sss)
+        if contexts > 1:
+            hs = HipStream(device)
+            hip_streams.append(hs)
+            x.set_stream(hs.handle)
+        x.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 0 if ctxs else 1)
+        if ctxs:
+            x.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+        for kv in filter(None, os.environ.get("PT_BENCH_LEG_OPTS", "").split(",")):   # A/B of leg options
+            k, _, val = kv.partition("=")
+            x.set_option(int(k), int(val))
+        x.resize_and_clear(W, H)
+        ctxs.append(x)
+    return ctxs, hip_streams, cam, int_bits, desc, i.size // 3
+
+
+def leg_profile(key, which, device, steps):
+    """--leg KEY --leg-camera ref|ff: only the timed frames of one scene leg
+    at one camera, with the leg's own contexts and traversal grid (SCENE_LEGS)
+    -- one warmup frame per context, then `steps` frames alternating between
+    them -- for rocprofv3 (tools/profile_workload.sh, workloads *_leg): the
+    counters then come from the configuration the leg times (VERDICT r05
+    item 6).  Prints one line with the frame count the summary divides by."""
+    import ptamd
+    import scenes
+    import torch
+    entry = next(e for e in SCENE_LEGS if e[0] == key)
+    _, scene_name, W, H, spp, depth, _, workload, s_ref, s_ff = entry
+    nctx, grid = s_ref if which == "ref" else s_ff
+    ctxs, hip_streams, cam, _, _, _ = leg_contexts(scene_name, W, H, depth, 3, device, nctx)
+    camera = scenes.DEFAULT_CAMERA if which == "ref" else cam
+    for x in ctxs:
+        x.set_camera(camera)
+        x.set_option(ptamd.PT_OPT_WF_GRID, grid)
+        x.set_option(ptamd.PT_OPT_WF_TAIL, 0 if nctx > 1 else -1)
+        x.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+    for x in ctxs:
+        x.render(0, spp)
+    torch.cuda.synchronize()
+    walls = time_frames_pipelined(ctxs, spp, steps, groups=1)
+    print(json.dumps({"leg": key, "camera": which, "workload": workload + ("_refcam" if which == "ref" else ""),
+                      "contexts": nctx, "wf_grid_percent": grid, "frames": nctx + steps,
+                      "ms_per_step": round(float(np.median(walls)), 3)}), flush=True)
+    del ctxs
+    torch.cuda.synchronize()
+    for hs in hip_streams:
+        hs.close()
+
+
 def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaustive_too=False, contexts=1,
               setup_ref=None, setup_ff=None):
     """One BASELINE config on one GPU (N = 1 only), at two cameras: BASELINE's
@@ -530,31 +603,8 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
     setup_ref = setup_ref or (contexts, 100)
     setup_ff = setup_ff or (contexts, 100)
     contexts = max(setup_ref[0], setup_ff[0])
-    scene, cam, int_bits, desc = load_scene(scene_name)
-    v, i, n, _, _ = scene.arrays()
-    del scene
-    ctxs = []
-    hip_streams = []
-    for _ in range(contexts):
-        x = ptamd.Renderer(device)
-        x.upload_scene(v, i, n, int_bits=int_bits)
-        x.upload_lights(scenes.REFERENCE_LIGHT)
-        x.set_params(depth, sss)
-        if contexts > 1:
-            hs = HipStream(device)
-            hip_streams.append(hs)
-            x.set_stream(hs.handle)
-        if ctxs:
-            x.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
-            x.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 0)
-        for kv in filter(None, os.environ.get("PT_BENCH_LEG_OPTS", "").split(",")):   # A/B of leg options
-            k, _, val = kv.partition("=")
-            x.set_option(int(k), int(val))
-        x.resize_and_clear(W, H)
-        ctxs.append(x)
+    ctxs, hip_streams, cam, int_bits, desc, ntri = leg_contexts(scene_name, W, H, depth, sss, device, contexts)
     r = ctxs[0]
-    ntri = i.size // 3
-    del v, i, n
     setup_s = time.perf_counter() - t_setup
     base = desc.split(", camera")[0]
 
@@ -614,7 +664,7 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
                "unit": "Mrays/s", "ms_per_step": round(dt * 1e3, 2), "steps": steps, "warmup": 1,
                "ms_per_frame": spread(walls), "kernel_ms_per_frame": spread(kt) if kt.size else None,
                "kernel": kname, "config": cfg,
-               "roofline": roofline_block(profiled_traffic(wl), kernel_ms, alg, kname, kernel_ms, kernel_ms,
+               "roofline": roofline_block(leg_traffic(wl), kernel_ms, alg, kname, kernel_ms, kernel_ms,
                                           int(kt.size),
                                           f"median wall ms per frame of runs of {steps} frames alternating over "
                                           f"{nctx} contexts (frames overlap)" if nctx > 1 else
@@ -625,7 +675,7 @@ def scene_leg(scene_name, W, H, spp, depth, sss, steps, device, workload, exhaus
                "verified_vs_exhaustive_basis": f"the last timed frame (context 0) bitwise against the same frame "
                                                f"through the exhaustive walk (PT_OPT_WIDE 0): {ex_bad} floats differ"}
         price_leg(out, wl, traced, kernel_ms, alg, ref[0])
-        prof = profiled_traffic(wl)
+        prof = leg_traffic(wl)
         if prof is not None and prof[1].get("bench_line"):
             # the committed counters' run against the timed one: same
             # contexts and grid
@@ -1281,7 +1331,7 @@ def main():
     ap.add_argument("--sss", type=int, default=3, help="SSS_MAX_BOUNCES (reference 3)")
     ap.add_argument("--collective", choices=["gather", "reduce"], default="gather")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--verify", type=int, choices=[0, 1], default=None,
+    ap.add_argument("--verify", type=int, choices=[0, 1], default=None, nargs="?", const=1,
                     help="N>1: compare the assembled frame with a 1-GPU render (default on at N > 1)")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VAL",
                     help="pt_set_option before timing (A/B of output-invariant kernel options)")
@@ -1311,6 +1361,9 @@ def main():
     ap.add_argument("--group-devices", default=None,
                     help="comma-separated ordinals: also run the one-process pt_create_multi leg over them "
                          "(default at N > 1: the N devices, from rank 0; 'none' skips it)")
+    ap.add_argument("--leg", default=None, help="only the timed frames of one scene leg (config3/4/5; profiling)")
+    ap.add_argument("--leg-camera", choices=["ref", "ff"], default="ref",
+                    help="--leg: BASELINE's camera (0,0,5) or the scene's frame-filling one")
     ap.add_argument("--group-only", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--group-rays", type=float, default=float("nan"), help=argparse.SUPPRESS)
     ap.add_argument("--dry-run", action="store_true",
@@ -1341,6 +1394,10 @@ def main():
 
     if args.group_only:
         group_only(args)
+        return
+    if args.leg:
+        import torch  # noqa: F401 -- torch's HIP runtime first (libptamd binds to it)
+        leg_profile(args.leg, args.leg_camera, int(os.environ.get("PT_BENCH_DEVICE", "0")), args.steps)
         return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no launcher: N ranks of this same command under torch.distributed.run

@@ -305,6 +305,10 @@ struct DistState {
   float* ingest = nullptr;               // emulated root: stand-in for the other ranks' slots
   size_t slot_floats = 0, cap_floats = 0;
   std::vector<float> layout_key;         // frame_key of the layout the slots were sized for
+  // root: frame buffers that hold a whole assembled frame of a layout (its
+  // culled items' constant (0,0,0,1) included); later frames of that layout
+  // rebuild only their live items there (the culled bytes are the same)
+  std::vector<std::pair<const void*, std::vector<float>>> assembled;
   bool ready = false;
   bool caller_streams = false;           // pt_dist_set_streams gave render streams (then at most 2)
 };
@@ -409,6 +413,9 @@ struct pt_context {
   int* d_unpack = nullptr;      // per entry: rank, x0, y0, slot (-1 = culled)
   size_t unpack_cap = 0;
   int n_unpack = 0;
+  int* d_unpack_live = nullptr;   // the same table without the culled items' entries
+  size_t unpack_live_cap = 0;
+  int n_unpack_live = 0;
   std::vector<float> unpack_key;
   std::vector<float> packed_key;   // frame parameters of the last pt_render_packed
   std::vector<float> key_scratch, items_scratch;   // per-launch keys, built without reallocating
@@ -988,10 +995,16 @@ int unpack_table(pt_context* c, const ptd::RenderParams& p, const std::vector<fl
     for (size_t i = 0; i < live.size(); ++i) add(live[i], (int)i);
     for (int it : culled) add(it, -1);
   }
+  std::vector<int> live_only;
+  for (size_t k = 0; k + 3 < table.size(); k += 4)
+    if (table[k + 3] >= 0) live_only.insert(live_only.end(), table.begin() + k, table.begin() + k + 4);
   { const int rc_ = quiesce(c); if (rc_) return rc_; }
   const int rc = upload_ints(table, &c->d_unpack, &c->unpack_cap);
   if (rc) return rc;
+  const int rl = upload_ints(live_only, &c->d_unpack_live, &c->unpack_live_cap);
+  if (rl) return rl;
   c->n_unpack = (int)(table.size() / 4);
+  c->n_unpack_live = (int)(live_only.size() / 4);
   c->unpack_key = key;
   return PT_OK;
 }
@@ -1492,6 +1505,7 @@ int pt_destroy(pt_context* c) {
   if (c->cost_ev) (void)hipEventDestroy(c->cost_ev);
   dev_free(c->d_pack_items);
   dev_free(c->d_unpack);
+  dev_free(c->d_unpack_live);
   dev_free(c->wf_block);
   for (auto& r : c->rb) {
     dev_free(r.dev);
@@ -2798,6 +2812,22 @@ int pt_dist_info(pt_context* c, int* comm_ranks, int* nranks, int* rank) {
   return PT_OK;
 }
 
+// Whether frame buffer `frame` already holds a whole assembled frame of the
+// layout `key` (its culled items' constant included).
+static bool dist_assembled(const DistState* d, const void* frame, const std::vector<float>& key) {
+  for (const auto& e : d->assembled)
+    if (e.first == frame) return e.second == key;
+  return false;
+}
+static void dist_mark_assembled(DistState* d, const void* frame, const std::vector<float>& key) {
+  for (auto& e : d->assembled)
+    if (e.first == frame) {
+      e.second = key;
+      return;
+    }
+  d->assembled.push_back({frame, key});
+}
+
 int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, void* frames, int n_frame_bufs) {
   if (c && c->group) return fail(PT_ERR_UNSUPPORTED, "pt_dist_run: not on a multi-device context (pt_create_multi)");
   if (!c) return fail(PT_ERR_INVALID, "null context");
@@ -2872,9 +2902,18 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, 
       p.pack_out = out;
       p.unpack_src = (const float4*)as.src;
       p.unpack_frame = (float4*)as.frame;
+      if (as.src && dist_assembled(d, as.frame, c->unpack_key)) {   // live items only
+        p.unpack_table = c->d_unpack_live;
+        p.n_unpack = c->n_unpack_live;
+      } else if (as.src) {
+        p.unpack_table = c->d_unpack;
+        p.n_unpack = c->n_unpack;
+        dist_mark_assembled(d, as.frame, c->unpack_key);
+      }
       rc = relaunch(c, p, t.lds, t.cnt);
     } else {
-      rc = render_impl(c, 0, n_batches, out, as, &t);
+      rc = render_impl(c, 0, n_batches, out, as, &t);   // a whole assembly (the full table)
+      if (rc == PT_OK && as.src) dist_mark_assembled(d, as.frame, c->unpack_key);
     }
     if (rc) break;
     PT_HIP(hipEventRecord(d->render_done[b], c->stream));
@@ -2903,8 +2942,11 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, 
       c->stream = d->streams[k % n_streams];
       PT_HIP(hipStreamWaitEvent(c->stream, d->gather_done[b], 0));
       float4* out = (float4*)((float*)frames + (size_t)(k % n_frame_bufs) * frame_f);
-      PT_HIP(ptd::launch_items_unpack(c->last, out, (const float4*)d->recv[b], slot / 4, c->d_unpack, c->n_unpack,
-                                      c->stream));
+      const bool live_only = dist_assembled(d, out, c->unpack_key);
+      PT_HIP(ptd::launch_items_unpack(c->last, out, (const float4*)d->recv[b], slot / 4,
+                                      live_only ? c->d_unpack_live : c->d_unpack,
+                                      live_only ? c->n_unpack_live : c->n_unpack, c->stream));
+      if (!live_only) dist_mark_assembled(d, out, c->unpack_key);
     }
   }
   // one use event per stream for the whole run (the launches above skip theirs)

@@ -185,6 +185,62 @@ def test_native_loop_back_to_back_calls(streams):
     r.dist_finalize()
 
 
+def test_native_loop_assembles_culled_items_once_per_buffer_and_layout():
+    """The root writes a frame buffer's culled items -- the constant
+    (0,0,0,1) -- in its first whole assembly of a layout and afterwards
+    rebuilds only the live items there.  Buffers new to
+    the loop, and every buffer after a camera change (another culled set),
+    get a whole assembly again: each must hold the single-GPU frame."""
+    import numpy as np
+    import torch
+    import ptamd
+    import scenes
+    scene = ptamd.Scene.load_obj(scenes.BOX_OBJ).build_bvh()
+    v, i, n, _, _ = scene.arrays()
+    cam2 = scenes.camera((0.5, -0.3, 3.5))
+
+    def setup(cam):
+        r = ptamd.Renderer(0)
+        r.upload_scene(v, i, n)
+        r.upload_lights(scenes.REFERENCE_LIGHT)
+        r.set_camera(cam)
+        r.set_params(4, 3)
+        r.resize_and_clear(320, 200)
+        return r
+
+    def want(cam):
+        one = setup(cam)
+        one.render(0, 4)
+        return one.read_accum().view(np.uint32).copy()
+
+    w1, w2 = want(scenes.DEFAULT_CAMERA), want(cam2)
+    assert not np.array_equal(w1, w2)
+    r = setup(scenes.DEFAULT_CAMERA)
+    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+    r.render(0, 4)   # fixes the item layout
+    r.dist_init(ptamd.Renderer.dist_unique_id(), 1, 0)
+
+    def check(frames, w, what):
+        r.dist_wait(30000)
+        r.synchronize()
+        for f in range(frames.shape[0]):
+            got = frames[f].cpu().numpy().reshape(-1).view(np.uint32)
+            assert np.array_equal(got, w), f"{what}, frame buffer {f}"
+
+    a = torch.full((3, 200, 320, 4), float("nan"), dtype=torch.float32, device="cuda:0")
+    r.dist_run(4, 5, a.data_ptr(), 3, n_streams=3)
+    r.dist_run(4, 4, a.data_ptr(), 3, n_streams=3)   # live items only: the culled constants stay
+    check(a, w1, "same buffers, same layout")
+    b = torch.full((3, 200, 320, 4), float("nan"), dtype=torch.float32, device="cuda:0")
+    r.dist_run(4, 4, b.data_ptr(), 3, n_streams=3)   # new buffers: whole assemblies
+    check(b, w1, "new buffers")
+    r.set_camera(cam2)
+    r.render(0, 4)
+    r.dist_run(4, 5, a.data_ptr(), 3, n_streams=3)   # another culled set: whole assemblies again
+    check(a, w2, "after a camera change")
+    r.dist_finalize()
+
+
 def test_bench_group_leg_members_on_one_device():
     """bench.py's pt_create_multi leg with two members
     on device 0: both exchanges timed and each last frame bitwise the

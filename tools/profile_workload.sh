@@ -20,6 +20,14 @@ case $WORKLOAD in
   sphere_1080p8_refcam) ARGS="--scene sphere --camera reference --steps 2 --warmup 1"; STEPS=2; WARM=1 ;;
   sphere_4k16_d8_refcam) ARGS="--scene sphere --camera reference --width 3840 --height 2160 --spp 16 --depth 8 --steps 1 --warmup 1"; STEPS=1; WARM=1 ;;
   synthetic10M_1080p8_refcam) ARGS="--scene synthetic:10000000 --camera reference --steps 1 --warmup 1"; STEPS=1; WARM=1 ;;
+  # the legs as bench.py times them (--leg: their contexts and traversal
+  # grid, frames in flight; SCENE_LEGS): WARM = one frame per context
+  sphere_1080p8_refcam_leg) ARGS="--leg config3 --leg-camera ref --steps 12"; STEPS=12; WARM=4 ;;
+  sphere_1080p8_leg) ARGS="--leg config3 --leg-camera ff --steps 12"; STEPS=12; WARM=4 ;;
+  sphere_4k16_d8_refcam_leg) ARGS="--leg config4 --leg-camera ref --steps 6"; STEPS=6; WARM=2 ;;
+  sphere_4k16_d8_leg) ARGS="--leg config4 --leg-camera ff --steps 6"; STEPS=6; WARM=2 ;;
+  synthetic10M_1080p8_refcam_leg) ARGS="--leg config5 --leg-camera ref --steps 12"; STEPS=12; WARM=3 ;;
+  synthetic10M_1080p8_leg) ARGS="--leg config5 --leg-camera ff --steps 12"; STEPS=12; WARM=2 ;;
   *) echo "unknown WORKLOAD $WORKLOAD"; exit 2 ;;
 esac
 OUT=gpurun_out/prof_${TAG}_${WORKLOAD}
