@@ -461,7 +461,8 @@ struct pt_context {
   hipEvent_t ring[kRing][2] = {};
   int ring_n = 0;
   int last_slot = 0;          // ring slot of the newest launch (pt_last_launch_ms)
-  int opt_timing = 1;         // PT_OPT_LAUNCH_TIMING: event pair on every k-th launch, 0 = none
+  int opt_timing = 0;         // PT_OPT_LAUNCH_TIMING: event pair on every k-th launch, 0 = none (default:
+                              // a pair costs the one-stream frame ~10 us, profiles/r06a)
   long long launch_n = 0;     // render launches since pt_reset_launch_times
   long long ring_launch[kRing] = {};   // launch number of each recorded pair
   DistState* dist = nullptr;           // pt_dist_init
@@ -691,112 +692,70 @@ static void mixed_origins(const ptd::RenderParams& p, const ptd::Part& part, con
 static const double kLaneInfl[4] = {1.0, 0.2121 / 0.2037, 0.2385 / 0.2037, 0.2775 / 0.2037};
 
 // The measured schedule of mixed lanes.  cost[k], k = y / 4 * blocks_x +
-// x / 16: the live work of the frame's 16x4 part k at one lane per pixel, in
-// wave time (render_kernel's cost feedback: every wave's duration added to
-// its part, divided by the lane factor it ran at).  A wave covers one part
-// at one lane per pixel, half of one at two, and so on, so a workgroup at s
-// lanes runs ~max over the parts it covers of cost * kLaneInfl[s] / s.
-// Whole-live tiles take the fewest lanes that keep their workgroups at most
-// Dmax long; tiles with culled parts keep their live parts at p.spl.  Items
-// go longest first, and the launch is simulated as greedy list scheduling
-// on `slots` resident workgroups for a range of Dmax; the shortest simulated
-// frame wins.  Any item order and lane count gives the same image.
+// x / 16: the live work of the frame's 16x4 part k at one lane per pixel
+// (render_kernel's cost feedback: every wave's duration added to the part
+// its pixels lie in, divided by the lane factor it ran at).  A workgroup at s
+// lanes lasts about the costliest part it covers * kLaneInfl[s] / s.
+// Whole-live tiles run as 16x8 halves at kWholeLanes = 2 lanes -- the least
+// work per sample whose workgroups fit inside a frame: at one lane the
+// costliest tiles outlast the whole frame at two -- and the live parts of
+// tiles with culled parts at p.spl lanes.  Every item goes longest first
+// (longest-processing-time list scheduling on the measured costs), so the
+// launch ends on its lightest items.  Box 1080p 8 spp, one context
+// (profiles/r06h, r06i): 0.2214 ms per frame against 0.2416 at 4 lanes in
+// the same order and 0.2349 for the best static mix (whole tiles at one lane
+// for half the resident workgroups); whole tiles at one lane as well lost
+// (0.2620: they outlast the frame), and so did splitting the last 5-35 % of
+// the work into 4-lane parts for a finer drain (+1 to +5 %).  Any item order
+// and lane count gives the same image.
 struct MixItem {
   int x, y;
   double dur;
 };
+constexpr int kWholeLanes = 2;
 static void measured_origins(const ptd::RenderParams& p, const ptd::Part& part, const std::vector<int>& live,
-                             const std::vector<double>& cost, long long slots, int max_lanes,
-                             std::vector<int>* org) {
+                             const std::vector<double>& cost, std::vector<int>* org) {
   const int spl = p.spl, rows = 16 / spl, lg_base = __builtin_ctz((unsigned)spl);
+  const int lanes = std::min(kWholeLanes, spl), lg_whole = __builtin_ctz((unsigned)lanes), hrows = 16 / lanes;
   const int tiles = ptd::part_count(part, p.blocks_total);
   std::vector<int> parts_live(tiles, 0);
   for (int it : live) parts_live[it / spl]++;
-  struct Tile {
-    int x, y, nlive;
-    double c[4];
-    std::vector<int> parts;
-  };
-  std::vector<Tile> tl;
-  std::vector<int> index(tiles, -1);
   auto part_cost = [&](int x, int y) {   // pixel (x, y)'s 16x4 part
     const size_t k = (size_t)(y >> 2) * p.blocks_x + (x >> 4);
     return k < cost.size() ? std::max(1.0, cost[k]) : 1.0;
   };
+  auto span_cost = [&](int x, int y, int nrows) {   // the costliest 16x4 part of rows [y, y + nrows)
+    double c = 0;
+    for (int yy = y; yy < y + std::max(nrows, 4); yy += 4) c = std::max(c, part_cost(x, yy));
+    return c;
+  };
+  std::vector<char> seen(tiles, 0);
+  std::vector<MixItem> items;
   for (int it : live) {
     const int li = it / spl;
-    if (index[li] < 0) {
-      int bx, by;
-      ptd::tile_block(ptd::part_tile(part, li), p.blocks_x, &bx, &by);
-      index[li] = (int)tl.size();
-      Tile t{bx * 16, by * 16, parts_live[li], {0, 0, 0, 0}, {}};
-      for (int k = 0; k < 4; ++k) t.c[k] = part_cost(t.x, t.y + 4 * k);
-      tl.push_back(t);
+    int bx, by;
+    ptd::tile_block(ptd::part_tile(part, li), p.blocks_x, &bx, &by);
+    const int x = bx * 16, y = by * 16;
+    if (parts_live[li] == spl) {   // a whole-live tile: its halves, once
+      if (seen[li]) continue;
+      seen[li] = 1;
+      for (int h = 0; h < lanes; ++h)
+        items.push_back({x | (lg_whole << ptd::kMixShift), y + h * hrows,
+                         span_cost(x, y + h * hrows, hrows) * kLaneInfl[lg_whole] / lanes});
+      continue;
     }
-    tl[index[li]].parts.push_back(it % spl);
+    const int yp = y + (it % spl) * rows;
+    items.push_back({x | (lg_base << ptd::kMixShift), yp, span_cost(x, yp, rows) * kLaneInfl[lg_base] / spl});
   }
-  double total = 0;
-  for (const Tile& t : tl)
-    for (double x : t.c) total += x;
-  const double lb = total / (4.0 * (double)std::max(1ll, slots));   // one lane per pixel, perfectly packed
-  std::vector<MixItem> best, items;
-  double best_span = 1e300;
-  std::vector<double> heap;
-  for (double f : {1e9, 2.0, 1.5, 1.2, 1.0, 0.85, 0.75, 0.6, 0.5, 0.35, 0.25, 0.18, 0.12}) {
-    const double dmax = lb * f;
-    items.clear();
-    for (const Tile& t : tl) {
-      if (t.nlive != spl) {   // culled parts: the live parts at p.spl (a part spans 4 / spl of the 16x4 parts)
-        for (int part_i : t.parts) {
-          const int y = t.y + part_i * rows;
-          double c = 0;
-          for (int yy = y; yy < y + rows; yy += 4) c = std::max(c, t.c[(yy - t.y) >> 2]);
-          if (rows < 4) c = t.c[(y - t.y) >> 2];
-          items.push_back({t.x | (lg_base << ptd::kMixShift), y, c * kLaneInfl[lg_base] / spl});
-        }
-        continue;
-      }
-      // the fewest lanes whose longest workgroup fits dmax
-      int lg = 0;
-      for (;; ++lg) {
-        const int s = 1 << lg, wrows = 16 / s;
-        double longest = 0;
-        for (int k = 0; k < 4; ++k) longest = std::max(longest, t.c[k]);
-        if (s >= max_lanes || longest * kLaneInfl[lg] / s <= dmax) {
-          for (int w = 0; w < s; ++w) {   // workgroup w: rows [w * wrows, (w + 1) * wrows)
-            double c = 0;
-            for (int yy = w * wrows; yy < (w + 1) * wrows; yy += 4) c = std::max(c, t.c[yy >> 2]);
-            if (wrows < 4) c = t.c[(w * wrows) >> 2];
-            items.push_back({t.x | (lg << ptd::kMixShift), t.y + w * wrows, c * kLaneInfl[lg] / s});
-          }
-          break;
-        }
-      }
-    }
-    std::stable_sort(items.begin(), items.end(), [](const MixItem& a, const MixItem& b) { return a.dur > b.dur; });
-    // greedy list scheduling: each item on the earliest free slot
-    heap.assign((size_t)std::max(1ll, slots), 0.0);
-    double span = 0;
-    for (const MixItem& m : items) {
-      std::pop_heap(heap.begin(), heap.end(), std::greater<double>());
-      heap.back() += m.dur;
-      span = std::max(span, heap.back());
-      std::push_heap(heap.begin(), heap.end(), std::greater<double>());
-    }
-    if (span < best_span * 0.999) {
-      best_span = span;
-      best = items;
-    }
-  }
-  for (const MixItem& m : best) {
+  std::stable_sort(items.begin(), items.end(), [](const MixItem& a, const MixItem& b) { return a.dur > b.dur; });
+  for (const MixItem& m : items) {
     org->push_back(m.x);
     org->push_back(m.y);
   }
-  if (const char* dump = getenv("PT_MIX_DUMP")) {   // diagnostics: part costs and the chosen schedule
+  if (const char* dump = getenv("PT_MIX_DUMP")) {   // diagnostics: the chosen schedule and its predicted durations
     if (FILE* f = fopen(dump, "w")) {
-      fprintf(f, "# slots %lld lb %.1f best_span %.1f items %zu\n", slots, lb, best_span, best.size());
-      for (const Tile& t : tl) fprintf(f, "T %d %d %d %.1f %.1f %.1f %.1f\n", t.x, t.y, t.nlive, t.c[0], t.c[1], t.c[2], t.c[3]);
-      for (const MixItem& m : best)
+      fprintf(f, "# items %zu\n", items.size());
+      for (const MixItem& m : items)
         fprintf(f, "I %d %d %d %.1f\n", m.x & ((1 << ptd::kMixShift) - 1), m.y, m.x >> ptd::kMixShift, m.dur);
       fclose(f);
     }
@@ -866,15 +825,13 @@ static int mix_feedback(pt_context* c, const ptd::RenderParams& p, uint32_t n_ba
   return PT_OK;
 }
 
-// How a launch mixes lane counts (render_impl): a static budget of whole
-// tiles (mixed_origins) until block costs are measured, then the measured
-// schedule (measured_origins).
+// How a launch mixes lane counts (render_impl): PT_OPT_MIXED_LANES k > 0, a
+// static budget of whole tiles (mixed_origins); -1, uniform lanes until the
+// part costs are measured, then the measured schedule (measured_origins).
 struct MixPlan {
   long long budget = 0;                       // whole tiles of the static schedule
-  const std::vector<double>* cost = nullptr;  // measured block costs, or null
+  const std::vector<double>* cost = nullptr;  // measured part costs, or null
   int gen = 0;                                // measured schedule generation (cache key)
-  long long slots = 0;
-  int max_lanes = 8;
 };
 
 static int compact_items(pt_context* c, ptd::RenderParams* p, const MixPlan* mix = nullptr) {
@@ -912,7 +869,7 @@ static int compact_items(pt_context* c, ptd::RenderParams* p, const MixPlan* mix
     if (mix && p->spl > 1 && (mix->cost || mix->budget > 0)) {
       std::vector<int> org;
       if (mix->cost)
-        measured_origins(*p, pt, live, *mix->cost, mix->slots, mix->max_lanes, &org);
+        measured_origins(*p, pt, live, *mix->cost, &org);
       else
         mixed_origins(*p, pt, live, mix->budget, &org);
       c->h_items.insert(c->h_items.end(), org.begin(), org.end());
@@ -1237,8 +1194,6 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
       // workgroups nearly all run at full occupancy (a mixed one measured its
       // drain's parts at low occupancy, too short: profiles/r06g)
       plan.budget = c->opt_mixed > 0 ? std::max(1ll, c->render_slots * c->opt_mixed / 100) : 0;
-      plan.slots = c->render_slots;
-      plan.max_lanes = (int)std::min<uint32_t>(8u, n_batches);
       if (c->opt_mixed < 0) {
         const int rm = mix_feedback(c, p, n_batches);
         if (rm) return rm;

@@ -33,8 +33,11 @@ extern "C" {
 /* ABI history.  2 (round 5): pt_group_check, pt_dist_info and
  * PT_OPT_GROUP_CHECK added; option values removed since 1 now return
  * PT_ERR_UNSUPPORTED: PT_OPT_KERNEL 2, PT_OPT_SM_BATCH, PT_OPT_PAIRS 1,
- * PT_OPT_WIDE_NODE 80 (kernels measured slower on every scene). */
-#define PT_ABI_VERSION 2
+ * PT_OPT_WIDE_NODE 80 (kernels measured slower on every scene).
+ * 3 (round 6): pt_mixed_info and PT_OPT_MIXED_LANES added; defaults changed:
+ * PT_OPT_LAUNCH_TIMING 0 (was 1), PT_OPT_ITEM_ORDER -1 auto (was 1);
+ * pt_group_check state 2 (probe failed). */
+#define PT_ABI_VERSION 3
 
 enum {
   PT_OK = 0,
@@ -355,13 +358,17 @@ int pt_dist_finalize(pt_context* ctx);
  * one batch of the frame per chunk).
  * Output is identical for every value. */
 #define PT_OPT_WF_PATHS 7
-/* PT_OPT_ITEM_ORDER: 1 (default) = live items (tile parts) launched heaviest
- * first by a host estimate (pixels inside the root box's rectangle), so long
- * workgroups start early and short ones fill the tail; 0 = scan order.  The
- * packed exchange layout follows the same order.  Output is identical. */
+/* PT_OPT_ITEM_ORDER: 1 = live items (tile parts) launched heaviest first by
+ * a host estimate (pixels inside the root box's rectangle), so long
+ * workgroups start early and short ones fill the tail; 0 = scan order; -1
+ * (default) = auto: scan order for a whole frame on the path-recursive
+ * kernel, heaviest first on a share of the frame and on the wavefront
+ * pipeline.  The packed exchange layout follows the same order.  Output is
+ * identical. */
 #define PT_OPT_ITEM_ORDER 8
 /* PT_OPT_LAUNCH_TIMING: record a HIP event pair around every k-th render
- * launch (default 1; 0 = none) for pt_last_launch_ms / pt_launch_times_ms /
+ * launch (0 = none, the default since ABI 3: on one stream a pair cost the box
+ * frame ~10 us of its ~0.25 ms) for pt_last_launch_ms / pt_launch_times_ms /
  * pt_launch_span_ms.  Output-invariant. */
 #define PT_OPT_LAUNCH_TIMING 9
 /* PT_OPT_COUNT_TRACED: 1 = run the fast kernels with counters of the work

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in decl if not hasattr(L, s)]
     assert not missing, missing
     assert sorted(decl) == sorted(ptamd.EXPORTS)
-    assert ptamd.lib().pt_abi_version() == 2   # 2: round 5 (pathtracer.h ABI history)
+    assert ptamd.lib().pt_abi_version() == 3   # 3: round 6 (pathtracer.h ABI history)
 
 
 def test_no_gpu_fails_loudly():

@@ -78,6 +78,7 @@ def main():
             ref = img
         elif not np.array_equal(img.view(np.uint32), ref.view(np.uint32)):
             print(f"WARNING: variant {name} output differs from {rs[0][0]}")
+        r.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 1)
         r.reset_launch_times()
     for _ in range(a.reps):
         for name, r in rs:
