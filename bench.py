@@ -1029,8 +1029,11 @@ def compact_leg(leg):
     if "error" in leg and "value" not in leg:
         return {"error": str(leg["error"])[:300]}
     if "n_gpus" in leg:   # a distributed leg
-        return {"value": leg.get("value"), "ms_per_step": leg.get("ms_per_step"), "n_gpus": leg.get("n_gpus"),
-                "verified": leg.get("verified_bitwise_vs_single_gpu"), "error": leg.get("error")}
+        out = {"value": leg.get("value"), "ms_per_step": leg.get("ms_per_step"), "n_gpus": leg.get("n_gpus"),
+               "verified": leg.get("verified_bitwise_vs_single_gpu")}
+        if leg.get("error"):
+            out["error"] = str(leg["error"])[:300]
+        return out
     out = _leg_camera(leg)
     ff = leg.get("frame_filling_camera")
     if ff:

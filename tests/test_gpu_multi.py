@@ -12,6 +12,7 @@ import os
 import socket
 import subprocess
 import sys
+import tempfile
 
 import pytest
 
@@ -27,12 +28,23 @@ def _run(cmd, env, timeout=180):
     # a collective one rank never reaches fails after 90 s with the others'
     # stacks (bench.py's process-group timeout), inside the test's own limit
     env = dict(env, PT_BENCH_TRACEBACK_AFTER_S=str(timeout - 30), PT_BENCH_PG_TIMEOUT_S="90")
+    env.setdefault("PT_BENCH_DETAIL", os.path.join(tempfile.mkdtemp(prefix="ptbench"), "detail.json"))
     try:
         return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
     except subprocess.TimeoutExpired as e:
         def tail(x):
             return (x.decode(errors="replace") if isinstance(x, bytes) else (x or ""))[-6000:]
         raise AssertionError(f"timed out after {timeout} s\nstdout:\n{tail(e.stdout)}\nstderr:\n{tail(e.stderr)}")
+
+
+def _record(res):
+    """bench.py's full record of a run: the last stdout line is the compact
+    line the driver parses (at most bench.LINE_MAX_BYTES), naming the detail
+    file that holds the full record."""
+    last = res.stdout.strip().splitlines()[-1]
+    assert len(last) <= 6144, len(last)
+    line = json.loads(last)
+    return json.load(open(line["detail_file"]))
 
 
 # torchrun --standalone binds its rendezvous store to a port of its own
@@ -64,9 +76,7 @@ def test_two_rank_bench_verifies_bitwise(collective, extra):
            "--no-scene-legs", "--collective", collective] + extra
     res = _run(cmd, env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
-    lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
-    assert lines, res.stdout[-2000:]
-    out = json.loads(lines[-1])
+    out = _record(res)
     assert out["n_gpus"] == 2
     assert out["verified_bitwise_vs_single_gpu"] is True
     assert out["config"]["rays_traced"] > 0
@@ -85,7 +95,7 @@ def test_native_step_loop_single_rank_rccl(streams):
            "--no-scene-legs", "--no-cpu-baseline", "--streams", str(streams)]
     res = _run(cmd, env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
-    out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
+    out = _record(res)
     assert out["config"]["step_loop"].startswith("native"), res.stderr[-2000:]
     assert out["verified_bitwise_vs_single_gpu"] is True
 
@@ -112,7 +122,7 @@ def test_native_step_loop_two_ranks_grouped_send_recv(streams):
            "--no-scene-legs", "--streams", str(streams)]
     res = _run(cmd, env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
-    out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
+    out = _record(res)
     assert out["n_gpus"] == 2
     assert out["config"]["step_loop"] == "native (pt_dist_run, PT_RCCL_LIB stand-in)", res.stderr[-2000:]
     assert out["verified_bitwise_vs_single_gpu"] is True
@@ -132,7 +142,7 @@ def test_two_rank_scene_legs_reduce_bitwise():
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1"]
     res = _run(cmd, env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
-    out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
+    out = _record(res)
     legs = out["configs"]
     assert set(legs) == {"config4", "config5"}, legs
     for key, leg in legs.items():
@@ -250,7 +260,7 @@ def test_bench_group_leg_members_on_one_device():
            "--no-cpu-baseline", "--group-devices", "0,0"]
     res = _run(cmd, env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-4000:]
-    out = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
+    out = _record(res)
     g = out["group_leg"]
     assert g["devices"] == [0, 0]
     for k in ("exchange0", "exchange1"):
