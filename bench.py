@@ -1099,7 +1099,7 @@ def compact_line(full, detail_path=None):
             out["cpu_baseline"]["single_thread_value"] = cb["single_thread"].get("value")
     sc = full.get("single_context")
     if sc:
-        out["single_context"] = {k: sc.get(k) for k in ("value", "ms_per_step", "steps", "kernel_ms",
+        out["single_context"] = {k: sc.get(k) for k in ("value", "ms_per_step", "steps", "kernel_ms", "schedule",
                                                         "verified_vs_oracle", "error") if sc.get(k) is not None}
     if full.get("primary_cull_off"):
         out["primary_cull_off_ms"] = full["primary_cull_off"].get("ms_per_step")
@@ -1875,24 +1875,33 @@ def main():
             sc.set_camera(cam)
             sc.set_params(DEPTH, SSS)
             sc.resize_and_clear(W, H)
-            sc.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 1)
+            # warmup: frame by frame until the library has measured this
+            # frame's block costs and switched to its measured lane schedule
+            # (PT_OPT_MIXED_LANES -1; a frame's cost copy lands while the next
+            # one is enqueued, so it takes a few frames), then `warmup` more
+            learn = 0
+            while learn < 60 and sc.mixed_info()[0] != 2:
+                sc.render(0, SPP)
+                sc.synchronize()
+                learn += 1
             for _ in range(max(3, args.warmup)):
                 sc.render(0, SPP)
             sc.synchronize()
-            sc.reset_launch_times()
+            sched = sc.mixed_info()
             t_sc = time.perf_counter()
             for _ in range(args.steps):
                 sc.render(0, SPP)
             sc.synchronize()
             dt_sc = time.perf_counter() - t_sc
-            kt_sc = sc.launch_times_ms()
             single_frame = sc.read_accum()
             single = {"ms_per_step": round(dt_sc / args.steps * 1e3, 4), "steps": args.steps,
                       "value": None if rays_per_frame != rays_per_frame else
                       round(rays_per_frame * args.steps / dt_sc / 1e6, 3),
-                      "kernel_ms": round(float(np.mean(kt_sc)), 4) if kt_sc.size else None,
-                      "basis": "one context, library defaults (no pt_set_option), its own stream; pt_render(0, spp) "
-                               "per frame back to back, synchronized at the end"}
+                      "schedule": {0: "uniform lanes", 1: "static mix", 2: "measured"}.get(sched[0], sched[0]),
+                      "frames_to_measure": learn,
+                      "basis": "one context, library defaults (no pt_set_option), its own stream; "
+                               "pt_render(0, spp) per frame back to back, synchronized at the end, after the frames "
+                               "in which the library measured its lane schedule"}
             sc.close()
             log(f"single context: {single['ms_per_step']} ms per frame")
         except ptamd.PTError as e:
