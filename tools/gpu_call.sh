@@ -16,6 +16,7 @@
 #   single[:K]        tools/single_ctx.py K (default 200): the one-context drop-in frame
 #   emu:N             rank 0 of an emulated N-GPU box run (PT_BENCH_EMULATE_RANKS=N, 200 steps)
 #   profile:WORKLOAD  tools/profile_workload.sh for WORKLOAD (rocprofv3 trace + PMC passes)
+#   rocprof_bench     the driver's command under rocprofv3 --kernel-trace --stats
 #   counters:box      SQ counters of the box render_kernel at the bench's options
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -71,6 +72,10 @@ for step in "$@"; do
     profile:*)
       TAG=$TAG WORKLOAD=${step#profile:} run 1100 "$OUT/profile_${step#profile:}.log" tools/profile_workload.sh
       tail -3 "$OUT/profile_${step#profile:}.log" ;;
+    rocprof_bench)
+      run 900 "$OUT/bench_rocprof.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rocprof_bench" \
+        -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5
+      tail -1 "$OUT/bench_rocprof.log" | cut -c1-300 ;;
     counters:box)
       run 300 "$OUT/box_counters.log" tools/r05_box_counters.sh
       tail -5 "$OUT/box_counters.log" ;;
