@@ -1089,7 +1089,7 @@ def compact_line(full, detail_path=None):
     c = full.get("config", {})
     out["config"] = {k: c[k] for k in ("workload", "parallelism", "kernel_options", "step_loop", "rays_per_frame",
                                        "rays_traced", "msamples_per_s", "rays_traced_per_s_M", "rccl_comm_ranks",
-                                       "partition_slots") if c.get(k) is not None}
+                                       "partition_slots", "lane_schedule") if c.get(k) is not None}
     out["roofline"] = compact_roofline(full.get("roofline"))
     cb = full.get("cpu_baseline")
     if cb:
@@ -1572,6 +1572,7 @@ def main():
     ingest = None   # the emulated root's stand-in for the gather's receive traffic
     nparts = max(world, emu)
     ctxs = [r]   # N = 1: the contexts frames alternate between
+    mixed_learn = []   # frames each N = 1 context took to measure its lane schedule
     box_streams = []   # HipStreams of the N = 1 contexts, closed before the legs
     if dist is None and emu == 1 and not args.packed:
         # args.streams > 1: frames alternate between that many contexts, each
@@ -1612,6 +1613,17 @@ def main():
             x.set_stream(xs.handle)
             x.resize_and_clear(W, H)
             ctxs.append(x)
+        # the library's measured lane schedule (PT_OPT_MIXED_LANES -1: whole
+        # tiles longest first on measured costs), frame by frame until it is
+        # in force on every context; untimed, before the clocks' pre-warm
+        # (which turns culling off and leaves the schedule alone)
+        for c in ctxs:
+            k = 0
+            while k < 60 and c.mixed_info()[0] != 2:
+                c.render(0, SPP)
+                c.synchronize()
+                k += 1
+            mixed_learn.append(k)
         state1 = {"k": 0}
 
         def step():
@@ -1884,6 +1896,13 @@ def main():
                 sc.render(0, SPP)
                 sc.synchronize()
                 learn += 1
+            # then at least 40 ms of frames back to back and `warmup` more: the
+            # frame-by-frame waits above let the GPU's clocks drop
+            t_w = time.perf_counter()
+            while (time.perf_counter() - t_w) < 0.04:
+                for _ in range(8):
+                    sc.render(0, SPP)
+                sc.synchronize()
             for _ in range(max(3, args.warmup)):
                 sc.render(0, SPP)
             sc.synchronize()
@@ -2018,6 +2037,10 @@ def main():
         }
         if traced is not None:
             add_traced(out_line["config"], traced, dt / args.steps)
+        if mixed_learn:
+            out_line["config"]["lane_schedule"] = {0: "uniform lanes", 1: "static mix", 2: "measured"}.get(
+                ctxs[0].mixed_info()[0], "?") if ctxs else None
+            out_line["config"]["frames_to_measure_schedule"] = mixed_learn
         if prof is not None and prof[1].get("sq_per_launch", {}).get("SQ_INSTS_VALU"):
             # the box frame is bound by vector-instruction issue, not HBM (its
             # scene lives in LDS): the primary roofline is VALU

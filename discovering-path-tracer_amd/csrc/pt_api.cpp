@@ -866,7 +866,7 @@ static int compact_items(pt_context* c, ptd::RenderParams* p, const MixPlan* mix
     origins(culled);
     c->live_org_off = c->h_items.size();
     int n_launch = (int)live.size();
-    if (mix && p->spl > 1 && (mix->cost || mix->budget > 0)) {
+    if (mix && (mix->cost || (p->spl > 1 && mix->budget > 0))) {
       std::vector<int> org;
       if (mix->cost)
         measured_origins(*p, pt, live, *mix->cost, &org);
@@ -887,7 +887,7 @@ static int compact_items(pt_context* c, ptd::RenderParams* p, const MixPlan* mix
       PT_HIP(hipMemcpy(c->d_items, c->h_items.data(), c->h_items.size() * sizeof(int), hipMemcpyHostToDevice));
     c->n_live_items = n_launch;
     c->n_culled_items = (int)culled.size();
-    c->items_mixed = mix && p->spl > 1 && (mix->cost || mix->budget > 0);
+    c->items_mixed = mix && (mix->cost || (p->spl > 1 && mix->budget > 0));
     // the lane count each block's workgroups run at (cost feedback)
     c->block_lanes.assign((size_t)p->blocks_total, 0);
     for (size_t k = 0; k + 1 < c->h_items.size() - c->live_org_off; k += 2) {
@@ -1182,7 +1182,9 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     // launches that render into the accumulation buffer
     MixPlan plan;
     bool mixed = false;
-    if (c->opt_mixed != 0 && !wf && lds && c->nranks == 1 && !pack_out && p.spl > 1 && !cnt) {
+    // (one lane per pixel: the measured schedule only orders whole tiles)
+    if (c->opt_mixed != 0 && !wf && lds && c->nranks == 1 && !pack_out && (p.spl > 1 || c->opt_mixed < 0) &&
+        !cnt) {
       mixed = true;
       const size_t lds_b = ptd::scene_lds_bytes(p);
       if (c->render_slots < 0 || c->render_slots_lds != lds_b) {
