@@ -1393,6 +1393,8 @@ def main():
         args.timing_every = 4 if args.streams == 1 else 1
         # the library keeps the last 512 event pairs
         args.timing_every = max(args.timing_every, -(-args.steps // 400))
+    elif args.timing_every > 0:
+        args.timing_every = max(args.timing_every, -(-args.steps // 400))
     DEPTH, SSS = args.depth, args.sss
 
     if args.group_only:
