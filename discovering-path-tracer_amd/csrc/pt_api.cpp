@@ -2835,6 +2835,7 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, 
         if (all[e] != d->streams[s]) PT_HIP(hipStreamWaitEvent(d->streams[s], d->entry[e], 0));
   }
   c->in_dist = true;
+  const bool self_p2p = emulated && getenv("PT_DIST_EMU_P2P") && atoi(getenv("PT_DIST_EMU_P2P")) == 1;
   // frames after the first of each kind (with and without an assembly) reuse
   // its launch parameters: nothing but the output and the assembled frame
   // change within a call (relaunch)
@@ -2875,9 +2876,21 @@ int pt_dist_run(pt_context* c, uint32_t n_batches, int n_frames, int n_streams, 
     if (rc) break;
     PT_HIP(hipEventRecord(d->render_done[b], c->stream));
     PT_HIP(hipStreamWaitEvent(d->comm_stream, d->render_done[b], 0));
-    if (emulated)   // the other ranks' slots: the bytes a real gather would write here
+    if (emulated && self_p2p) {
+      // measurement (PT_DIST_EMU_P2P=1): the other ranks' slots through
+      // RCCL itself -- one grouped self send/recv per emulated rank, the
+      // calls the root's real gather makes -- so the emulated step carries
+      // RCCL's host and device cost per frame
+      PT_NCCL(R->GroupStart());
+      for (int r = 1; r < c->nranks; ++r) {
+        PT_NCCL(R->Send(d->ingest + (size_t)(r - 1) * slot, slot, ncclFloat32, 0, d->comm, d->comm_stream));
+        PT_NCCL(R->Recv(d->recv[b] + (size_t)r * slot, slot, ncclFloat32, 0, d->comm, d->comm_stream));
+      }
+      PT_NCCL(R->GroupEnd());
+    } else if (emulated) {   // the other ranks' slots: the bytes a real gather would write here
       PT_HIP(hipMemcpyAsync(d->recv[b] + slot, d->ingest, (size_t)(c->nranks - 1) * slot * sizeof(float),
                             hipMemcpyDeviceToDevice, d->comm_stream));
+    }
     if (d->nranks > 1) {
       PT_NCCL(R->GroupStart());
       if (d->rank == 0)
