@@ -397,6 +397,13 @@ struct pt_context {
   std::vector<double> block_cost;              // per 16x4 part, at one lane per pixel (averaged)
   int scene_serial = 0;                        // bumped by scene and light uploads
   int last_mix = 0;                            // pt_mixed_info: the last launch's schedule
+  // What the accumulation buffer's culled items hold (render_impl): 0 not
+  // known, 1 finite (+-0 after a clear), 2 (0,0,0,1) in every culled item of
+  // the item layout culled_key in buffer culled_buf.  Only the library's own
+  // calls are assumed to write the buffer.
+  int culled_state = 0;
+  std::vector<float> culled_key;
+  const void* culled_buf = nullptr;
   long long render_slots = -1;                 // resident LDS render workgroups (mixed lanes' budget)
   size_t render_slots_lds = 0;                 // ... at this many bytes of staged scene
   size_t culled_org_off = 0;   // h_items / d_items: where the culled items' first pixels start
@@ -1216,6 +1223,16 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     }
   }
   c->last = p;   // the item exchange (pt_items_*) follows the last rendered frame
+  // Culled items written once (culled_state): a launch whose culled items
+  // already hold (0,0,0,1) in this buffer under this item layout -- a fold of
+  // (0,0,0,1) samples into (0,0,0,1) is (0,0,0,1), whatever the batch --
+  // skips their fill workgroups (23 MB of writes per box 1080p frame).
+  const bool culled_launch = p.n_cull >= 0 && p.items && !pack_out && !c->stats_mode && n_batches > 0;
+  bool culled_skipped = false;
+  if (culled_launch && c->culled_state == 2 && c->culled_buf == c->d_accum && c->culled_key == c->items_key) {
+    p.n_culled_items = 0;
+    culled_skipped = true;
+  }
   c->last_kernel = wf ? 3 : 1;
   c->last_valid = true;
   p.unpack_src = nullptr;
@@ -1223,6 +1240,7 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.unpack_table = nullptr;
   p.n_unpack = 0;
   p.unpack_slot_f4 = 0;
+  if (pack_out && as.frame == (void*)c->d_accum) c->culled_state = 0;   // the assembly writes this buffer
   if (pack_out) {
     frame_key(c, p, &c->key_scratch);
     const std::vector<float>& key = c->key_scratch;
@@ -1348,12 +1366,28 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
     c->timed = true;
   }
   c->launch_n++;
+  // the state of the culled items after this launch (culled_state)
+  if (culled_launch && !culled_skipped) {
+    const bool same = c->culled_state == 2 && c->culled_buf == c->d_accum && c->culled_key == c->items_key;
+    const bool exact = (c->opt_fresh && first_batch == 0) || same ||
+                       (first_batch == 0 && c->culled_state == 1 && c->culled_buf == c->d_accum);
+    c->culled_state = exact ? 2 : 0;
+    c->culled_key = c->items_key;
+    c->culled_buf = c->d_accum;
+  } else if (!culled_launch && !pack_out && n_batches > 0) {
+    c->culled_state = 0;   // every pixel rendered (no culling, stats mode): not tracked
+  }
   return PT_OK;
 }
 
 }  // namespace
 
 int pt_fail_internal(int code, const std::string& msg) { return fail(code, msg); }
+void pt_note_accum_written(pt_context* c, bool finite) {
+  if (!c) return;
+  c->culled_state = finite ? 1 : 0;
+  c->culled_buf = c->d_accum;
+}
 
 extern "C" {
 
@@ -1687,6 +1721,8 @@ int pt_clear_accum(pt_context* c) {
   }
   PT_HIP(ptd::launch_clear(c->d_accum, c->width, c->height, part_of(c, c->rank),
                            c->d_parts + (size_t)c->rank * ptd::kMaxSlots, c->stream));
+  c->culled_state = 1;
+  c->culled_buf = c->d_accum;
   return mark_shared(c);
 }
 
@@ -1720,6 +1756,7 @@ int pt_bind_accum(pt_context* c, void* ptr, int w, int h) {
   c->own_accum = false;
   c->width = w;
   c->height = h;
+  c->culled_state = 0;   // the caller's buffer: its content is not known
   return PT_OK;
 }
 
@@ -2005,6 +2042,7 @@ int pt_tiles_unpack(pt_context* c, const void* src, int src_rank, void* frame) {
   }
   PT_HIP(ptd::launch_tiles(false, (float4*)frame, (float4*)src, c->width, c->height, part_of(c, src_rank),
                            c->d_parts + (size_t)src_rank * ptd::kMaxSlots, c->stream));
+  if (frame == (void*)c->d_accum) c->culled_state = 0;
   return note_use(c);
 }
 
@@ -2058,6 +2096,7 @@ int pt_items_unpack_all(pt_context* c, const void* src, size_t slot_floats, void
   if (rc) return rc;
   PT_HIP(ptd::launch_items_unpack(c->last, (float4*)frame, (const float4*)src, slot_floats / 4, c->d_unpack,
                                   c->n_unpack, c->stream));
+  if (frame == (void*)c->d_accum) c->culled_state = 0;
   return note_use(c);
 }
 

@@ -262,6 +262,7 @@ int setup_frame(pt_group* g, bool arm = true, bool history = true) {
       G_HIP(hipStreamWaitEvent(g->s[(size_t)r], g->start, 0));
       G_HIP(hipMemcpyPeerAsync(pt_accum_device_ptr(c), g->dev[(size_t)r], g->frame, g->dev[0], frame_bytes,
                                g->s[(size_t)r]));
+      pt_note_accum_written(c, false);
     }
     int tiles = 0;
     G_RC(pt_tiles_owned(c, &tiles));
@@ -545,6 +546,8 @@ int clear_accum(pt_group* g) {
   G_HIP(hipSetDevice(g->dev[0]));
   for (int r = 1; r < g->n; ++r) G_HIP(hipStreamWaitEvent(g->s[0], g->done[(size_t)r], 0));
   G_HIP(hipMemsetAsync(g->frame, 0, (size_t)g->W * g->H * 16, g->s[0]));
+  for (int r = 0; r < g->n; ++r)   // the members that render into the frame itself see it cleared
+    if (r == 0 || !g->staged) pt_note_accum_written(g->m[(size_t)r], true);
   if (g->staged)
     for (int r = 1; r < g->n; ++r) G_RC(pt_clear_accum(g->m[(size_t)r]));
   return PT_OK;

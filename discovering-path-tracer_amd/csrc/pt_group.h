@@ -17,6 +17,10 @@ struct pt_group;
 
 // Sets pt_last_error() on the calling thread and returns code (pt_api.cpp).
 int pt_fail_internal(int code, const std::string& msg);
+// The group wrote a member's accumulation buffer itself (a memset, a peer
+// copy): what its culled items hold is no longer what the member last wrote.
+// finite: every pixel is now +-0 (a memset to zero).
+void pt_note_accum_written(pt_context* c, bool finite);
 
 namespace ptg {
 int make(const int* ordinals, int n, pt_group** out);

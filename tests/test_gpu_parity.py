@@ -232,6 +232,54 @@ def test_mixed_lanes_static_budgets(budget, spl, nb, first):
     _assert_same(r.read_accum(), ref, f"mixed budget {budget} spl {spl} nb {nb} first {first}")
 
 
+def test_culled_items_written_once_per_layout():
+    """A launch skips the fill of culled items that already hold (0,0,0,1) in
+    its buffer under the same item layout (render_impl's culled_state): every
+    frame of a sequence that exercises the state -- repeats, a continuation,
+    a camera change and back (the previous camera's live pixels become
+    culled), a clear, a caller buffer full of NaN with and without
+    PT_OPT_FRESH_BATCH0 -- is bitwise the oracle's."""
+    import torch
+    v, i, n = _box()
+    W, H = 333, 250
+    cam2 = scenes.camera((0.6, -0.4, 3.2))
+    r = _setup(v, i, n)
+    r.resize_and_clear(W, H)
+    want1_2, _ = _oracle(v, i, n, W, H, nb=2)
+    want1_5, _ = _oracle(v, i, n, W, H, nb=5)
+    want2_2, _ = _oracle(v, i, n, W, H, nb=2, cam=cam2)
+    r.render(0, 2)
+    _assert_same(r.read_accum(), want1_2, "first frame")
+    r.render(0, 2)
+    _assert_same(r.read_accum(), want1_2, "repeat (fill skipped)")
+    r.render(2, 3)
+    _assert_same(r.read_accum(), want1_5, "continuation")
+    r.set_camera(cam2)
+    r.render(0, 2)
+    _assert_same(r.read_accum(), want2_2, "another camera")
+    r.set_camera(scenes.DEFAULT_CAMERA)
+    r.render(0, 2)
+    _assert_same(r.read_accum(), want1_2, "back to the first camera")
+    r.clear()
+    r.render(0, 2)
+    _assert_same(r.read_accum(), want1_2, "after a clear")
+    nanbuf = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda:0")
+    r.bind_accum(nanbuf.data_ptr(), W, H)
+    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+    for k in range(2):
+        r.render(0, 2)
+        _assert_same(r.read_accum(), want1_2, f"fresh frame {k} over NaN")
+    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 0)
+    r.render(0, 2)
+    _assert_same(r.read_accum(), want1_2, "reference semantics after fresh frames")
+    nanbuf.fill_(float("nan"))   # written behind the library's back: bind again
+    r.bind_accum(nanbuf.data_ptr(), W, H)
+    r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+    r.render(0, 2)
+    _assert_same(r.read_accum(), want1_2, "fresh frame over a re-bound NaN buffer")
+    r.close()
+
+
 def test_partition_sum_is_bit_exact():
     v, i, n = _box()
     W, H, nb = 200, 120, 2
