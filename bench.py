@@ -901,6 +901,136 @@ def group_exchange_record(peer, dt, steps, rays_per_frame, same):
             "unit": "Mrays/s", "verified_bitwise_vs_single_gpu": bool(same)}
 
 
+class IpcFrames:
+    """--collective ipc: the root's frame buffers shared with every rank
+    through HIP IPC (one hipMalloc of `nbuf` W x H float4 frames on the
+    root, its handle broadcast, hipIpcOpenMemHandle elsewhere).  Each rank's
+    contexts bind a buffer as their accumulation buffer and render their own
+    tiles straight into it -- over xGMI on a multi-GPU node, as the one-process
+    group's peer stores do -- so no gather, no assembly and no RCCL call per
+    frame.  Disjoint tiles: the ranks never write the same pixel."""
+
+    def __init__(self, dist, rank, W, H, nbuf, coll_dev):
+        import ctypes
+        import torch
+        self.hip = hip_runtime()
+        self.rank, self.nbuf = rank, nbuf
+        self.frame_bytes = W * H * 16
+        self.ptr = None
+        self.opened = False
+        class IpcHandle(ctypes.Structure):   # hipIpcMemHandle_t: 64 opaque bytes, passed by value to open
+            _fields_ = [("reserved", ctypes.c_ubyte * 64)]
+        err = 0
+        handle = IpcHandle()
+        if rank == 0:
+            p = ctypes.c_void_p()
+            err = self.hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(self.frame_bytes * nbuf))
+            if err == 0:
+                self.ptr = p.value
+                err = self.hip.hipIpcGetMemHandle(ctypes.byref(handle), ctypes.c_void_p(self.ptr))
+        t = torch.tensor([err] + list(handle.reserved), dtype=torch.int32, device=coll_dev)
+        dist.broadcast(t, 0)
+        if int(t[0].item()) != 0:
+            raise RuntimeError(f"hipMalloc / hipIpcGetMemHandle on the root: error {int(t[0].item())}")
+        if rank != 0:
+            h = IpcHandle()
+            h.reserved[:] = [int(x) & 0xff for x in t[1:].tolist()]
+            p = ctypes.c_void_p()
+            # hipIpcMemLazyEnablePeerAccess = 1
+            self.hip.hipIpcOpenMemHandle.argtypes = [ctypes.POINTER(ctypes.c_void_p), IpcHandle, ctypes.c_uint]
+            e = self.hip.hipIpcOpenMemHandle(ctypes.byref(p), h, ctypes.c_uint(1))
+            if e != 0:
+                raise RuntimeError(f"hipIpcOpenMemHandle: error {e}")
+            self.ptr = p.value
+            self.opened = True
+
+    def buffer(self, j):
+        return self.ptr + j * self.frame_bytes
+
+    def read(self, j):
+        """Root: frame buffer j on the host."""
+        import ctypes
+        out = np.empty(self.frame_bytes // 4, np.float32)
+        e = self.hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(self.buffer(j)),
+                               ctypes.c_size_t(self.frame_bytes), ctypes.c_int(2))   # hipMemcpyDeviceToHost
+        if e != 0:
+            raise RuntimeError(f"hipMemcpy: error {e}")
+        return out
+
+    def close(self):
+        import ctypes
+        if self.opened:
+            self.hip.hipIpcCloseMemHandle(ctypes.c_void_p(self.ptr))
+        elif self.rank == 0 and self.ptr:
+            self.hip.hipFree(ctypes.c_void_p(self.ptr))
+        self.ptr = None
+
+
+def setup_ipc(dist, device, world, rank, W, H, spp, v, i, n, int_bits, light, cam, depth, sss, opts, coll_dev,
+              want=None, nbuf=3):
+    """--collective ipc: `nbuf` contexts per rank (own stream each), context j
+    bound to the root's frame buffer j (IpcFrames) with this rank's tiles of a
+    world-way partition; frame k renders on context k % nbuf.  Self-check
+    first: every rank renders one frame per buffer, then the root compares
+    each buffer with `want` (its single-GPU frame) bit for bit.  Every rank
+    returns the same answer: the contexts, or None (the caller then runs the
+    gather), with the reason."""
+    import ptamd
+    import torch
+    ok, why = 1, ""
+    frames = ctxs = None
+    streams = []
+    try:
+        frames = IpcFrames(dist, rank, W, H, nbuf, coll_dev)
+        ctxs = []
+        for j in range(nbuf):
+            x = ptamd.Renderer(device)
+            x.upload_scene(v, i, n, int_bits=int_bits)
+            x.upload_lights(light)
+            x.set_camera(cam)
+            x.set_params(depth, sss)
+            x.set_partition(world, rank)
+            x.set_option(ptamd.PT_OPT_FRESH_BATCH0, 1)
+            x.set_option(ptamd.PT_OPT_LAUNCH_TIMING, 0)
+            for kv in opts:
+                k, _, val = kv.partition("=")
+                x.set_option(int(k), int(val))
+            hs = HipStream(device)
+            streams.append(hs)
+            x.set_stream(hs.handle)
+            x.bind_accum(frames.buffer(j), W, H)
+            ctxs.append(x)
+        for x in ctxs:
+            x.render(0, spp)
+        torch.cuda.synchronize(device)
+    except Exception as e:   # noqa: BLE001 -- every rank must reach the vote below
+        ok, why = 0, f"rank {rank}: {type(e).__name__}: {e}"
+    dist.barrier()   # every rank's frames are complete before the root reads them
+    if ok and rank == 0 and want is not None:
+        for j in range(nbuf):
+            got = frames.read(j).view(np.uint32)
+            if not np.array_equal(got, want.view(np.uint32)):
+                ok, why = 0, f"ipc self-check: buffer {j} differs from the single-GPU frame in " \
+                             f"{int(np.count_nonzero(got != want.view(np.uint32)))} floats"
+                break
+    flag = torch.tensor([ok], dtype=torch.int32, device=coll_dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 0:
+        if why:
+            print(f"bench: ipc exchange unavailable, gathering instead: {why}", file=sys.stderr, flush=True)
+        torch.cuda.synchronize(device)
+        if ctxs:
+            for x in ctxs:
+                x.close()
+        for hs in streams:
+            hs.close()
+        dist.barrier()
+        if frames is not None:
+            frames.close()
+        return None, why or "another rank failed its ipc setup or self-check"
+    return {"frames": frames, "ctxs": ctxs, "streams": streams}, ""
+
+
 def setup_native(r, dist, dev, world, rank, W, H, spp, v, i, n, int_bits, light, cam, depth, sss, coll_dev,
                  n_streams=2):
     """RCCL communicator for pt_dist_run and a 6-frame bitwise self-check on
@@ -1089,7 +1219,8 @@ def compact_line(full, detail_path=None):
     c = full.get("config", {})
     out["config"] = {k: c[k] for k in ("workload", "parallelism", "kernel_options", "step_loop", "rays_per_frame",
                                        "rays_traced", "msamples_per_s", "rays_traced_per_s_M", "rccl_comm_ranks",
-                                       "partition_slots", "lane_schedule") if c.get(k) is not None}
+                                       "partition_slots", "lane_schedule", "exchange_fallback")
+                     if c.get(k) is not None}
     out["roofline"] = compact_roofline(full.get("roofline"))
     cb = full.get("cpu_baseline")
     if cb:
@@ -1332,7 +1463,10 @@ def main():
     ap.add_argument("--spp", type=int, default=8)
     ap.add_argument("--depth", type=int, default=4, help="MAX_DEPTH (reference 4; SURVEY §8d config 4 uses 8)")
     ap.add_argument("--sss", type=int, default=3, help="SSS_MAX_BOUNCES (reference 3)")
-    ap.add_argument("--collective", choices=["gather", "reduce"], default="gather")
+    ap.add_argument("--collective", choices=["gather", "reduce", "ipc"], default="gather",
+                    help="N > 1 frame exchange: sparse RCCL gather of the live items (default), SUM reduce of "
+                         "whole frames, or ipc: every rank renders its tiles straight into the root's frame "
+                         "buffers (HIP IPC), falling back to the gather if its self-check fails")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", type=int, choices=[0, 1], default=None, nargs="?", const=1,
                     help="N>1: compare the assembled frame with a 1-GPU render (default on at N > 1)")
@@ -1575,6 +1709,25 @@ def main():
     nparts = max(world, emu)
     ctxs = [r]   # N = 1: the contexts frames alternate between
     mixed_learn = []   # frames each N = 1 context took to measure its lane schedule
+    ipc, ipc_error = None, None
+    if dist is not None and args.collective == "ipc":
+        # the root's single-GPU frame for the exchange's self-check
+        want_ref = None
+        if rank == 0:
+            ref = ptamd.Renderer(device)
+            ref.upload_scene(v, i, n, int_bits=int_bits)
+            ref.upload_lights(light)
+            ref.set_camera(cam)
+            ref.set_params(DEPTH, SSS)
+            ref.resize_and_clear(W, H)
+            ref.render(0, SPP)
+            want_ref = ref.read_accum().copy()
+            ref.close()
+        log("ipc exchange: setup and self-check")
+        ipc, ipc_error = setup_ipc(dist, device, world, rank, W, H, SPP, v, i, n, int_bits, light, cam, DEPTH, SSS,
+                                   args.opt, dev if backend == "nccl" else "cpu", want=want_ref)
+        if ipc is None:
+            args.collective = "gather"   # equal shares: the root-slot rule is the gather's, not applied here
     box_streams = []   # HipStreams of the N = 1 contexts, closed before the legs
     if dist is None and emu == 1 and not args.packed:
         # args.streams > 1: frames alternate between that many contexts, each
@@ -1631,6 +1784,15 @@ def main():
         def step():
             c = ctxs[state1["k"] % len(ctxs)]
             state1["k"] += 1
+            c.render(0, SPP)
+    elif ipc is not None:
+        # every rank renders its tiles of frame k straight into the root's
+        # frame buffer k % 3 (IpcFrames): nothing to exchange or assemble
+        state_ipc = {"k": 0}
+
+        def step():
+            c = ipc["ctxs"][state_ipc["k"] % len(ipc["ctxs"])]
+            state_ipc["k"] += 1
             c.render(0, SPP)
     elif args.collective == "reduce":
         r.set_option(ptamd.PT_OPT_FRESH_BATCH0, 0)
@@ -1940,14 +2102,17 @@ def main():
         ref.resize_and_clear(W, H)
         ref.render(0, SPP)
         want = ref.read_accum()
-        # --assemble 2 assembles frames into outs[stream]; 0 and 1 into outs[0]
-        frames = (outs if args.assemble == 2 else [out]) if args.collective == "gather" else [frame]
-        if native is None and args.collective == "gather" and args.assemble == 2:
+        if ipc is not None:   # the root's frame buffers, every one holding a whole frame
+            frames = [ipc["frames"].read(j) for j in range(ipc["frames"].nbuf)]
+        else:
+            # --assemble 2 assembles frames into outs[stream]; 0 and 1 into outs[0]
+            frames = (outs if args.assemble == 2 else [out]) if args.collective == "gather" else [frame]
+        if ipc is None and native is None and args.collective == "gather" and args.assemble == 2:
             # the Python step: only the buffers a fused or trailing assembly wrote
             frames = [outs[x] for x in sorted(state["written"])]
             assert frames, "bench --verify: no frame was assembled"
         for f in frames:
-            got = f.cpu().numpy().reshape(-1)
+            got = f.cpu().numpy().reshape(-1) if ipc is None else f
             verified = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
             if not verified:
                 break
@@ -2019,7 +2184,8 @@ def main():
             "config": {"workload": wl, "width": W, "height": H, "spp": SPP, "max_depth": DEPTH,
                        "sss_bounces": SSS,
                        "partition_slots": slots,
-                       "parallelism": (f"tiles{world}-" + ("sparse-gather" if args.collective == "gather" else "reduce"))
+                       "parallelism": (f"tiles{world}-" + ("ipc-peer-stores" if ipc is not None else
+                                                           "sparse-gather" if args.collective == "gather" else "reduce"))
                        if world > 1 else ("single-packed" if args.packed else
                                           f"single, frames alternating over {len(ctxs)} contexts (one stream and "
                                           "accumulation buffer each)" if pipelined else "single"),
@@ -2097,6 +2263,8 @@ def main():
             out_line["group_leg"] = group
         if comm_ranks is not None:
             out_line["config"]["rccl_comm_ranks"] = comm_ranks
+        if ipc_error:
+            out_line["config"]["exchange_fallback"] = ipc_error[:300]
         if world == 1 and emu == 1 and default_cfg and not (args.no_scene_legs or args.profile_run or args.packed):
             torch.cuda.synchronize(dev)
             del r
@@ -2121,6 +2289,17 @@ def main():
             print(oracle_mismatch, file=sys.stderr, flush=True)
     else:
         oracle_mismatch = None
+    if ipc is not None:   # ranks drop their mappings of the root's buffers, then the root frees them
+        torch.cuda.synchronize(dev)
+        for x in ipc["ctxs"]:
+            x.close()
+        for hs in ipc["streams"]:
+            hs.close()
+        if rank != 0:
+            ipc["frames"].close()
+        dist.barrier()
+        if rank == 0:
+            ipc["frames"].close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

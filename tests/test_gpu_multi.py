@@ -67,7 +67,8 @@ def _free_port():
     raise RuntimeError("no free port in 20000-29999")
 
 
-@pytest.mark.parametrize("collective,extra", [("gather", []), ("reduce", []), ("gather", ["--assemble", "0"])])
+@pytest.mark.parametrize("collective,extra", [("gather", []), ("reduce", []), ("gather", ["--assemble", "0"]),
+                                             ("ipc", [])])
 def test_two_rank_bench_verifies_bitwise(collective, extra):
     env = dict(os.environ, PT_BENCH_DEVICE="0", PT_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
@@ -80,6 +81,11 @@ def test_two_rank_bench_verifies_bitwise(collective, extra):
     assert out["n_gpus"] == 2
     assert out["verified_bitwise_vs_single_gpu"] is True
     assert out["config"]["rays_traced"] > 0
+    if collective == "ipc":
+        # the ranks rendered straight into the root's frame buffers (HIP IPC
+        # within the one GPU), no fallback to the gather
+        assert "exchange_fallback" not in out["config"], out["config"]
+        assert out["config"]["parallelism"] == "tiles2-ipc-peer-stores"
 
 
 @pytest.mark.parametrize("streams", [2, 3])
