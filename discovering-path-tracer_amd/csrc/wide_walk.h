@@ -80,6 +80,23 @@ PT_FN float wq_dec(uint32_t w, int j, float s, float p) { return fma_((float)((w
 #define PT_WIDE_LDS_STACK 8
 #endif
 constexpr int kWideLds = PT_WIDE_LDS_STACK;   // stack entries per lane kept in LDS (a ring)
+#ifndef PT_WIDE_PUSH
+#define PT_WIDE_PUSH 1
+#endif
+#ifndef PT_WIDE_POP2
+#define PT_WIDE_POP2 0
+#endif
+// PT_WIDE_QRAW: the leaf queue holds the child ref as the node stores it
+// (~rank), and the flush takes the complement once per tested candidate
+// instead of the walk once per child per step
+#ifndef PT_WIDE_QRAW
+#define PT_WIDE_QRAW 1
+#endif
+#ifndef PT_WIDE_POPWAIT
+#define PT_WIDE_POPWAIT 1
+#endif
+PT_FN int wide_qput(int c) { return PT_WIDE_QRAW ? c : ~c; }
+PT_FN int wide_qrank(int q) { return PT_WIDE_QRAW ? ~q : q; }
 // position of stack entry i in the LDS ring
 PT_FN int wide_ring(int i) { return (kWideLds & (kWideLds - 1)) == 0 ? (i & (kWideLds - 1)) : (i % kWideLds); }
 // hits[] markers: the ray needs the exact threaded walk (wide_ray_ok false,
@@ -174,6 +191,12 @@ PT_FN int2 wide_pop(WideRay& R, const int2* lds, int ls, const int2* ovf, long l
   if (R.sp < R.lo) {
     R.lo = R.sp;
     e = ovf[(long long)R.sp * os];
+#if PT_WIDE_POPWAIT && defined(__HIP_DEVICE_COMPILE__)
+    // wait for the overflow entry here, on this rare path: otherwise the
+    // join after the branch waits for every vector-memory operation of the
+    // wave (vmcnt(0)), stores of hits and evicted entries included, on every pop
+    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0), expcnt and lgkmcnt unconstrained
+#endif
   }
   return e;
 }
@@ -242,7 +265,7 @@ PT_FN bool wide_flush(WideRay& R, const float4* __restrict__ tris, const int* ca
     float4 A[KB], B[KB], C[KB];
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
-      r[k] = cand[(i + k < n ? i + k : i) * 64];
+      r[k] = wide_qrank(cand[(i + k < n ? i + k : i) * 64]);
       const float4* T = tris + 3 * (size_t)r[k];
       A[k] = T[0];
       B[k] = T[1];
@@ -266,11 +289,41 @@ template <bool CNT, bool QUEUE = false, bool QN = false>
 PT_FN bool wide_step(WideRay& R, const float4* __restrict__ nodes, const float4* __restrict__ tris, int2* lds,
                      int ls, int2* ovf, long long os, int stack_cap, bool* exact, uint32_t* cn, uint32_t* cl,
                      int* cand = nullptr, const float4* __restrict__ leaf_box = nullptr) {
+#if PT_WIDE_POP2
+  // PT_WIDE_POP2: the top two entries are read together, so a pop whose entry
+  // is culled goes on to the next one without a second LDS round trip (the
+  // ring slot below the top always exists; an entry below lo is re-read from
+  // the overflow area, as in wide_pop)
+  while (R.cur < 0) {
+    if (R.sp == 0) return true;
+    const unsigned long long w1 = *(const unsigned long long*)&lds[wide_ring(R.sp - 1) * ls];
+    const unsigned long long w2 = *(const unsigned long long*)&lds[wide_ring(R.sp - 2) * ls];
+    --R.sp;
+    int2 e = make_int2((int)(uint32_t)w1, (int)(uint32_t)(w1 >> 32));
+    if (R.sp < R.lo) {
+      R.lo = R.sp;
+      e = ovf[(long long)R.sp * os];
+    }
+    if (!(R.lim < u2f((uint32_t)e.y))) {
+      R.cur = e.x;
+      break;
+    }
+    if (R.sp == 0) return true;
+    --R.sp;
+    e = make_int2((int)(uint32_t)w2, (int)(uint32_t)(w2 >> 32));
+    if (R.sp < R.lo) {
+      R.lo = R.sp;
+      e = ovf[(long long)R.sp * os];
+    }
+    if (!(R.lim < u2f((uint32_t)e.y))) R.cur = e.x;
+  }
+#else
   while (R.cur < 0) {
     if (R.sp == 0) return true;
     const int2 e = wide_pop(R, lds, ls, ovf, os);
     if (!(R.lim < u2f((uint32_t)e.y))) R.cur = e.x;   // still able to hold a winner
   }
+#endif
   float4 lx, hx, ly, hy, lz, hz, cf, kf;
   if (QN) {
     const float4* nd = nodes + (size_t)R.cur * kWideQNodeF4;
@@ -309,13 +362,13 @@ PT_FN bool wide_step(WideRay& R, const float4* __restrict__ nodes, const float4*
   uint32_t lm = (h0 && c0 < 0 ? 1u : 0u) | (h1 && c1 < 0 ? 2u : 0u) | (h2 && c2 < 0 ? 4u : 0u) |
                 (h3 && c3 < 0 ? 8u : 0u);
   if (QUEUE) {   // ... or queue them for the wave-wide flush
-    cand[R.nc * 64] = ~c0;
+    cand[R.nc * 64] = wide_qput(c0);
     R.nc += (lm & 1u) ? 1 : 0;
-    cand[R.nc * 64] = ~c1;
+    cand[R.nc * 64] = wide_qput(c1);
     R.nc += (lm & 2u) ? 1 : 0;
-    cand[R.nc * 64] = ~c2;
+    cand[R.nc * 64] = wide_qput(c2);
     R.nc += (lm & 4u) ? 1 : 0;
-    cand[R.nc * 64] = ~c3;
+    cand[R.nc * 64] = wide_qput(c3);
     R.nc += (lm & 8u) ? 1 : 0;
     lm = 0u;
   }
@@ -343,10 +396,21 @@ PT_FN bool wide_step(WideRay& R, const float4* __restrict__ nodes, const float4*
   // a push loop over the sorted slots measured 3 % slower on configs 3 and 5,
   // profiles/r04j: the same stack order, more select and branch instructions.)
   const bool l0 = live & 1u, l1 = (live >> 1) & 1u, l2 = (live >> 2) & 1u, l3 = (live >> 3) & 1u;
+#if PT_WIDE_PUSH
+  // Six pairwise orders instead of twelve: every t_near is finite here
+  // (wide_ray_ok bounds the origin, the scene and |1/d|, so no slab product
+  // is NaN), hence n_a <= n_b is exactly !(n_b < n_a) -- the same ranks.
+  const bool b10 = n1 < n0, b20 = n2 < n0, b30 = n3 < n0, b21 = n2 < n1, b31 = n3 < n1, b32 = n3 < n2;
+  const int r0 = (l1 && b10) + (l2 && b20) + (l3 && b30);
+  const int r1 = (l0 && !b10) + (l2 && b21) + (l3 && b31);
+  const int r2 = (l0 && !b20) + (l1 && !b21) + (l3 && b32);
+  const int r3 = (l0 && !b30) + (l1 && !b31) + (l2 && !b32);
+#else
   const int r0 = (l1 && n1 < n0) + (l2 && n2 < n0) + (l3 && n3 < n0);
   const int r1 = (l0 && n0 <= n1) + (l2 && n2 < n1) + (l3 && n3 < n1);
   const int r2 = (l0 && n0 <= n2) + (l1 && n1 <= n2) + (l3 && n3 < n2);
   const int r3 = (l0 && n0 <= n3) + (l1 && n1 <= n3) + (l2 && n2 <= n3);
+#endif
   const int n_live = __builtin_popcount(live);
   R.cur = -1;
   if (n_live == 0) return false;
@@ -355,14 +419,25 @@ PT_FN bool wide_step(WideRay& R, const float4* __restrict__ nodes, const float4*
     return true;
   }
   const int top = R.sp + n_live - 1;   // stack entries after the pushes
-  while (top - R.lo > kWideLds) {      // the LDS ring's oldest entries move to the overflow area
+  // PT_WIDE_PUSH 2: the ring keeps one slot free, ring(top), and every child
+  // is written unconditionally -- a pushed one to its rank's slot, the
+  // nearest and the dead ones to the free slot -- with no branch per child
+  constexpr int kRingUse = PT_WIDE_PUSH >= 2 ? kWideLds - 1 : kWideLds;
+  while (top - R.lo > kRingUse) {      // the LDS ring's oldest entries move to the overflow area
     ovf[(long long)R.lo * os] = lds[wide_ring(R.lo) * ls];
     ++R.lo;
   }
-  if (l0 && r0 > 0) lds[wide_ring(top - r0) * ls] = make_int2(c0, (int)f2u(th0));
-  if (l1 && r1 > 0) lds[wide_ring(top - r1) * ls] = make_int2(c1, (int)f2u(th1));
-  if (l2 && r2 > 0) lds[wide_ring(top - r2) * ls] = make_int2(c2, (int)f2u(th2));
-  if (l3 && r3 > 0) lds[wide_ring(top - r3) * ls] = make_int2(c3, (int)f2u(th3));
+  if (PT_WIDE_PUSH >= 2) {
+    lds[wide_ring(l0 && r0 > 0 ? top - r0 : top) * ls] = make_int2(c0, (int)f2u(th0));
+    lds[wide_ring(l1 && r1 > 0 ? top - r1 : top) * ls] = make_int2(c1, (int)f2u(th1));
+    lds[wide_ring(l2 && r2 > 0 ? top - r2 : top) * ls] = make_int2(c2, (int)f2u(th2));
+    lds[wide_ring(l3 && r3 > 0 ? top - r3 : top) * ls] = make_int2(c3, (int)f2u(th3));
+  } else {
+    if (l0 && r0 > 0) lds[wide_ring(top - r0) * ls] = make_int2(c0, (int)f2u(th0));
+    if (l1 && r1 > 0) lds[wide_ring(top - r1) * ls] = make_int2(c1, (int)f2u(th1));
+    if (l2 && r2 > 0) lds[wide_ring(top - r2) * ls] = make_int2(c2, (int)f2u(th2));
+    if (l3 && r3 > 0) lds[wide_ring(top - r3) * ls] = make_int2(c3, (int)f2u(th3));
+  }
   R.sp = top;
   R.cur = (l0 && r0 == 0) ? c0 : (l1 && r1 == 0) ? c1 : (l2 && r2 == 0) ? c2 : c3;
   return false;

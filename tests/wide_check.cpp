@@ -67,7 +67,7 @@ bool flush_lexmin(WideRay& R, const float4* tris, const int* cand, uint32_t* cl,
   bool any = false;
   unsigned long long key = ~0ull;
   for (int i = n - 1; i >= 0; --i) {
-    const int r = cand[i * 64];
+    const int r = wide_qrank(cand[i * 64]);
     const float4* T = tris + 3 * (size_t)r;
     ++*cl;
     float t;

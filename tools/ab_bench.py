@@ -71,9 +71,13 @@ def main():
         r.resize_and_clear(a.w, a.h)
         rs.append((name, r))
     ref = None
+    digest = None
     for name, r in rs:
         r.render(0, a.spp)   # warm + parity between variants
         img = r.read_accum()
+        if digest is None:   # compared across library builds by tools/ab_libs_scenes.sh
+            import hashlib
+            digest = hashlib.sha1(img.tobytes()).hexdigest()[:12]
         if ref is None or a.no_parity:
             ref = img
         elif not np.array_equal(img.view(np.uint32), ref.view(np.uint32)):
@@ -89,7 +93,7 @@ def main():
     for name, r in rs:
         t = r.launch_times_ms()
         out[name] = {"mean_ms": float(t.mean()), "min_ms": float(t.min()), "std_ms": float(t.std())}
-    print(json.dumps({"scene": a.scene, "W": a.w, "H": a.h, "spp": a.spp, "results": out}))
+    print(json.dumps({"scene": a.scene, "W": a.w, "H": a.h, "spp": a.spp, "frame_sha1": digest, "results": out}))
 
 
 if __name__ == "__main__":

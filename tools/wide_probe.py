@@ -19,12 +19,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scene", default="sphere:6")
     ap.add_argument("--spp", type=int, default=8)
+    ap.add_argument("--grid", type=int, default=100, help="PT_OPT_WF_GRID (percent of the traversal grid)")
+    ap.add_argument("--refcam", action="store_true", help="BASELINE's camera (0,0,5), the legs' primary")
     a = ap.parse_args()
     scene, cam = ab_bench.load_scene(a.scene)
     r = ptamd.Renderer(0)
     r.upload(scene)
     r.upload_lights(scenes.REFERENCE_LIGHT)
-    r.set_camera(cam)
+    r.set_camera(scenes.DEFAULT_CAMERA if a.refcam else cam)
+    r.set_option(ptamd.PT_OPT_WF_GRID, a.grid)
     r.set_params(4, 3)
     r.resize_and_clear(1920, 1080)
     r.reset_stats()
@@ -34,7 +37,7 @@ def main():
     walking, idle_more, idle_drain, steps, waiting = (t["closest_walks"], t["shadow_walks"], t["nodes"],
                                                       t["tri_tests"], t["primaries"])
     lanes = 64.0 * max(steps, 1)
-    print(json.dumps({"scene": a.scene, "wave_steps": steps, "walking": walking / lanes,
+    print(json.dumps({"scene": a.scene, "grid": a.grid, "refcam": a.refcam, "wave_steps": steps, "walking": walking / lanes,
                       "idle_rays_left": idle_more / lanes, "idle_drain": idle_drain / lanes,
                       "waiting_on_queue": waiting / lanes}))
 
