@@ -1060,8 +1060,6 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
   p.wide_rank_of = nullptr;
   p.wide_ovf = nullptr;
   p.wide_ovf_lanes = 0;
-  p.wide_carry = nullptr;
-  p.wide_carry_cap = 0;
   p.wide_stack = 0;
   p.wide_handback = 0;
   p.wf_fuse = 0;
@@ -1303,12 +1301,8 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
         { const int rc_ = quiesce(c); if (rc_) return rc_; }
         dev_free(c->d_wide_ovf);
         c->wide_ovf_lanes = 0;
-        // two sets: the two halves of a chunk trace concurrently (launch_wavefront);
-        // then the handed-off walks' records, flags zero (ptd::kWideCarryCap)
-        const size_t ovf_bytes = 2 * (size_t)lanes * (size_t)stack * sizeof(int2);
-        const size_t carry_bytes = (size_t)ptd::kWideCarryCap * 3 * sizeof(float4);
-        PT_HIP(hipMalloc((void**)&c->d_wide_ovf, ovf_bytes + carry_bytes));
-        PT_HIP(hipMemsetAsync((char*)c->d_wide_ovf + ovf_bytes, 0, carry_bytes, c->stream));
+        // two sets: the two halves of a chunk trace concurrently (launch_wavefront)
+        PT_HIP(hipMalloc((void**)&c->d_wide_ovf, 2 * (size_t)lanes * (size_t)stack * sizeof(int2)));
         c->wide_ovf_lanes = lanes;
         c->wide_ovf_stack = stack;
       }
@@ -1322,9 +1316,6 @@ int render_impl(pt_context* c, uint32_t first_batch, uint32_t n_batches, float4*
       p.wide_ovf = c->d_wide_ovf;
       p.wide_ovf_lanes = c->wide_ovf_lanes;
       p.wide_stack = stack;
-      p.wide_carry = (float4*)((char*)c->d_wide_ovf + 2 * (size_t)c->wide_ovf_lanes * (size_t)c->wide_ovf_stack *
-                                                          sizeof(int2));
-      p.wide_carry_cap = ptd::kWideCarryCap;
       p.wide_handback = c->opt_wide == 2 ? 1 : 0;
       // fused shadow walks: hit records carry the rank in 29 bits
       p.wf_fuse = c->opt_wf_fuse && c->n_tris <= ptd::kHitRankMask && c->n_lights > 0 ? 1 : 0;

@@ -92,11 +92,6 @@ struct RenderParams {
   int wf_tail;              // PT_OPT_WF_TAIL: a list of fewer rays than this is finished by wf_tail_kernel (0: never)
   int wf_grid;              // PT_OPT_WF_GRID: the persistent traversal grid in percent of a full-occupancy grid (1-100)
   int wide_refill;          // PT_OPT_WF_REFILL: idle lanes at which a wave of the wide trace kernel refills
-  // walks handed off by sparse waves once the list is exhausted (wide trace
-  // kernel, PT_WIDE_CARRY): wide_carry_cap records of 3 float4, flag word
-  // zero when free; 0 = off
-  float4* wide_carry;
-  int wide_carry_cap;
   const float4* nodes;
   const float4* tris;
   const LightDev* lights;
@@ -208,8 +203,6 @@ constexpr int kRayKindMask = 3, kRayFuse = 4, kRayPrimary = 8;
 // hits[s].y of a fused closest hit: rank | kHitFused | (kHitOccluded if the
 // shadow ray was occluded)
 constexpr int kHitFused = 0x40000000, kHitOccluded = 0x20000000, kHitRankMask = 0x1fffffff;
-// records of handed-off walks per context (RenderParams::wide_carry), 12 MB
-constexpr int kWideCarryCap = 1 << 18;
 constexpr size_t kWfBytesPerPath = 2 * (size_t)kWfStateF4 * 16 + 16 + 2 * (4 + 32) + 8;
 // rays a path may trace in one sample: the primary ray, then per bounce the
 // light shadow rays, sss_bounces x (walk ray + light shadow rays) and the

@@ -2085,7 +2085,6 @@ __device__ __forceinline__ int fused_shadow_ray(const RenderParams& P, v3 o, v3 
   return 2;
 }
 constexpr int kFuseWalk = 16;   // lane state: walking the fused shadow ray
-constexpr int kRestarted = 32;  // lane state (PT_WIDE_CARRY): a deposited walk, restarted (not deposited again)
 
 // PT_WIDE_FLUSH_WAVE: the wave's queued leaf candidates tested one per lane.
 // wide_flush runs a lane's queue in its own lane, so a flush takes as many
@@ -2111,12 +2110,6 @@ constexpr int kRestarted = 32;  // lane state (PT_WIDE_CARRY): a deposited walk,
 #endif
 #ifndef PT_WIDE_OWNER3
 #define PT_WIDE_OWNER3 0
-#endif
-#ifndef PT_WIDE_CARRY
-#define PT_WIDE_CARRY 0
-#endif
-#ifndef PT_WIDE_CARRY_T
-#define PT_WIDE_CARRY_T 16
 #endif
 // Inclusive prefix sum over the wave's 64 lanes (every lane active) by DPP
 // row shifts within each row of 16 and row broadcasts across rows: six VALU
@@ -2243,9 +2236,6 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
   int fz = 0, cr = 0;
   uint32_t aux = 0u;
   Ctr c = {0u, 0u, 0u, 0u, 0u};
-  bool swept = false;   // PT_WIDE_CARRY: this wave has left (counted) and deposits nothing more
-  bool deposited = false;   // PT_WIDE_CARRY: this wave has deposited its walks (once per launch)
-  int claim = -1, claim_n = 0;   // PT_WIDE_CARRY: deposited walks this wave takes
   // A lane whose walk is over (fin, queue empty): its answer goes to the
   // hit list -- or, after a closest hit whose first-light shadow ray the
   // trace kernel walks (PT_OPT_WF_FUSE), that ray starts in the lane.
@@ -2324,128 +2314,6 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
         }
       }
     }
-#if PT_WIDE_CARRY
-    // Drain compaction.  Once the list is exhausted a wave's walks end one by
-    // one and the wave steps on with few lanes (the lane census's "idle in
-    // the drain").  A wave down to PT_WIDE_CARRY_T walking lanes deposits its
-    // walks -- ray, kind, best (t, rank) so far, fused-walk state, list slot
-    // -- after testing its queued candidates, at the end of a shared array.
-    // The wave whose deposit fills position 64 j + 63 owns batch j: it
-    // restarts those 64 walks from the root with their best as the limit.
-    // Other depositors leave.  The last wave to leave (a count of the waves
-    // that left) restarts the final partial batch.  A restarted walk finds
-    // every triangle that could still win or tie (culling only removes boxes
-    // whose triangles cannot; ties keep going to the lower rank), so its
-    // answer is the one the walk would have returned.  A walk is deposited
-    // at most once, and the last wave deposits nothing, so the launch ends.
-    // One atomic per deposit and per wave leaving (a shared claim counter
-    // measured 21M contended CAS retries per frame).
-    // A wave deposits once per launch, so the deposits fit when
-    // wide_carry_cap >= waves x PT_WIDE_CARRY_T (else the hand-off is off).
-    const bool carry = P.wide_carry_cap >= (int)gridDim.x * 4 * PT_WIDE_CARRY_T;
-    if (!more && carry && !swept && !deposited) {
-      const int nw = (int)__popcll(__ballot(p >= 0 && !fin));
-      if (nw > 0 && nw <= PT_WIDE_CARRY_T && __ballot(p >= 0 && (fin || (fz & kRestarted))) == 0ull) {
-        if (FW && __ballot(p >= 0 && R.nc > 0) != 0ull &&
-            wide_flush_wave<CNT, QN>(R, p >= 0, P.wide_tris, cand, fkeys[FW ? wave : 0], lane, &c.leaves,
-                                     P.wide_leafbox)) {
-          fin = true;   // occluded
-          R.sp = 0;
-          R.cur = -1;
-        }
-        const unsigned long long el = __ballot(p >= 0 && !fin);
-        if (el != 0ull && __ballot(p >= 0 && fin) == 0ull) {   // every walk still on: deposit them all
-          const int k = (int)__popcll(el);
-          deposited = true;
-          int base = 0;
-          if (lane == 0) base = atomicAdd(&B.counters[8], k);
-          base = __builtin_amdgcn_readfirstlane(base);
-#ifdef PT_WIDE_CARRY_PROBE
-          if (lane == 0) atomicAdd(&P.stats[4], (unsigned long long)k);
-#endif
-          const int idx = base + (int)__popcll(el & ((1ull << lane) - 1ull));
-          const bool fits = base + k <= P.wide_carry_cap;
-          if (((el >> lane) & 1ull) && idx < P.wide_carry_cap) {
-            // Every word by an atomic exchange, their completion awaited,
-            // then the flag: read-modify-write atomics are performed where
-            // all XCDs see them (a plain load may hit a stale line in the
-            // reader's own L2), with no release fence (which writes back
-            // the whole L2) or acquire (which invalidates it).  A deposit
-            // that does not fit marks its positions as holes and keeps its walks.
-            int* rec = (int*)(P.wide_carry + 3 * (size_t)idx);
-            if (fits) {
-              const int w[11] = {__float_as_int(R.o.x), __float_as_int(R.o.y), __float_as_int(R.o.z),
-                                 __float_as_int(R.lim), __float_as_int(R.d.x), __float_as_int(R.d.y),
-                                 __float_as_int(R.d.z), R.best, R.shadow | (fz << 8), (int)aux, cr};
-#pragma unroll
-              for (int q = 0; q < 11; ++q) atomicExch(rec + q, w[q]);
-              __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0): the record's words are in place
-              atomicExch(rec + 11, p + 1);
-              p = -1;
-              fz = 0;
-            } else {
-              atomicExch(rec + 11, -1);
-            }
-          }
-          // the owner of the batch this deposit completed takes it
-          if (fits && (base + k) / 64 > base / 64) claim = ((base + k) / 64 - 1) * 64, claim_n = 64;
-        }
-      }
-    }
-    if (claim >= 0 || (!more && carry && !swept && __ballot(p >= 0) == 0ull)) {
-      if (claim < 0) {   // this wave leaves; the last one to leave takes the final partial batch
-        int ex = 0, n = 0;
-        if (lane == 0) {
-          ex = atomicAdd(&B.counters[9], 1) + 1;
-          n = min(atomicAdd(&B.counters[8], 0), P.wide_carry_cap);
-        }
-        ex = __builtin_amdgcn_readfirstlane(ex);
-        n = __builtin_amdgcn_readfirstlane(n);
-        swept = true;
-        if (ex < (int)gridDim.x * 4 || n % 64 == 0) break;
-        claim = n / 64 * 64;
-        claim_n = n % 64;
-      }
-      if (lane < claim_n) {
-        int* rec = (int*)(P.wide_carry + 3 * (size_t)(claim + lane));
-        int f = 0;
-        // the depositor stores its records right after reserving them
-        for (int spin = 0; spin < (1 << 20); ++spin) {
-          f = atomicAdd(rec + 11, 0);
-#ifdef PT_WIDE_CARRY_PROBE
-          atomicAdd(&P.stats[7], 1ull);
-#endif
-          if (f != 0) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (f > 0) {   // the words, read after the flag was seen
-          int w[11];
-#pragma unroll
-          for (int q = 0; q < 11; ++q) w[q] = atomicAdd(rec + q, 0);
-          wide_start(R, mk(__int_as_float(w[0]), __int_as_float(w[1]), __int_as_float(w[2])),
-                     mk(__int_as_float(w[4]), __int_as_float(w[5]), __int_as_float(w[6])), (w[8] & 1) != 0,
-                     __int_as_float(w[3]));
-          R.lim = __int_as_float(w[3]);
-          R.best = w[7];
-          fz = (w[8] >> 8) | kRestarted;
-          aux = (uint32_t)w[9];
-          cr = w[10];
-          p = f - 1;
-          fin = false;
-        }
-        if (f != 0) atomicExch(rec + 11, 0);   // free for the next launch
-      }
-#ifdef PT_WIDE_CARRY_PROBE
-      if (lane == 0) {
-        atomicAdd(&P.stats[5], (unsigned long long)claim_n);
-        atomicAdd(&P.stats[8], 1ull);
-      }
-#endif
-      claim = -1;
-      claim_n = 0;
-      if (!swept && __ballot(p >= 0) == 0ull) continue;   // a batch of holes only: leave through the count
-    }
-#endif
     if (!more && __ballot(p >= 0) == 0ull) break;
     for (int it = 0; it < PT_WIDE_STEPS; ++it) {
       bool exact = false;
@@ -2565,11 +2433,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
 #endif
 constexpr int kWfBins = 16;
 __global__ __launch_bounds__(256, PT_WF_SHADE_MIN_BLOCKS) void wf_shade_kernel(RenderParams P, WfBuffers B, int cur) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    B.counters[2] = 0;   // the next traversal's cursor
-    B.counters[8] = 0;   // ... and its handed-off walks (written, claimed)
-    B.counters[9] = 0;
-  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) B.counters[2] = 0;   // the next traversal's cursor
   const int count = B.counters[cur];
   if (count < P.wf_tail) return;   // PT_OPT_WF_TAIL: wf_tail_kernel has finished these paths
   CamFrame F = {};   // camera frame: used by PH_BEGIN only
@@ -3060,8 +2924,6 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
       bh[1].hits = b.hits + sb;
       bh[1].counters = b.counters + 4;
       ph[1].wide_ovf = p.wide_ovf ? p.wide_ovf + (size_t)p.wide_ovf_lanes * (size_t)p.wide_stack : nullptr;
-      ph[0].wide_carry_cap = ph[1].wide_carry_cap = p.wide_carry_cap / 2;   // half the records each
-      ph[1].wide_carry = p.wide_carry ? p.wide_carry + 3 * (size_t)(p.wide_carry_cap / 2) : nullptr;
       e = hipEventRecord(ev_fork, stream);
       if (e == hipSuccess) e = hipStreamWaitEvent(stream2, ev_fork, 0);
       if (e != hipSuccess) return e;
@@ -3069,7 +2931,6 @@ hipError_t launch_wavefront(const RenderParams& p0, const WfBuffers& b, bool lds
     for (int h = 0; h < H; ++h) {
       const long long n = pxn[h] * p.n_batches;
       e = hipMemsetAsync(bh[h].counters, 0, 3 * sizeof(int), sh[h]);
-      if (e == hipSuccess) e = hipMemsetAsync(bh[h].counters + 8, 0, 2 * sizeof(int), sh[h]);   // handed-off walks
       if (e != hipSuccess) return e;
       if (cnt)
         wf_gen_kernel<true><<<(unsigned)((n + 255) / 256), 256, 0, sh[h]>>>(ph[h], bh[h], n, px0[h] * p.n_batches);
