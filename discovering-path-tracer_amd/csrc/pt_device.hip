@@ -2108,13 +2108,8 @@ constexpr int kFuseWalk = 16;   // lane state: walking the fused shadow ray
 #ifndef PT_WIDE_FLUSH_WAVE
 #define PT_WIDE_FLUSH_WAVE 1
 #endif
-// PT_WIDE_FLUSH_LAZY: the flush tests the candidates of the lanes that made
-// it necessary (a queue that cannot take another node's leaves, a finished
-// walk) first and stops after the window that completes them, the last
-// window filled with other lanes' candidates; the rest stay queued.  A
-// partially tested queue keeps its untested tail at its front.
-#ifndef PT_WIDE_FLUSH_LAZY
-#define PT_WIDE_FLUSH_LAZY 0
+#ifndef PT_WIDE_OWNER3
+#define PT_WIDE_OWNER3 0
 #endif
 // Inclusive prefix sum over the wave's 64 lanes (every lane active) by DPP
 // row shifts within each row of 16 and row broadcasts across rows: six VALU
@@ -2129,41 +2124,37 @@ __device__ __forceinline__ int wave_incl_sum(int v) {
   return v;
 }
 template <bool CNT, bool QN>
-__device__ __forceinline__ bool wide_flush_wave(WideRay& R, bool mine, bool prio, const float4* __restrict__ tris, int* cand,
+__device__ __forceinline__ bool wide_flush_wave(WideRay& R, bool mine, const float4* __restrict__ tris, const int* cand,
                                                 unsigned long long* keys, int lane, uint32_t* cl,
                                                 const float4* __restrict__ leaf_box) {
   const int n = mine ? R.nc : 0;
-#if PT_WIDE_FLUSH_LAZY
-  // positions: the prio lanes' candidates [0, tp) in lane order, then the
-  // others'; both inclusive sums (< 2^15) packed in one word for the search
-  const int np = prio ? n : 0;
-  const int ip = wave_incl_sum(np);
-  const int io = wave_incl_sum(n - np);
-  const int tp = __builtin_amdgcn_readlane(ip, 63);
-  const int total = tp + __builtin_amdgcn_readlane(io, 63);
-  const int incl = ip | ((tp + io) << 16);
-  const int off = prio ? ip - np : tp + io - (n - np);
-  const int tested = min(total, max((tp + 63) / 64, 1) * 64);
-#else
   const int incl = wave_incl_sum(n);   // inclusive prefix sum of the queue lengths
   const int total = __builtin_amdgcn_readlane(incl, 63);
   const int off = incl - n;
-  const int tested = total;
-#endif
   keys[lane] = ~0ull;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int* qbase = cand - lane;   // the wave's queue: [k][lane]
-  for (int base = 0; base < tested; base += 64) {
+#if PT_WIDE_OWNER3
+  // the inclusive sums at the ends of the wave's four 16-lane blocks (the
+  // last is `total`): wave-uniform, read once per flush
+  const int e15 = __builtin_amdgcn_readlane(incl, 15), e31 = __builtin_amdgcn_readlane(incl, 31),
+            e47 = __builtin_amdgcn_readlane(incl, 47);
+#endif
+  for (int base = 0; base < total; base += 64) {
     const int target = base + lane;
     int L = 0;   // the owner: lanes whose inclusive sum is <= target
-#if PT_WIDE_FLUSH_LAZY
-    const int sh = target < tp ? 0 : 16;   // the sequence the target lies in
-#pragma unroll
-    for (int s = 32; s >= 1; s >>= 1) {
-      const int v = (__shfl(incl, L + s - 1) >> sh) & 0xffff;
-      if (v <= target) L += s;
+#if PT_WIDE_OWNER3
+    // The same count in two dependent LDS round trips instead of six (the
+    // sums never decrease): whole 16-lane blocks by the uniform block ends,
+    // then whole 4-lane groups inside the block, then lanes inside the group
+    L = (e15 <= target ? 16 : 0) + (e31 <= target ? 16 : 0) + (e47 <= target ? 16 : 0);
+    {
+      const int a0 = __shfl(incl, L + 3), a1 = __shfl(incl, L + 7), a2 = __shfl(incl, L + 11);
+      L += (a0 <= target ? 4 : 0) + (a1 <= target ? 4 : 0) + (a2 <= target ? 4 : 0);
+      const int b0 = __shfl(incl, L), b1 = __shfl(incl, L + 1), b2 = __shfl(incl, L + 2);
+      L += (b0 <= target ? 1 : 0) + (b1 <= target ? 1 : 0) + (b2 <= target ? 1 : 0);
     }
 #else
 #pragma unroll
@@ -2178,7 +2169,7 @@ __device__ __forceinline__ bool wide_flush_wave(WideRay& R, bool mine, bool prio
     const v3 d = mk(__shfl(R.d.x, L), __shfl(R.d.y, L), __shfl(R.d.z, L));
     const float lim = __shfl(R.lim, L);
     const int shadow = __shfl(R.shadow, L);
-    if (target < tested) {
+    if (target < total) {
       const int r = wide_qrank(qbase[(target - offL) * 64 + L]);
       const float4* T = tris + 3 * (size_t)r;
       const float4 A = T[0], B = T[1], C = T[2];
@@ -2197,19 +2188,6 @@ __device__ __forceinline__ bool wide_flush_wave(WideRay& R, bool mine, bool prio
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (n == 0) return false;
-#if PT_WIDE_FLUSH_LAZY
-  const int done = min(max(tested - off, 0), n);   // candidates of this lane tested
-  if (done == 0) return false;
-  const unsigned long long k = keys[lane];
-  if (k != ~0ull && R.shadow) {
-    R.nc = 0;
-    R.best = 1;
-    return true;
-  }
-  for (int i = 0; i < n - done; ++i) cand[i * 64] = cand[(done + i) * 64];   // the untested tail to the front
-  R.nc = n - done;
-  if (k == ~0ull) return false;
-#else
   R.nc = 0;
   const unsigned long long k = keys[lane];
   if (k == ~0ull) return false;
@@ -2217,7 +2195,6 @@ __device__ __forceinline__ bool wide_flush_wave(WideRay& R, bool mine, bool prio
     R.best = 1;
     return true;
   }
-#endif
   const float tm = __uint_as_float((uint32_t)(k >> 32));
   const int rm = (int)(uint32_t)k;
   if (tm < R.lim || (tm == R.lim && R.best >= 0 && rm < R.best)) {   // wide_cand's rule
@@ -2387,7 +2364,7 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
 #endif
         if (__ballot(p >= 0 && R.nc > kWideQ - 4) || (int)__popcll(waiting) >= PT_WIDE_FLUSH_T ||
             (waiting && __ballot(p >= 0 && !fin) == 0ull)) {
-#ifdef PT_WIDE_PROBE_FLUSH   // flush loop use: [4] flushes, [5] sum of candidates, [6] sum of 64-candidate windows, [7] steps
+#ifdef PT_WIDE_PROBE_FLUSH   // flush loop use: [4] flushes, [5] sum of candidates, [6] sum of the largest queue, [7] steps
           {
             int mx = p >= 0 ? R.nc : 0, sm = mx;
 #pragma unroll
@@ -2398,12 +2375,11 @@ __global__ __launch_bounds__(256, PT_WIDE_MIN_BLOCKS) void wf_trace_wide_kernel(
             if (lane == 0) {
               atomicAdd(&P.stats[4], 1ull);
               atomicAdd(&P.stats[5], (unsigned long long)sm);
-              atomicAdd(&P.stats[6], (unsigned long long)(FW ? (sm + 63) / 64 : mx));
+              atomicAdd(&P.stats[6], (unsigned long long)mx);
             }
           }
 #endif
-          if (FW ? wide_flush_wave<CNT, QN>(R, p >= 0, p >= 0 && (fin || R.nc > kWideQ - 4), P.wide_tris, cand,
-                                            fkeys[FW ? wave : 0], lane, &c.leaves,
+          if (FW ? wide_flush_wave<CNT, QN>(R, p >= 0, P.wide_tris, cand, fkeys[FW ? wave : 0], lane, &c.leaves,
                                             P.wide_leafbox)
                  : (p >= 0 && R.nc > 0 &&
                     wide_flush<CNT, QN>(R, P.wide_tris, cand, &c.leaves, P.wide_leafbox))) {
@@ -2696,8 +2672,7 @@ __global__ __launch_bounds__(256, PT_WF_TAIL_MIN_BLOCKS) void wf_tail_kernel(Ren
       const unsigned long long waiting = __ballot(p >= 0 && fin && R.nc > 0);
       if (__ballot(p >= 0 && R.nc > kWideQ - 4) || (int)__popcll(waiting) >= PT_WIDE_FLUSH_T ||
           (waiting && __ballot(p >= 0 && !fin) == 0ull)) {
-        if (PT_WIDE_FLUSH_WAVE ? wide_flush_wave<CNT, QN>(R, p >= 0, p >= 0 && (fin || R.nc > kWideQ - 4), P.wide_tris,
-                                                          cand, fkeys[PT_WIDE_FLUSH_WAVE ? wave : 0],
+        if (PT_WIDE_FLUSH_WAVE ? wide_flush_wave<CNT, QN>(R, p >= 0, P.wide_tris, cand, fkeys[PT_WIDE_FLUSH_WAVE ? wave : 0],
                                                         lane, &c.leaves, P.wide_leafbox)
                                : (p >= 0 && R.nc > 0 && wide_flush<CNT, QN>(R, P.wide_tris, cand, &c.leaves, P.wide_leafbox))) {
           fin = true;   // occluded

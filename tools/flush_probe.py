@@ -2,7 +2,10 @@
 """Flush-loop use of the wide trace kernel (a PT_WIDE_PROBE_FLUSH build,
 loaded with PTAMD_LIB=ab/<name>.so): flushes, candidates per flush, the
 largest queue per flush (the loop's trip count), and walking lanes per step.
-  PTAMD_LIB=ab/fprobe.so python3 tools/flush_probe.py --scene sphere:6"""
+  PTAMD_LIB=ab/fprobe.so python3 tools/flush_probe.py --scene sphere:6
+The windows-per-flush figure needs the probe build of commit 97cc2b3 (its
+counter [6] sums 64-candidate windows; the product source, kept at the
+profiled text, sums each flush's largest queue there)."""
 import argparse
 import json
 import os
