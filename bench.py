@@ -1024,8 +1024,10 @@ def setup_ipc(dist, device, world, rank, W, H, spp, v, i, n, int_bits, light, ca
                 x.close()
         for hs in streams:
             hs.close()
+        if frames is not None and rank != 0:   # mappings dropped before the root frees the buffers
+            frames.close()
         dist.barrier()
-        if frames is not None:
+        if frames is not None and rank == 0:
             frames.close()
         return None, why or "another rank failed its ipc setup or self-check"
     return {"frames": frames, "ctxs": ctxs, "streams": streams}, ""
