@@ -6,7 +6,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export GROUPS_LIST="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES"
-for g in 100 25; do
+for g in ${GRIDS:-100 25}; do
   CAM=reference TAG=${WTAG:-r05w}_g$g AB_ARGS="--scene sphere:6 --reps 1 v:opt20=$g" bash tools/wf_counters.sh > gpurun_out/${WTAG:-r05w}_g${g}.txt 2>&1
   grep wf_trace gpurun_out/${WTAG:-r05w}_g${g}.txt
 done
